@@ -1,0 +1,242 @@
+/*
+ * quill_gpu.h — C-ABI of the MI355X (gfx950) prover hot path for Quill.
+ *
+ * Drop-in boundary for gio54321/quill-zkvm (reference mounted at /root/reference):
+ * every entry point below names the reference item it replaces (file:line).
+ * A Rust shim binds these with `extern "C"` and keeps the
+ * reference's `MultilinearPCS` / `SumcheckProof` / `ZeroCheckProof` surfaces.
+ *
+ * Conventions
+ *  - Field elements (BN254 Fr and Fq) are 4 x uint64 little-endian limbs in
+ *    Montgomery form with R = 2^256: exactly arkworks' in-memory
+ *    `Fp256(BigInt([u64; 4]))`, so a Rust shim passes `&[Fr]` as a pointer
+ *    with no conversion.
+ *  - A G1 point is `uint64_t xy[8]` (x limbs then y limbs, Montgomery) plus an
+ *    infinity flag (`uint8_t`), i.e. ark-ec `Affine<G1Config>` field order.
+ *  - The Fiat-Shamir transcript (transcript/src/transcript.rs:5-74) is carried
+ *    as its 32-byte BLAKE3 chaining state `uint8_t state[32]`, updated in place.
+ *  - Every function returns an int status: 0 = QG_OK, < 0 = error.  Nothing
+ *    unwinds across the ABI; qg_last_error() describes the last failure on a
+ *    context.  The reference prover panics where these return
+ *    QG_ERR_INVALID / QG_ERR_ASSERT (pcs/src/kzg.rs:62-65,85,
+ *    hyperplonk/src/piops/multiset_check.rs:51,63); a Rust shim maps a non-zero
+ *    status to `panic!` to keep those semantics.
+ *  - Calls are synchronous (they may use internal HIP streams).  A context is
+ *    bound to one device; use one context per thread.
+ */
+#ifndef QUILL_GPU_H
+#define QUILL_GPU_H
+
+#include <stddef.h>
+#include <stdint.h>
+
+#ifdef __cplusplus
+extern "C" {
+#endif
+
+#define QG_OK 0
+#define QG_ERR_INVALID (-1)     /* bad argument / size (reference: assert! panic) */
+#define QG_ERR_DEVICE (-2)      /* HIP runtime error */
+#define QG_ERR_OOM (-3)         /* device allocation failed */
+#define QG_ERR_UNSUPPORTED (-4) /* expression / size outside the supported envelope */
+#define QG_ERR_ASSERT (-5)      /* prover-side sanity check failed (reference: assert!) */
+#define QG_ERR_COMM (-6)        /* RCCL failure */
+
+typedef struct qg_ctx qg_ctx;
+typedef struct qg_srs qg_srs;
+typedef struct qg_buf qg_buf;
+
+/* ---------------------------------------------------------------- context */
+/* Device context (one HIP device, its streams and scratch). */
+int qg_ctx_create(int device, qg_ctx** out);
+int qg_ctx_destroy(qg_ctx* ctx);
+const char* qg_last_error(const qg_ctx* ctx);
+/* Library / build identification (e.g. "gfx950"). */
+const char* qg_version(void);
+
+/* Multi-GPU: attach an RCCL communicator (one process per GPU).  `unique_id`
+ * is the 128-byte ncclUniqueId produced by qg_comm_unique_id() on rank 0 and
+ * broadcast by the caller (e.g. torch.distributed).  After this, qg_msm_g1 /
+ * qg_kzg_commit on an SRS *shard* return the sum over all ranks, and
+ * qg_sumcheck_prove treats its tables as the rank's block of the hypercube
+ * (high index bits = rank). */
+int qg_comm_unique_id(uint8_t out_id[128]);
+int qg_ctx_attach_comm(qg_ctx* ctx, int rank, int world, const uint8_t unique_id[128]);
+
+/* ---------------------------------------------------------------- transcript */
+/* Transcript::new(domain)                  transcript/src/transcript.rs:14-22 */
+int qg_transcript_new(const uint8_t* domain, size_t len, uint8_t state[32]);
+/* Transcript::append_bytes(msg)            transcript.rs:25-31 */
+int qg_transcript_append(uint8_t state[32], const uint8_t* msg, size_t len);
+/* Transcript::draw_challenge(n) (n <= 64)  transcript.rs:48-62 */
+int qg_transcript_draw(uint8_t state[32], uint8_t* out, size_t n);
+/* Transcript::draw_field_element::<Fr>()   transcript.rs:70-74 (out: Montgomery) */
+int qg_transcript_draw_fr(uint8_t state[32], uint64_t out_fr[4]);
+/* ark-serialize uncompressed encodings used with append_serializable
+ * (transcript.rs:33-37): Fr -> 32 B canonical LE; G1 -> 64 B (x||y, SW flags). */
+int qg_fr_serialize(const uint64_t fr[4], uint8_t out[32]);
+int qg_g1_serialize(const uint64_t xy[8], uint8_t infinity, uint8_t out[64]);
+
+/* ---------------------------------------------------------------- SRS */
+/* Upload `n` affine bases (KZG::g1_points, pcs/src/kzg.rs:10-23), x||y Montgomery
+ * limbs per point (n x 8 uint64) + per-point infinity flags (may be NULL).
+ * The device keeps the bases affine (this removes the per-commit
+ * `into_affine` of every SRS point, kzg.rs:67-71) together with the MSM's
+ * precomputed window-shifted copies. */
+int qg_srs_upload(qg_ctx* ctx, const uint64_t* affine_xy, const uint8_t* infinity, size_t n,
+                  qg_srs** out);
+/* KZG::trusted_setup with an explicit tau (kzg.rs:35-59): bases [tau^i] g for
+ * i < n, generated on the device.  `g_xy` NULL = the BN254 generator (1, 2). */
+int qg_srs_generate(qg_ctx* ctx, const uint64_t tau[4], const uint64_t* g_xy, size_t n,
+                    qg_srs** out);
+/* Bases [tau^(offset+i)] g for i < n: the shard [offset, offset+n) of a larger
+ * SRS (one shard per rank for the multi-GPU MSM). */
+int qg_srs_generate_range(qg_ctx* ctx, const uint64_t tau[4], const uint64_t* g_xy,
+                          uint64_t offset, size_t n, qg_srs** out);
+int qg_srs_destroy(qg_srs* srs);
+size_t qg_srs_len(const qg_srs* srs);
+/* Copy bases [offset, offset+n) back to the host (affine, Montgomery). */
+int qg_srs_download(const qg_srs* srs, size_t offset, size_t n, uint64_t* affine_xy,
+                    uint8_t* infinity);
+
+/* ---------------------------------------------------------------- device vectors */
+/* Fr vectors resident in HBM (for callers that keep witnesses on the device). */
+int qg_buf_create(qg_ctx* ctx, size_t n, qg_buf** out);
+int qg_buf_destroy(qg_buf* buf);
+size_t qg_buf_len(const qg_buf* buf);
+int qg_buf_upload(qg_buf* buf, const uint64_t* fr, size_t n);
+int qg_buf_download(const qg_buf* buf, uint64_t* fr, size_t n);
+/* Fill with uniform Fr from splitmix64->xoshiro256** keyed by (seed, index
+ * block); used for synthetic benchmark witnesses. */
+int qg_buf_fill_random(qg_buf* buf, uint64_t seed);
+
+/* ---------------------------------------------------------------- MSM / KZG */
+/* E::G1::msm_unchecked(bases, scalars) (pcs/src/kzg.rs:72): sum of
+ * scalars[i] * srs[i] over i < n (n <= qg_srs_len).  Bit-exact: the affine
+ * result is the unique group element. */
+int qg_msm_g1(qg_ctx* ctx, const qg_srs* srs, const uint64_t* scalars, size_t n,
+              uint64_t out_xy[8], uint8_t* out_inf);
+int qg_msm_g1_dev(qg_ctx* ctx, const qg_srs* srs, const qg_buf* scalars, size_t n,
+                  uint64_t out_xy[8], uint8_t* out_inf);
+/* KZG::commit (kzg.rs:61-73): QG_ERR_INVALID when n > max_degree + 1
+ * (reference: assert! at kzg.rs:62-65). */
+int qg_kzg_commit(qg_ctx* ctx, const qg_srs* srs, const uint64_t* poly, size_t n,
+                  uint64_t out_xy[8], uint8_t* out_inf);
+
+/* KZGOpeningProof (kzg.rs:25-32). */
+typedef struct qg_kzg_opening {
+  uint64_t x[4];
+  uint64_t y[4];
+  uint64_t proof_xy[8];
+  uint8_t proof_inf;
+  uint8_t _pad[7];
+} qg_kzg_opening;
+
+/* KZG::open (kzg.rs:75-96): y = p(x), q = (p - y)/(X - x), proof = commit(q). */
+int qg_kzg_open(qg_ctx* ctx, const qg_srs* srs, const uint64_t* poly, size_t n,
+                const uint64_t x[4], qg_kzg_opening* out);
+
+/* ---------------------------------------------------------------- multilinear PCS */
+/* MLEvalProof (pcs/src/mlpcs.rs:32-44) without the point (caller owns it). */
+typedef struct qg_mle_proof {
+  uint64_t evaluation[4];
+  uint64_t s_comm_xy[8];
+  uint8_t s_comm_inf;
+  uint8_t _pad[7];
+  qg_kzg_opening poly_opening;
+  qg_kzg_opening poly_opening_inv;
+  qg_kzg_opening s_opening;
+  qg_kzg_opening s_opening_inv;
+} qg_mle_proof;
+
+/* MultilinearPCS::open == MLEvalProof::prove (mlpcs.rs:83-124, trait impl
+ * :191-198): opens the hypercube evaluations `poly` (len n) at `point`
+ * (nvars Fr).  `state` is the transcript, advanced exactly as the reference
+ * (append point, evaluation, s_comm; draw r). */
+int qg_mle_open(qg_ctx* ctx, const qg_srs* srs, const uint64_t* poly, size_t n,
+                const uint64_t* point, size_t nvars, uint8_t state[32], qg_mle_proof* out);
+
+/* Building blocks of the opening, exposed for testing and for callers that
+ * batch their own protocol:
+ *  compute_pr (mlpcs.rs:68-78) == eq(bin(i), point) table, untrimmed (2^nvars) */
+int qg_eq_table(qg_ctx* ctx, const uint64_t* point, size_t nvars, uint64_t* out);
+/*  InnerProductProof::compute_s_polynomial (pcs/src/ipa.rs:122-157), untrimmed:
+ *  out has max(nf, ng) - 1 entries (caller trims trailing zeros). */
+int qg_s_polynomial(qg_ctx* ctx, const uint64_t* f, size_t nf, const uint64_t* g, size_t ng,
+                    uint64_t* out);
+/*  sum_i f[i] g[i] over min(nf, ng)  (mlpcs.rs:91-94, ipa.rs:66-69) */
+int qg_inner_product(qg_ctx* ctx, const uint64_t* f, size_t nf, const uint64_t* g, size_t ng,
+                     uint64_t out[4]);
+
+/* ---------------------------------------------------------------- sumcheck */
+/* Virtual-polynomial expression (hyperplonk/src/utils/virtual_polynomial.rs:9-18)
+ * in postfix form: INPUT(i) pushes table i, CONST(c) pushes consts[c],
+ * ADD / MUL pop two and push the result.  Sub is ADD(a, MUL(CONST(-1), b)) as
+ * in the reference (:67-77). */
+#define QG_OP_INPUT 0
+#define QG_OP_CONST 1
+#define QG_OP_ADD 2
+#define QG_OP_MUL 3
+typedef struct qg_expr_op {
+  uint32_t op;
+  uint32_t arg;
+} qg_expr_op;
+
+/* SumcheckProof::prove (hyperplonk/src/piops/sumcheck.rs:28-114) for
+ * h(g_0..g_{k-1}) = program.  tables[i] = 2^nvars Fr evaluations of g_i
+ * (host pointers).  Absorbs num_vars and claimed_sum, then per round the
+ * trimmed coefficient-form message; binds index bit 0 first.
+ * Outputs (caller-allocated):
+ *   round_coeffs : nvars * (max_degree+1) * 4 uint64, row j = message j
+ *                  coefficients (trailing zeros trimmed, rest zero-filled)
+ *   round_lens   : nvars uint32, trimmed length of each message
+ *   point        : nvars Fr (the EvaluationClaim point)
+ *   evaluation   : h at the point (EvaluationClaim::evaluation)
+ * `max_degree` = the expression's syntactic degree (qg_expr_degree). */
+int qg_expr_degree(const qg_expr_op* prog, size_t prog_len, uint32_t* out_degree);
+int qg_sumcheck_prove(qg_ctx* ctx, uint32_t nvars, uint32_t ntables,
+                      const uint64_t* const* tables, const qg_expr_op* prog, size_t prog_len,
+                      const uint64_t* consts, size_t nconsts, const uint64_t claimed_sum[4],
+                      uint8_t state[32], uint64_t* round_coeffs, uint32_t* round_lens,
+                      uint64_t* point, uint64_t evaluation[4]);
+/* Same with device-resident tables (the caller's buffers are not modified). */
+int qg_sumcheck_prove_dev(qg_ctx* ctx, uint32_t nvars, uint32_t ntables,
+                          const qg_buf* const* tables, const qg_expr_op* prog, size_t prog_len,
+                          const uint64_t* consts, size_t nconsts, const uint64_t claimed_sum[4],
+                          uint8_t state[32], uint64_t* round_coeffs, uint32_t* round_lens,
+                          uint64_t* point, uint64_t evaluation[4]);
+
+/* ZeroCheckProof::prove (hyperplonk/src/piops/zerocheck.rs:14-49): draws
+ * z (nvars challenges), builds eq(., z) on the device (eq_eval.rs:6-31),
+ * runs the sumcheck of h * eq with claimed sum 0 and returns the zero-check
+ * claim evaluation = sumcheck claim / eq(z, point).  If `eq_out` is not NULL
+ * it receives the eq table (2^nvars Fr) so the caller can mirror the store
+ * mutation of zerocheck.rs:27-29.  Outputs as qg_sumcheck_prove, with
+ * round messages of degree max_degree(h) + 1. */
+int qg_zerocheck_prove(qg_ctx* ctx, uint32_t nvars, uint32_t ntables,
+                       const uint64_t* const* tables, const qg_expr_op* prog, size_t prog_len,
+                       const uint64_t* consts, size_t nconsts, uint8_t state[32],
+                       uint64_t* round_coeffs, uint32_t* round_lens, uint64_t* point,
+                       uint64_t evaluation[4], uint64_t* eq_out);
+int qg_zerocheck_prove_dev(qg_ctx* ctx, uint32_t nvars, uint32_t ntables,
+                           const qg_buf* const* tables, const qg_expr_op* prog, size_t prog_len,
+                           const uint64_t* consts, size_t nconsts, uint8_t state[32],
+                           uint64_t* round_coeffs, uint32_t* round_lens, uint64_t* point,
+                           uint64_t evaluation[4]);
+
+/* ---------------------------------------------------------------- profiling */
+/* Per-kernel device time (ms) of the last call on this context, measured with
+ * HIP events on the stream the kernels run on.  `name` is one of the kernel
+ * group names listed in DESIGN.md (e.g. "msm_accumulate", "sumcheck_round").
+ * Returns total ms and the launch count. */
+int qg_ctx_enable_timing(qg_ctx* ctx, int enable);
+/* Device Fq Montgomery-multiplication throughput (multiplies per second) from
+ * a dependent-chain microbenchmark saturating every CU: the compute roof the
+ * MSM's 11-Fq-mult-per-add cost is priced against. */
+int qg_microbench_fq_mul(qg_ctx* ctx, double* mul_per_s);
+int qg_ctx_kernel_time(const qg_ctx* ctx, const char* name, double* total_ms, uint32_t* launches);
+
+#ifdef __cplusplus
+}
+#endif
+#endif /* QUILL_GPU_H */

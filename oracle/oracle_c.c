@@ -1,0 +1,635 @@
+/*
+ * oracle_c.c — C restatement of the reference's CPU algorithms.
+ * TEST INFRASTRUCTURE ONLY: used by tests/ (checked against the Python oracle)
+ * and by bench.py's cpu_baseline leg.  Never linked into the product.
+ *
+ * Restates (third-party code the reference calls; not vendored in /root/reference):
+ *  - ark-ff 0.5.0 Fp256 Montgomery arithmetic (4 x u64, CIOS), Cargo.lock:56-57
+ *  - ark-ec 0.5.0 short-Weierstrass Jacobian group law (dbl-2009-l,
+ *    add-2007-bl, madd-2007-bl) and VariableBaseMSM::msm_bigint_wnaf:
+ *    c = 3 if n < 32 else ln_without_floats(n) + 2 (log2(n)*69/100),
+ *    signed digits (make_digits, last digit absorbs the carry),
+ *    2^c Jacobian buckets per window, running-sum reduction, window
+ *    doubling — single-threaded exactly like the reference (no rayon in
+ *    Cargo.lock, so cfg_into_iter! is sequential).  Call site pcs/src/kzg.rs:72.
+ *  - KZG::commit as written (pcs/src/kzg.rs:61-73): into_affine of every SRS
+ *    point on every call, then the MSM.
+ *  - sumcheck prover round loop (hyperplonk/src/piops/sumcheck.rs:28-114) in
+ *    evaluation form for h = prod of k tables, with the BLAKE3 transcript
+ *    (transcript/src/transcript.rs) — a lower bound on the reference's
+ *    per-pair DensePolynomial-allocating structure.
+ */
+#include <stdint.h>
+#include <stdlib.h>
+#include <string.h>
+#include <time.h>
+
+typedef unsigned __int128 u128;
+typedef struct { uint64_t v[4]; } fp;
+
+typedef struct {
+  uint64_t p[4];
+  uint64_t inv; /* -p^{-1} mod 2^64 */
+  uint64_t r2[4];
+  uint64_t one[4];
+} modulus;
+
+static const modulus FR = {
+    {0x43e1f593f0000001ull, 0x2833e84879b97091ull, 0xb85045b68181585dull, 0x30644e72e131a029ull},
+    0xc2e1f593efffffffull,
+    {0x1bb8e645ae216da7ull, 0x53fe3ab1e35c59e3ull, 0x8c49833d53bb8085ull, 0x0216d0b17f4e44a5ull},
+    {0xac96341c4ffffffbull, 0x36fc76959f60cd29ull, 0x666ea36f7879462eull, 0x0e0a77c19a07df2full}};
+static const modulus FQ = {
+    {0x3c208c16d87cfd47ull, 0x97816a916871ca8dull, 0xb85045b68181585dull, 0x30644e72e131a029ull},
+    0x87d20782e4866389ull,
+    {0xf32cfc5b538afa89ull, 0xb5e71911d44501fbull, 0x47ab1eff0a417ff6ull, 0x06d89f71cab8351full},
+    {0xd35d438dc58f0d9dull, 0x0a78eb28f5c70b3dull, 0x666ea36f7879462cull, 0x0e0a77c19a07df2full}};
+
+static inline int geq(const uint64_t a[4], const uint64_t b[4]) {
+  for (int i = 3; i >= 0; i--) {
+    if (a[i] != b[i]) return a[i] > b[i];
+  }
+  return 1;
+}
+static inline void sub4(uint64_t r[4], const uint64_t a[4], const uint64_t b[4]) {
+  uint64_t br = 0;
+  for (int i = 0; i < 4; i++) {
+    u128 d = (u128)a[i] - b[i] - br;
+    r[i] = (uint64_t)d;
+    br = (uint64_t)(d >> 127);
+  }
+}
+static inline fp f_add(const modulus* m, fp a, fp b) {
+  fp r;
+  uint64_t c = 0;
+  for (int i = 0; i < 4; i++) {
+    u128 s = (u128)a.v[i] + b.v[i] + c;
+    r.v[i] = (uint64_t)s;
+    c = (uint64_t)(s >> 64);
+  }
+  if (geq(r.v, m->p)) sub4(r.v, r.v, m->p);
+  return r;
+}
+static inline fp f_sub(const modulus* m, fp a, fp b) {
+  fp r;
+  if (geq(a.v, b.v)) {
+    sub4(r.v, a.v, b.v);
+  } else {
+    uint64_t t[4];
+    sub4(t, m->p, b.v);
+    uint64_t c = 0;
+    for (int i = 0; i < 4; i++) {
+      u128 s = (u128)a.v[i] + t[i] + c;
+      r.v[i] = (uint64_t)s;
+      c = (uint64_t)(s >> 64);
+    }
+  }
+  return r;
+}
+/* CIOS Montgomery multiplication (ark-ff "no-carry" path applies: top limb < 2^63-1) */
+static inline fp f_mul(const modulus* m, fp a, fp b) {
+  uint64_t t[4] = {0, 0, 0, 0};
+  for (int i = 0; i < 4; i++) {
+    u128 A = (u128)a.v[0] * b.v[i] + t[0];
+    uint64_t t0 = (uint64_t)A;
+    uint64_t k = t0 * m->inv;
+    u128 C = (u128)k * m->p[0] + t0;
+    for (int j = 1; j < 4; j++) {
+      A = (u128)a.v[j] * b.v[i] + t[j] + (uint64_t)(A >> 64);
+      C = (u128)k * m->p[j] + (uint64_t)A + (uint64_t)(C >> 64);
+      t[j - 1] = (uint64_t)C;
+    }
+    t[3] = (uint64_t)(C >> 64) + (uint64_t)(A >> 64);
+  }
+  fp r = {{t[0], t[1], t[2], t[3]}};
+  if (geq(r.v, m->p)) sub4(r.v, r.v, m->p);
+  return r;
+}
+static inline int f_is_zero(fp a) { return !(a.v[0] | a.v[1] | a.v[2] | a.v[3]); }
+static inline int f_eq(fp a, fp b) { return !memcmp(&a, &b, sizeof(fp)); }
+static inline fp f_one(const modulus* m) {
+  fp r;
+  memcpy(r.v, m->one, 32);
+  return r;
+}
+static fp f_inv(const modulus* m, fp a) {
+  uint64_t e[4];
+  memcpy(e, m->p, 32);
+  e[0] -= 2;
+  fp r = f_one(m);
+  for (int i = 3; i >= 0; i--)
+    for (int b = 63; b >= 0; b--) {
+      r = f_mul(m, r, r);
+      if ((e[i] >> b) & 1) r = f_mul(m, r, a);
+    }
+  return r;
+}
+static inline fp f_from_mont(const modulus* m, fp a) {
+  fp one = {{1, 0, 0, 0}};
+  return f_mul(m, a, one);
+}
+static inline fp f_to_mont(const modulus* m, fp a) {
+  fp r2;
+  memcpy(r2.v, m->r2, 32);
+  return f_mul(m, a, r2);
+}
+
+/* ---------------------------------------------------------------- G1 */
+typedef struct { fp x, y; int inf; } g1a;
+typedef struct { fp x, y, z; } g1j; /* z = 0 -> infinity */
+
+static inline int j_is_inf(const g1j* p) { return f_is_zero(p->z); }
+static g1j j_zero(void) {
+  g1j r;
+  memset(&r, 0, sizeof r);
+  r.y = f_one(&FQ);
+  return r;
+}
+/* dbl-2009-l (a = 0) */
+static void j_double(g1j* p) {
+  if (j_is_inf(p)) return;
+  const modulus* m = &FQ;
+  fp A = f_mul(m, p->x, p->x), B = f_mul(m, p->y, p->y), C = f_mul(m, B, B);
+  fp t = f_add(m, p->x, B);
+  fp D = f_sub(m, f_sub(m, f_mul(m, t, t), A), C);
+  D = f_add(m, D, D);
+  fp E = f_add(m, f_add(m, A, A), A);
+  fp F = f_mul(m, E, E);
+  fp X3 = f_sub(m, F, f_add(m, D, D));
+  fp C8 = f_add(m, C, C);
+  C8 = f_add(m, C8, C8);
+  C8 = f_add(m, C8, C8);
+  fp Y3 = f_sub(m, f_mul(m, E, f_sub(m, D, X3)), C8);
+  fp Z3 = f_mul(m, p->y, p->z);
+  Z3 = f_add(m, Z3, Z3);
+  p->x = X3;
+  p->y = Y3;
+  p->z = Z3;
+}
+/* madd-2007-bl: p += q (affine) */
+static void j_add_affine(g1j* p, const g1a* q) {
+  if (q->inf) return;
+  const modulus* m = &FQ;
+  if (j_is_inf(p)) {
+    p->x = q->x;
+    p->y = q->y;
+    p->z = f_one(m);
+    return;
+  }
+  fp Z1Z1 = f_mul(m, p->z, p->z);
+  fp U2 = f_mul(m, q->x, Z1Z1);
+  fp S2 = f_mul(m, f_mul(m, q->y, p->z), Z1Z1);
+  if (f_eq(p->x, U2)) {
+    if (f_eq(p->y, S2)) {
+      j_double(p);
+    } else {
+      *p = j_zero();
+    }
+    return;
+  }
+  fp H = f_sub(m, U2, p->x);
+  fp HH = f_mul(m, H, H);
+  fp I = f_add(m, HH, HH);
+  I = f_add(m, I, I);
+  fp J = f_mul(m, H, I);
+  fp r = f_sub(m, S2, p->y);
+  r = f_add(m, r, r);
+  fp V = f_mul(m, p->x, I);
+  fp X3 = f_sub(m, f_sub(m, f_mul(m, r, r), J), f_add(m, V, V));
+  fp Y1J = f_mul(m, p->y, J);
+  fp Y3 = f_sub(m, f_mul(m, r, f_sub(m, V, X3)), f_add(m, Y1J, Y1J));
+  fp t = f_add(m, p->z, H);
+  fp Z3 = f_sub(m, f_sub(m, f_mul(m, t, t), Z1Z1), HH);
+  p->x = X3;
+  p->y = Y3;
+  p->z = Z3;
+}
+/* add-2007-bl: p += q (Jacobian) */
+static void j_add(g1j* p, const g1j* q) {
+  if (j_is_inf(q)) return;
+  if (j_is_inf(p)) {
+    *p = *q;
+    return;
+  }
+  const modulus* m = &FQ;
+  fp Z1Z1 = f_mul(m, p->z, p->z), Z2Z2 = f_mul(m, q->z, q->z);
+  fp U1 = f_mul(m, p->x, Z2Z2), U2 = f_mul(m, q->x, Z1Z1);
+  fp S1 = f_mul(m, f_mul(m, p->y, q->z), Z2Z2);
+  fp S2 = f_mul(m, f_mul(m, q->y, p->z), Z1Z1);
+  if (f_eq(U1, U2)) {
+    if (f_eq(S1, S2)) {
+      j_double(p);
+    } else {
+      *p = j_zero();
+    }
+    return;
+  }
+  fp H = f_sub(m, U2, U1);
+  fp I = f_add(m, H, H);
+  I = f_mul(m, I, I);
+  fp J = f_mul(m, H, I);
+  fp r = f_sub(m, S2, S1);
+  r = f_add(m, r, r);
+  fp V = f_mul(m, U1, I);
+  fp X3 = f_sub(m, f_sub(m, f_mul(m, r, r), J), f_add(m, V, V));
+  fp S1J = f_mul(m, S1, J);
+  fp Y3 = f_sub(m, f_mul(m, r, f_sub(m, V, X3)), f_add(m, S1J, S1J));
+  fp t = f_add(m, p->z, q->z);
+  fp Z3 = f_mul(m, f_sub(m, f_sub(m, f_mul(m, t, t), Z1Z1), Z2Z2), H);
+  p->x = X3;
+  p->y = Y3;
+  p->z = Z3;
+}
+static g1a j_to_affine(const g1j* p) {
+  g1a r;
+  memset(&r, 0, sizeof r);
+  if (j_is_inf(p)) {
+    r.inf = 1;
+    return r;
+  }
+  const modulus* m = &FQ;
+  fp zi = f_inv(m, p->z), zi2 = f_mul(m, zi, zi);
+  r.x = f_mul(m, p->x, zi2);
+  r.y = f_mul(m, p->y, f_mul(m, zi2, zi));
+  return r;
+}
+
+/* ---------------------------------------------------------------- ark MSM */
+static size_t ln_without_floats(size_t a) { /* log2(a) * 69 / 100 */
+  size_t l = 0;
+  while (((size_t)1 << (l + 1)) <= a) l++;
+  return l * 69 / 100;
+}
+
+/* signed digits of a canonical 254-bit scalar (ark-ec make_digits) */
+static void make_digits(const uint64_t s[4], int w, int num_bits, int64_t* out) {
+  const uint64_t radix = 1ull << w, mask = radix - 1;
+  uint64_t carry = 0;
+  const int count = (num_bits + w - 1) / w;
+  for (int i = 0; i < count; i++) {
+    int bit_offset = i * w, u64_idx = bit_offset / 64, bit_idx = bit_offset % 64;
+    uint64_t buf;
+    if (bit_idx < 64 - w || u64_idx == 3) buf = s[u64_idx] >> bit_idx;
+    else buf = (s[u64_idx] >> bit_idx) | (s[u64_idx + 1] << (64 - bit_idx));
+    uint64_t coef = carry + (buf & mask);
+    carry = (coef + radix / 2) >> w;
+    int64_t digit = (int64_t)coef - (int64_t)(carry << w);
+    if (i == count - 1) digit += (int64_t)(carry << w);
+    out[i] = digit;
+  }
+}
+
+/* scalars: Montgomery Fr (4 x u64 each); bases affine */
+static g1j msm_ark(const g1a* bases, const fp* scalars, size_t n) {
+  const int c = n < 32 ? 3 : (int)ln_without_floats(n) + 2;
+  const int num_bits = 254;
+  const int digits = (num_bits + c - 1) / c;
+  int64_t* dig = (int64_t*)malloc(sizeof(int64_t) * digits * (n ? n : 1));
+  for (size_t i = 0; i < n; i++) {
+    fp cs = f_from_mont(&FR, scalars[i]);
+    make_digits(cs.v, c, num_bits, dig + i * digits);
+  }
+  g1j* buckets = (g1j*)malloc(sizeof(g1j) << c);
+  g1j* win = (g1j*)malloc(sizeof(g1j) * digits);
+  for (int w = 0; w < digits; w++) {
+    for (size_t b = 0; b < ((size_t)1 << c); b++) buckets[b] = j_zero();
+    for (size_t i = 0; i < n; i++) {
+      int64_t d = dig[i * digits + w];
+      if (d > 0) {
+        j_add_affine(&buckets[d - 1], &bases[i]);
+      } else if (d < 0) {
+        g1a nb = bases[i];
+        if (!nb.inf) nb.y = f_sub(&FQ, (fp){{0, 0, 0, 0}}, nb.y);
+        j_add_affine(&buckets[-d - 1], &nb);
+      }
+    }
+    g1j run = j_zero(), res = j_zero();
+    for (size_t b = ((size_t)1 << c); b-- > 0;) {
+      j_add(&run, &buckets[b]);
+      j_add(&res, &run);
+    }
+    win[w] = res;
+  }
+  g1j total = j_zero();
+  for (int w = digits - 1; w >= 1; w--) {
+    j_add(&total, &win[w]);
+    for (int k = 0; k < c; k++) j_double(&total);
+  }
+  j_add(&total, &win[0]);
+  free(dig);
+  free(buckets);
+  free(win);
+  return total;
+}
+
+static double now_s(void) {
+  struct timespec ts;
+  clock_gettime(CLOCK_MONOTONIC, &ts);
+  return ts.tv_sec + ts.tv_nsec * 1e-9;
+}
+
+/* ---------------------------------------------------------------- exported */
+/* out_xy: affine Montgomery (8 u64) + inf flag.  bases: n x 8 u64 (+ inf flags) */
+int oc_msm(const uint64_t* bases_xy, const uint8_t* inf, const uint64_t* scalars, size_t n,
+           uint64_t out_xy[8], uint8_t* out_inf) {
+  g1a* b = (g1a*)malloc(sizeof(g1a) * (n ? n : 1));
+  for (size_t i = 0; i < n; i++) {
+    memcpy(b[i].x.v, bases_xy + 8 * i, 32);
+    memcpy(b[i].y.v, bases_xy + 8 * i + 4, 32);
+    b[i].inf = inf ? inf[i] : 0;
+  }
+  g1j r = msm_ark(b, (const fp*)scalars, n);
+  g1a a = j_to_affine(&r);
+  memcpy(out_xy, a.x.v, 32);
+  memcpy(out_xy + 4, a.y.v, 32);
+  *out_inf = (uint8_t)a.inf;
+  free(b);
+  return 0;
+}
+
+/* [tau^i] g for i < n via a 32 x 256 fixed-base comb on g (bases for the baseline) */
+static void gen_srs(fp tau_mont, size_t n, g1a* out) {
+  const modulus* m = &FQ;
+  g1a g;
+  memset(&g, 0, sizeof g);
+  fp one = {{1, 0, 0, 0}}, two = {{2, 0, 0, 0}};
+  g.x = f_to_mont(m, one);
+  g.y = f_to_mont(m, two);
+  g1a* tbl = (g1a*)malloc(sizeof(g1a) * 32 * 256);
+  g1j base;
+  base.x = g.x;
+  base.y = g.y;
+  base.z = f_one(m);
+  for (int k = 0; k < 32; k++) {
+    g1j acc = j_zero();
+    for (int j = 0; j < 256; j++) {
+      tbl[k * 256 + j] = j_to_affine(&acc);
+      j_add(&acc, &base);
+    }
+    for (int d = 0; d < 8; d++) j_double(&base);
+  }
+  fp t = f_one(&FR);
+  for (size_t i = 0; i < n; i++) {
+    fp c = f_from_mont(&FR, t);
+    g1j acc = j_zero();
+    for (int k = 0; k < 32; k++) {
+      unsigned byte = (unsigned)((c.v[k / 8] >> (8 * (k % 8))) & 255);
+      if (byte) j_add_affine(&acc, &tbl[k * 256 + byte]);
+    }
+    out[i] = j_to_affine(&acc);
+    t = f_mul(&FR, t, tau_mont);
+  }
+  free(tbl);
+}
+
+static uint64_t sm_state;
+static uint64_t splitmix(void) {
+  uint64_t z = (sm_state += 0x9E3779B97F4A7C15ull);
+  z = (z ^ (z >> 30)) * 0xBF58476D1CE4E5B9ull;
+  z = (z ^ (z >> 27)) * 0x94D049BB133111EBull;
+  return z ^ (z >> 31);
+}
+static fp rand_fr(void) {
+  for (;;) {
+    fp v;
+    for (int i = 0; i < 4; i++) v.v[i] = splitmix();
+    v.v[3] &= (1ull << 62) - 1;
+    if (!geq(v.v, FR.p)) return f_to_mont(&FR, v);
+  }
+}
+
+/*
+ * Timed baseline on a sample of n = 2^log_n scalars (single thread):
+ *   t_msm    : msm_unchecked only (bases already affine)
+ *   t_commit : KZG::commit as written = into_affine of all SRS points + MSM
+ * Returns 0; writes seconds.
+ */
+int oc_bench_msm(int log_n, uint64_t seed, double* t_msm, double* t_commit, uint64_t out_xy[8]) {
+  size_t n = (size_t)1 << log_n;
+  sm_state = seed;
+  g1a* bases = (g1a*)malloc(sizeof(g1a) * n);
+  fp* sc = (fp*)malloc(sizeof(fp) * n);
+  fp tau = rand_fr();
+  gen_srs(tau, n, bases);
+  for (size_t i = 0; i < n; i++) sc[i] = rand_fr();
+  /* KZG keeps g1_points in projective form (kzg.rs:20); convert on each commit */
+  g1j* proj = (g1j*)malloc(sizeof(g1j) * n);
+  for (size_t i = 0; i < n; i++) {
+    proj[i].x = bases[i].x;
+    proj[i].y = bases[i].y;
+    proj[i].z = f_one(&FQ);
+    /* scale Z so the projective representation is non-trivial, like a computed SRS */
+    fp z = f_add(&FQ, f_one(&FQ), f_one(&FQ));
+    fp z2 = f_mul(&FQ, z, z);
+    proj[i].x = f_mul(&FQ, proj[i].x, z2);
+    proj[i].y = f_mul(&FQ, proj[i].y, f_mul(&FQ, z2, z));
+    proj[i].z = z;
+  }
+  double a = now_s();
+  g1j r = msm_ark(bases, sc, n);
+  double b = now_s();
+  g1a* conv = (g1a*)malloc(sizeof(g1a) * n);
+  for (size_t i = 0; i < n; i++) conv[i] = j_to_affine(&proj[i]);
+  double c = now_s();
+  *t_msm = b - a;
+  *t_commit = (c - b) + (b - a);
+  g1a ra = j_to_affine(&r);
+  memcpy(out_xy, ra.x.v, 32);
+  memcpy(out_xy + 4, ra.y.v, 32);
+  free(bases);
+  free(sc);
+  free(proj);
+  free(conv);
+  return 0;
+}
+
+/* ---------------------------------------------------------------- BLAKE3 + sumcheck */
+static const uint32_t B3IV[8] = {0x6A09E667u, 0xBB67AE85u, 0x3C6EF372u, 0xA54FF53Au,
+                                 0x510E527Fu, 0x9B05688Cu, 0x1F83D9ABu, 0x5BE0CD19u};
+static const int B3P[16] = {2, 6, 3, 10, 7, 0, 4, 13, 1, 11, 12, 5, 9, 14, 15, 8};
+#define ROTR(x, n) (((x) >> (n)) | ((x) << (32 - (n))))
+static void b3g(uint32_t* s, int a, int b, int c, int d, uint32_t x, uint32_t y) {
+  s[a] += s[b] + x; s[d] = ROTR(s[d] ^ s[a], 16); s[c] += s[d]; s[b] = ROTR(s[b] ^ s[c], 12);
+  s[a] += s[b] + y; s[d] = ROTR(s[d] ^ s[a], 8);  s[c] += s[d]; s[b] = ROTR(s[b] ^ s[c], 7);
+}
+static void b3c(const uint32_t cv[8], const uint32_t blk[16], uint64_t ctr, uint32_t len,
+                uint32_t flags, uint32_t out[16]) {
+  uint32_t s[16], m[16], t[16];
+  for (int i = 0; i < 8; i++) s[i] = cv[i];
+  for (int i = 0; i < 4; i++) s[8 + i] = B3IV[i];
+  s[12] = (uint32_t)ctr; s[13] = (uint32_t)(ctr >> 32); s[14] = len; s[15] = flags;
+  memcpy(m, blk, 64);
+  for (int r = 0; r < 7; r++) {
+    b3g(s, 0, 4, 8, 12, m[0], m[1]); b3g(s, 1, 5, 9, 13, m[2], m[3]);
+    b3g(s, 2, 6, 10, 14, m[4], m[5]); b3g(s, 3, 7, 11, 15, m[6], m[7]);
+    b3g(s, 0, 5, 10, 15, m[8], m[9]); b3g(s, 1, 6, 11, 12, m[10], m[11]);
+    b3g(s, 2, 7, 8, 13, m[12], m[13]); b3g(s, 3, 4, 9, 14, m[14], m[15]);
+    for (int i = 0; i < 16; i++) t[i] = m[B3P[i]];
+    memcpy(m, t, 64);
+  }
+  for (int i = 0; i < 8; i++) { out[i] = s[i] ^ s[i + 8]; out[i + 8] = s[i + 8] ^ cv[i]; }
+}
+/* single-chunk BLAKE3 XOF (inputs < 1024 bytes: all sumcheck transcript messages) */
+static void b3_small(const uint8_t* in, size_t len, uint8_t* out, size_t olen) {
+  uint32_t cv[8], blk[16], o[16];
+  memcpy(cv, B3IV, 32);
+  size_t nblk = len ? (len + 63) / 64 : 1;
+  for (size_t b = 0; b < nblk; b++) {
+    uint8_t buf[64] = {0};
+    size_t take = len - b * 64 < 64 ? len - b * 64 : 64;
+    if (len) memcpy(buf, in + b * 64, take);
+    for (int i = 0; i < 16; i++)
+      blk[i] = buf[4*i] | (buf[4*i+1] << 8) | (buf[4*i+2] << 16) | ((uint32_t)buf[4*i+3] << 24);
+    uint32_t flags = (b == 0 ? 1 : 0) | (b == nblk - 1 ? 2 : 0);
+    if (b == nblk - 1) {
+      size_t pos = 0;
+      for (uint64_t ctr = 0; pos < olen; ctr++) {
+        b3c(cv, blk, ctr, (uint32_t)(len ? take : 0), flags | 8, o);
+        for (int i = 0; i < 64 && pos < olen; i++) out[pos++] = (uint8_t)(o[i / 4] >> (8 * (i % 4)));
+      }
+    } else {
+      b3c(cv, blk, 0, 64, flags, o);
+      memcpy(cv, o, 32);
+    }
+  }
+}
+static void tr_append(uint8_t st[32], const uint8_t* msg, size_t len) {
+  uint8_t buf[1024];
+  memcpy(buf, st, 32);
+  memcpy(buf + 32, msg, len);
+  b3_small(buf, 32 + len, st, 32);
+}
+static fp tr_draw_fr(uint8_t st[32]) {
+  uint8_t buf[41], ch[48];
+  memcpy(buf, st, 32);
+  memcpy(buf + 32, "challenge", 9);
+  b3_small(buf, 41, ch, 48);
+  tr_append(st, ch, 48);
+  fp lo, hi = {{0, 0, 0, 0}};
+  memcpy(lo.v, ch, 32);
+  memcpy(hi.v, ch + 32, 16);
+  fp r2, r3;
+  memcpy(r2.v, FR.r2, 32);
+  r3 = f_mul(&FR, r2, r2); /* R^2*R^2/R = R^3 */
+  return f_add(&FR, f_mul(&FR, lo, r2), f_mul(&FR, hi, r3));
+}
+static void fr_bytes(fp x, uint8_t* out) {
+  fp c = f_from_mont(&FR, x);
+  memcpy(out, c.v, 32);
+}
+
+/*
+ * Sumcheck prover for h = prod_{i<k} g_i, tables Montgomery (k x 2^nvars),
+ * transcript state in/out.  Writes round coefficients (nvars x (k+1), trimmed
+ * lengths in lens) and the point.  Tables are copied (the reference clones).
+ */
+int oc_sumcheck_prod(int nvars, int k, const uint64_t* tables, const uint64_t claimed[4],
+                     uint8_t state[32], uint64_t* coeffs, uint32_t* lens, uint64_t* point,
+                     uint64_t evaluation[4]) {
+  size_t N = (size_t)1 << nvars;
+  fp* g = (fp*)malloc(sizeof(fp) * N * k);
+  memcpy(g, tables, sizeof(fp) * N * k);
+  uint8_t m8[8];
+  for (int i = 0; i < 8; i++) m8[i] = (uint8_t)((uint64_t)nvars >> (8 * i));
+  tr_append(state, m8, 8);
+  uint8_t b32[32];
+  fp cs;
+  memcpy(cs.v, claimed, 32);
+  fr_bytes(cs, b32);
+  tr_append(state, b32, 32);
+  const int np = k + 1;
+  /* inverse Vandermonde on 0..k */
+  fp V[16][16];
+  for (int j = 0; j < np; j++) {
+    fp poly[17] = {{{0}}};
+    poly[0] = f_one(&FR);
+    int deg = 0;
+    fp den = f_one(&FR);
+    for (int mm = 0; mm < np; mm++) {
+      if (mm == j) continue;
+      fp nm = {{(uint64_t)mm, 0, 0, 0}};
+      nm = f_sub(&FR, (fp){{0, 0, 0, 0}}, f_to_mont(&FR, nm));
+      fp np2[17] = {{{0}}};
+      for (int t = 0; t <= deg; t++) {
+        np2[t] = f_add(&FR, np2[t], f_mul(&FR, poly[t], nm));
+        np2[t + 1] = f_add(&FR, np2[t + 1], poly[t]);
+      }
+      deg++;
+      memcpy(poly, np2, sizeof poly);
+      int64_t d = j - mm;
+      fp dd = {{(uint64_t)(d < 0 ? -d : d), 0, 0, 0}};
+      dd = f_to_mont(&FR, dd);
+      if (d < 0) dd = f_sub(&FR, (fp){{0, 0, 0, 0}}, dd);
+      den = f_mul(&FR, den, dd);
+    }
+    fp di = f_inv(&FR, den);
+    for (int t = 0; t < np; t++) V[t][j] = f_mul(&FR, poly[t], di);
+  }
+  size_t half = N;
+  for (int j = 0; j < nvars; j++) {
+    half >>= 1;
+    fp sums[16];
+    for (int t = 0; t < np; t++) sums[t] = (fp){{0, 0, 0, 0}};
+    for (size_t p = 0; p < half; p++) {
+      fp lo[8], df[8];
+      for (int i = 0; i < k; i++) {
+        lo[i] = g[i * N + 2 * p];
+        df[i] = f_sub(&FR, g[i * N + 2 * p + 1], lo[i]);
+      }
+      for (int t = 0; t < np; t++) {
+        if (t) for (int i = 0; i < k; i++) lo[i] = f_add(&FR, lo[i], df[i]);
+        fp prod = lo[0];
+        for (int i = 1; i < k; i++) prod = f_mul(&FR, prod, lo[i]);
+        sums[t] = f_add(&FR, sums[t], prod);
+      }
+    }
+    fp co[16];
+    uint32_t len = 0;
+    for (int t = 0; t < np; t++) {
+      fp acc = {{0, 0, 0, 0}};
+      for (int u = 0; u < np; u++) acc = f_add(&FR, acc, f_mul(&FR, V[t][u], sums[u]));
+      co[t] = acc;
+      if (!f_is_zero(acc)) len = t + 1;
+    }
+    uint8_t msg[8 + 16 * 32];
+    for (int i = 0; i < 8; i++) msg[i] = (uint8_t)((uint64_t)len >> (8 * i));
+    for (uint32_t t = 0; t < len; t++) fr_bytes(co[t], msg + 8 + 32 * t);
+    tr_append(state, msg, 8 + 32 * len);
+    fp r = tr_draw_fr(state);
+    for (int t = 0; t < np; t++) memcpy(coeffs + 4 * ((size_t)j * np + t), (t < (int)len ? co[t] : (fp){{0,0,0,0}}).v, 32);
+    lens[j] = len;
+    memcpy(point + 4 * j, r.v, 32);
+    for (int i = 0; i < k; i++)
+      for (size_t p = 0; p < half; p++) {
+        fp a = g[i * N + 2 * p], b = g[i * N + 2 * p + 1];
+        g[i * N + p] = f_add(&FR, a, f_mul(&FR, r, f_sub(&FR, b, a)));
+      }
+  }
+  fp e = g[0];
+  for (int i = 1; i < k; i++) e = f_mul(&FR, e, g[i * N]);
+  memcpy(evaluation, e.v, 32);
+  free(g);
+  return 0;
+}
+
+/* Timed sumcheck baseline on 2^log_n, k = 3 random tables. */
+int oc_bench_sumcheck(int log_n, uint64_t seed, double* seconds) {
+  size_t N = (size_t)1 << log_n;
+  sm_state = seed;
+  fp* t = (fp*)malloc(sizeof(fp) * N * 3);
+  for (size_t i = 0; i < 3 * N; i++) t[i] = rand_fr();
+  uint8_t st[32] = {0};
+  uint64_t cl[4] = {0, 0, 0, 0};
+  uint64_t* co = (uint64_t*)malloc(sizeof(uint64_t) * 4 * 4 * log_n);
+  uint32_t* lens = (uint32_t*)malloc(sizeof(uint32_t) * log_n);
+  uint64_t* pt = (uint64_t*)malloc(sizeof(uint64_t) * 4 * log_n);
+  uint64_t ev[4];
+  double a = now_s();
+  oc_sumcheck_prod(log_n, 3, (const uint64_t*)t, cl, st, co, lens, pt, ev);
+  *seconds = now_s() - a;
+  free(t);
+  free(co);
+  free(lens);
+  free(pt);
+  return 0;
+}

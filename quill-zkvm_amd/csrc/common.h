@@ -1,0 +1,182 @@
+// Shared host-side infrastructure of libquill_gpu: context, scratch arena,
+// error handling at the C-ABI, HIP-event kernel timing.
+#pragma once
+#include <hip/hip_runtime.h>
+
+#include <map>
+#include <stdexcept>
+#include <string>
+#include <vector>
+
+#include "../../include/quill_gpu.h"
+#include "curve.h"
+#include "field.h"
+
+namespace qg {
+
+struct Error : std::runtime_error {
+  int code;
+  Error(int c, const std::string& m) : std::runtime_error(m), code(c) {}
+};
+
+#define QG_HIP(call)                                                                  \
+  do {                                                                                \
+    hipError_t _e = (call);                                                           \
+    if (_e != hipSuccess)                                                             \
+      throw ::qg::Error(_e == hipErrorOutOfMemory ? QG_ERR_OOM : QG_ERR_DEVICE,       \
+                        std::string(#call) + ": " + hipGetErrorString(_e));           \
+  } while (0)
+
+#define QG_CHECK(cond, code, msg)                  \
+  do {                                             \
+    if (!(cond)) throw ::qg::Error((code), (msg)); \
+  } while (0)
+
+// Launch-and-check helper: kernel errors surface at the call.
+#define QG_LAUNCH_CHECK() QG_HIP(hipGetLastError())
+
+inline unsigned div_up(size_t a, size_t b) { return (unsigned)((a + b - 1) / b); }
+
+}  // namespace qg
+
+struct qg_comm_state;  // RCCL (comm.hip)
+
+struct qg_ctx {
+  int device = 0;
+  hipStream_t stream = nullptr;
+  std::string last_error;
+  // grow-only scratch arena, one slot per purpose
+  std::map<std::string, std::pair<void*, size_t>> scratch;
+  // timing
+  bool timing = false;
+  struct Ev {
+    std::string name;
+    hipEvent_t a, b;
+  };
+  std::vector<Ev> pending;
+  std::map<std::string, std::pair<double, uint32_t>> ktime;
+  std::vector<hipEvent_t> event_pool;
+  // RCCL
+  qg_comm_state* comm = nullptr;
+  int rank = 0, world = 1;
+
+  void* scratch_get(const std::string& slot, size_t bytes) {
+    auto it = scratch.find(slot);
+    if (it != scratch.end() && it->second.second >= bytes) return it->second.first;
+    if (it != scratch.end()) {
+      QG_HIP(hipFree(it->second.first));
+      scratch.erase(it);
+    }
+    void* p = nullptr;
+    size_t b = bytes ? bytes : 16;
+    QG_HIP(hipMalloc(&p, b));
+    scratch[slot] = {p, b};
+    return p;
+  }
+  template <class T>
+  T* scratch_as(const std::string& slot, size_t count) {
+    return reinterpret_cast<T*>(scratch_get(slot, count * sizeof(T)));
+  }
+
+  hipEvent_t ev_get() {
+    if (!event_pool.empty()) {
+      hipEvent_t e = event_pool.back();
+      event_pool.pop_back();
+      return e;
+    }
+    hipEvent_t e;
+    QG_HIP(hipEventCreate(&e));
+    return e;
+  }
+  // begin/end a timed region on the context stream
+  int tbegin(const char* name) {
+    if (!timing) return -1;
+    Ev e{name, ev_get(), ev_get()};
+    QG_HIP(hipEventRecord(e.a, stream));
+    pending.push_back(e);
+    return (int)pending.size() - 1;
+  }
+  void tend(int h) noexcept {
+    if (h < 0) return;
+    (void)hipEventRecord(pending[h].b, stream);
+  }
+  // resolve pending events (after a stream sync)
+  void tresolve() {
+    for (auto& e : pending) {
+      float ms = 0.f;
+      QG_HIP(hipEventElapsedTime(&ms, e.a, e.b));
+      auto& slot = ktime[e.name];
+      slot.first += ms;
+      slot.second += 1;
+      event_pool.push_back(e.a);
+      event_pool.push_back(e.b);
+    }
+    pending.clear();
+  }
+  void sync() {
+    QG_HIP(hipStreamSynchronize(stream));
+    if (timing) tresolve();
+  }
+};
+
+struct qg_buf {
+  qg_ctx* ctx = nullptr;
+  size_t n = 0;
+  qg::Fr* d = nullptr;
+};
+
+struct qg_srs {
+  qg_ctx* ctx = nullptr;
+  size_t n = 0;  // number of bases
+  int c = 0;     // MSM window bits (signed digits)
+  int W = 0;     // number of windows = ceil(255 / c)
+  // W * n affine points; table[w * n + i] = 2^(c*w) * base_i   (infinity = (0,0))
+  qg::G1Affine* d_table = nullptr;
+};
+
+// scoped timer
+struct QgTimed {
+  qg_ctx* c;
+  int h;
+  QgTimed(qg_ctx* ctx, const char* name) : c(ctx), h(ctx->tbegin(name)) {}
+  ~QgTimed() { c->tend(h); }
+};
+
+// Wrap a C-ABI body: no exception crosses the boundary.
+template <class F>
+static int qg_guard(qg_ctx* ctx, F&& f) {
+  try {
+    f();
+    return QG_OK;
+  } catch (const qg::Error& e) {
+    if (ctx) ctx->last_error = e.what();
+    return e.code;
+  } catch (const std::bad_alloc&) {
+    if (ctx) ctx->last_error = "host allocation failed";
+    return QG_ERR_OOM;
+  } catch (const std::exception& e) {
+    if (ctx) ctx->last_error = e.what();
+    return QG_ERR_DEVICE;
+  } catch (...) {
+    if (ctx) ctx->last_error = "unknown error";
+    return QG_ERR_DEVICE;
+  }
+}
+
+// ---- internal entry points shared between translation units -------------
+namespace qg {
+// MSM over device scalars; result (XYZZ, summed over RCCL ranks if attached)
+G1Affine msm_device(qg_ctx* ctx, const qg_srs* srs, const Fr* d_scalars, size_t n);
+void fr_upload(qg_ctx* ctx, Fr* d, const uint64_t* h, size_t n);
+void fr_download(qg_ctx* ctx, uint64_t* h, const Fr* d, size_t n);
+// affine G1 -> ABI (xy Montgomery limbs + inf flag)
+void g1_export(const G1Affine& a, uint64_t xy[8], uint8_t* inf);
+G1Affine g1_import(const uint64_t xy[8], uint8_t inf);
+void g1_serialize(const G1Affine& a, uint8_t out[64]);
+Fr fr_import(const uint64_t v[4]);
+void fr_export(const Fr& a, uint64_t v[4]);
+// eq(bin(i), z) table on the device (sumcheck.hip)
+void eq_table_device(qg_ctx* ctx, const Fr* d_z, uint32_t nvars, Fr* d_out);
+// RCCL helpers (comm.hip); no-ops when world == 1
+void comm_allgather_bytes(qg_ctx* ctx, const void* d_send, void* d_recv, size_t bytes);
+}  // namespace qg

@@ -1,0 +1,457 @@
+// Multilinear PCS opening passes for gfx950 — replaces
+//   KZG::open                          pcs/src/kzg.rs:75-96
+//   MLEvalProof::compute_pr / prove    pcs/src/mlpcs.rs:52-124
+//   InnerProductProof::compute_s_polynomial  pcs/src/ipa.rs:122-157
+//
+//  * compute_pr == the eq table (identity pinned by the KATs at
+//    mlpcs.rs:226-242): built in O(2^n) on the device, no IFFT.
+//  * y = p(x) and q = (p - y)/(X - x) come out of ONE suffix-Horner scan
+//    s_i = c_i + x s_{i+1}:  y = s_0, q_i = s_{i+1}.  The scan is blocked:
+//    per-chunk zero-carry values, a recursive scan of the chunk carries with
+//    multiplier x^B, then a per-chunk apply pass.
+//  * S_k = sum_i (f_{i+k+1} g_i + g_{i+k+1} f_i) is the upper half of
+//    h = f*rev(g) + rev(f)*g.  Two forward NTTs (F, G) suffice:
+//    NTT(rev f)[j] = w^{j(M-1)} F[-j], so H[j] = w^{j(M-1)} (F[j]G[-j] + F[-j]G[j]).
+//  * Every commitment is the device MSM (msm.hip) over device-resident data.
+#include <string.h>
+
+#include <vector>
+
+#include "blake3.h"
+#include "common.h"
+
+using namespace qg;
+
+namespace qg {
+
+static constexpr int ML_BLOCK = 256;
+static constexpr int SH_B = 32;  // suffix-Horner chunk length
+
+// ---------------------------------------------------------------- reductions
+QG_DEV Fr shfl_xor_fr2(const Fr& a, int m) {
+  Fr r;
+#pragma unroll
+  for (int i = 0; i < 8; i++) r.v[i] = __shfl_xor(a.v[i], m, 64);
+  return r;
+}
+
+QG_DEV Fr block_sum_fr(Fr v, Fr* lds) {
+  for (int m = 32; m > 0; m >>= 1) v = v + shfl_xor_fr2(v, m);
+  const int lane = threadIdx.x & 63, wid = threadIdx.x >> 6, nw = blockDim.x >> 6;
+  if (lane == 0) lds[wid] = v;
+  __syncthreads();
+  Fr acc = Fr::zero();
+  if (threadIdx.x == 0)
+    for (int w = 0; w < nw; w++) acc = acc + lds[w];
+  __syncthreads();
+  return acc;
+}
+
+__global__ void __launch_bounds__(ML_BLOCK)
+    k_dot(const Fr* __restrict__ f, const Fr* __restrict__ g, size_t n, Fr* __restrict__ partial) {
+  __shared__ Fr lds[ML_BLOCK / 64];
+  Fr acc = Fr::zero();
+  for (size_t i = (size_t)blockIdx.x * blockDim.x + threadIdx.x; i < n;
+       i += (size_t)gridDim.x * blockDim.x)
+    acc = acc + f[i] * g[i];
+  acc = block_sum_fr(acc, lds);
+  if (threadIdx.x == 0) partial[blockIdx.x] = acc;
+}
+
+__global__ void __launch_bounds__(ML_BLOCK)
+    k_sum(const Fr* __restrict__ in, size_t n, Fr* __restrict__ out) {
+  __shared__ Fr lds[ML_BLOCK / 64];
+  Fr acc = Fr::zero();
+  for (size_t i = threadIdx.x; i < n; i += blockDim.x) acc = acc + in[i];
+  acc = block_sum_fr(acc, lds);
+  if (threadIdx.x == 0) *out = acc;
+}
+
+static Fr dot_device(qg_ctx* ctx, const Fr* f, const Fr* g, size_t n) {
+  if (n == 0) return Fr::zero();
+  QgTimed tm(ctx, "inner_product");
+  unsigned blocks = (unsigned)std::min<size_t>(2048, div_up(n, ML_BLOCK));
+  Fr* part = ctx->scratch_as<Fr>("dot_part", blocks + 1);
+  hipLaunchKernelGGL(k_dot, dim3(blocks), dim3(ML_BLOCK), 0, ctx->stream, f, g, n, part);
+  QG_LAUNCH_CHECK();
+  hipLaunchKernelGGL(k_sum, dim3(1), dim3(ML_BLOCK), 0, ctx->stream, part, (size_t)blocks,
+                     part + blocks);
+  QG_LAUNCH_CHECK();
+  Fr r;
+  QG_HIP(hipMemcpyAsync(&r, part + blocks, sizeof(Fr), hipMemcpyDeviceToHost, ctx->stream));
+  ctx->sync();
+  return r;
+}
+
+// ---------------------------------------------------------------- suffix Horner
+// A_k = sum_{i in chunk k} c_i x^(i - start_k)
+__global__ void k_sh_local(const Fr* __restrict__ c, size_t L, Fr x, Fr* __restrict__ A) {
+  size_t k = (size_t)blockIdx.x * blockDim.x + threadIdx.x;
+  size_t s = k * SH_B;
+  if (s >= L) return;
+  size_t e = s + SH_B < L ? s + SH_B : L;
+  Fr acc = Fr::zero();
+  for (size_t i = e; i-- > s;) acc = c[i] + x * acc;
+  A[k] = acc;
+}
+
+// s_i for every i given T_{k+1} (suffix value at the start of chunk k+1)
+__global__ void k_sh_apply(const Fr* __restrict__ c, size_t L, Fr x, const Fr* __restrict__ T,
+                           size_t nchunks, Fr* __restrict__ s_out) {
+  size_t k = (size_t)blockIdx.x * blockDim.x + threadIdx.x;
+  size_t s = k * SH_B;
+  if (s >= L) return;
+  size_t e = s + SH_B < L ? s + SH_B : L;
+  Fr acc = (k + 1 < nchunks) ? T[k + 1] : Fr::zero();
+  for (size_t i = e; i-- > s;) {
+    acc = c[i] + x * acc;
+    s_out[i] = acc;
+  }
+}
+
+// small case: one thread
+__global__ void k_sh_serial(const Fr* __restrict__ c, size_t L, Fr x, Fr* __restrict__ s_out) {
+  if (threadIdx.x != 0 || blockIdx.x != 0) return;
+  Fr acc = Fr::zero();
+  for (size_t i = L; i-- > 0;) {
+    acc = c[i] + x * acc;
+    s_out[i] = acc;
+  }
+}
+
+// s = suffix Horner of c (length L) at x: s_i = c_i + x s_{i+1}
+static void suffix_horner(qg_ctx* ctx, const Fr* c, size_t L, const Fr& x, Fr* s, int depth = 0) {
+  if (L == 0) return;
+  if (L <= SH_B) {
+    hipLaunchKernelGGL(k_sh_serial, dim3(1), dim3(64), 0, ctx->stream, c, L, x, s);
+    QG_LAUNCH_CHECK();
+    return;
+  }
+  const size_t nch = (L + SH_B - 1) / SH_B;
+  Fr* A = ctx->scratch_as<Fr>("sh_A" + std::to_string(depth), nch);
+  Fr* T = ctx->scratch_as<Fr>("sh_T" + std::to_string(depth), nch);
+  hipLaunchKernelGGL(k_sh_local, dim3(div_up(nch, ML_BLOCK)), dim3(ML_BLOCK), 0, ctx->stream, c,
+                     L, x, A);
+  QG_LAUNCH_CHECK();
+  // T_k = A_k + x^B T_{k+1}
+  Fr xb = fpow_small(x, SH_B);
+  suffix_horner(ctx, A, nch, xb, T, depth + 1);
+  hipLaunchKernelGGL(k_sh_apply, dim3(div_up(nch, ML_BLOCK)), dim3(ML_BLOCK), 0, ctx->stream, c, L,
+                     x, T, nch, s);
+  QG_LAUNCH_CHECK();
+}
+
+// ---------------------------------------------------------------- NTT
+__global__ void k_bitrev_copy(const Fr* __restrict__ in, size_t nin, Fr* __restrict__ out,
+                              int logn, int reverse_input, size_t rev_len) {
+  size_t i = (size_t)blockIdx.x * blockDim.x + threadIdx.x;
+  size_t n = (size_t)1 << logn;
+  if (i >= n) return;
+  size_t j = __brevll((unsigned long long)i) >> (64 - logn);
+  Fr v = Fr::zero();
+  // source element i (optionally of the reversed length-rev_len sequence)
+  size_t src = i;
+  bool ok = true;
+  if (reverse_input) {
+    if (i < rev_len) src = rev_len - 1 - i;
+    else ok = false;
+  }
+  if (ok && src < nin) v = in[src];
+  out[j] = v;
+}
+
+// radix-2 DIT stages with half-span m < 512 done in LDS on 1024-element tiles
+__global__ void __launch_bounds__(512)
+    k_ntt_tile(Fr* __restrict__ a, const Fr* __restrict__ tw, int logn, int stages) {
+  __shared__ Fr sh[1024];
+  const size_t base = (size_t)blockIdx.x * 1024;
+  sh[threadIdx.x] = a[base + threadIdx.x];
+  sh[threadIdx.x + 512] = a[base + threadIdx.x + 512];
+  __syncthreads();
+  for (int s = 0; s < stages; s++) {
+    const uint32_t m = 1u << s;  // half span
+    const uint32_t t = threadIdx.x;
+    const uint32_t grp = t >> s, j = t & (m - 1);
+    const uint32_t i0 = grp * 2 * m + j, i1 = i0 + m;
+    // twiddle w_{2m}^j = w_N^{j * N/(2m)}
+    const Fr w = tw[(size_t)j << (logn - 1 - s)];
+    Fr u = sh[i0], v = sh[i1] * w;
+    sh[i0] = u + v;
+    sh[i1] = u - v;
+    __syncthreads();
+  }
+  a[base + threadIdx.x] = sh[threadIdx.x];
+  a[base + threadIdx.x + 512] = sh[threadIdx.x + 512];
+}
+
+__global__ void k_ntt_stage(Fr* __restrict__ a, const Fr* __restrict__ tw, int logn, int s) {
+  size_t t = (size_t)blockIdx.x * blockDim.x + threadIdx.x;
+  const size_t n = (size_t)1 << logn;
+  if (t >= n / 2) return;
+  const size_t m = (size_t)1 << s;
+  const size_t grp = t >> s, j = t & (m - 1);
+  const size_t i0 = grp * 2 * m + j, i1 = i0 + m;
+  const Fr w = tw[j << (logn - 1 - s)];
+  Fr u = a[i0], v = a[i1] * w;
+  a[i0] = u + v;
+  a[i1] = u - v;
+}
+
+// in-place NTT of a (already bit-reversed) with twiddle table tw[k] = w^k, k < n/2
+static void ntt_bitreversed(qg_ctx* ctx, Fr* a, const Fr* tw, int logn) {
+  const size_t n = (size_t)1 << logn;
+  int s = 0;
+  if (logn >= 10) {
+    hipLaunchKernelGGL(k_ntt_tile, dim3((unsigned)(n / 1024)), dim3(512), 0, ctx->stream, a, tw,
+                       logn, 10);
+    QG_LAUNCH_CHECK();
+    s = 10;
+  }
+  for (; s < logn; s++) {
+    hipLaunchKernelGGL(k_ntt_stage, dim3(div_up(n / 2, 256)), dim3(256), 0, ctx->stream, a, tw,
+                       logn, s);
+    QG_LAUNCH_CHECK();
+  }
+}
+
+__global__ void k_powers_ml(Fr base, size_t n, int K, Fr* out) {
+  size_t t = (size_t)blockIdx.x * blockDim.x + threadIdx.x;
+  size_t i0 = t * (size_t)K;
+  if (i0 >= n) return;
+  Fr x = fpow_small(base, (uint64_t)i0);
+  for (int j = 0; j < K && i0 + j < n; j++) {
+    out[i0 + j] = x;
+    x = x * base;
+  }
+}
+
+// H[j] = w^{j(M-1)} (F[j] G[-j] + F[-j] G[j]), times n^{-1} folded in later
+__global__ void k_s_combine(const Fr* __restrict__ F, const Fr* __restrict__ G,
+                            const Fr* __restrict__ twM, size_t n, Fr* __restrict__ H) {
+  size_t j = (size_t)blockIdx.x * blockDim.x + threadIdx.x;
+  if (j >= n) return;
+  size_t nj = (n - j) & (n - 1);
+  Fr v = F[j] * G[nj] + F[nj] * G[j];
+  H[j] = v * twM[j];
+}
+
+__global__ void k_scale_copy(const Fr* __restrict__ in, Fr s, size_t n, Fr* __restrict__ out) {
+  size_t i = (size_t)blockIdx.x * blockDim.x + threadIdx.x;
+  if (i >= n) return;
+  out[i] = in[i] * s;
+}
+
+// host-side 256-bit exponent power
+static Fr fr_pow_big(Fr a, const uint32_t e[8]) {
+  Fr r = Fr::one();
+  for (int i = 7; i >= 0; i--)
+    for (int b = 31; b >= 0; b--) {
+      r = fsqr(r);
+      if ((e[i] >> b) & 1u) r = r * a;
+    }
+  return r;
+}
+
+// primitive 2^logn-th root of unity: 5^((r-1)/2^logn)
+static Fr root_of_unity(int logn) {
+  uint32_t e[8];
+  for (int i = 0; i < 8; i++) e[i] = FrP::P[i];
+  e[0] -= 1;  // r - 1 (low limb of r is odd)
+  for (int k = 0; k < logn; k++) {  // shift right by logn
+    for (int i = 0; i < 8; i++) e[i] = (e[i] >> 1) | (i < 7 ? (e[i + 1] << 31) : 0u);
+  }
+  return fr_pow_big(from_u64<FrP>(5), e);
+}
+
+// S polynomial (M - 1 coefficients, untrimmed) of f (nf) and g (ng), device in/out
+static void s_poly_device(qg_ctx* ctx, const Fr* f, size_t nf, const Fr* g, size_t ng, Fr* S) {
+  const size_t M = nf > ng ? nf : ng;
+  if (M <= 1) return;
+  QgTimed tm(ctx, "s_polynomial");
+  int logn = 0;
+  while (((size_t)1 << logn) < 2 * M - 1) logn++;
+  QG_CHECK(logn <= 28, QG_ERR_UNSUPPORTED, "S-polynomial NTT beyond 2-adicity");
+  if (logn < 1) logn = 1;
+  const size_t n = (size_t)1 << logn;
+  Fr* F = ctx->scratch_as<Fr>("ntt_F", n);
+  Fr* G = ctx->scratch_as<Fr>("ntt_G", n);
+  Fr* H = ctx->scratch_as<Fr>("ntt_H", n);
+  Fr* tw = ctx->scratch_as<Fr>("ntt_tw", n / 2 + 1);
+  Fr* twi = ctx->scratch_as<Fr>("ntt_twi", n / 2 + 1);
+  Fr* twM = ctx->scratch_as<Fr>("ntt_twM", n);
+  Fr w = root_of_unity(logn);
+  Fr wi = finv(w);
+  const int K = 64;
+  hipLaunchKernelGGL(k_powers_ml, dim3(div_up(div_up(n / 2, K), 256)), dim3(256), 0, ctx->stream,
+                     w, n / 2, K, tw);
+  QG_LAUNCH_CHECK();
+  hipLaunchKernelGGL(k_powers_ml, dim3(div_up(div_up(n / 2, K), 256)), dim3(256), 0, ctx->stream,
+                     wi, n / 2, K, twi);
+  QG_LAUNCH_CHECK();
+  // w^{j(M-1)} for j < n
+  Fr wM = fpow_small(w, (uint64_t)(M - 1));
+  hipLaunchKernelGGL(k_powers_ml, dim3(div_up(div_up(n, K), 256)), dim3(256), 0, ctx->stream, wM,
+                     n, K, twM);
+  QG_LAUNCH_CHECK();
+  hipLaunchKernelGGL(k_bitrev_copy, dim3(div_up(n, 256)), dim3(256), 0, ctx->stream, f, nf, F,
+                     logn, 0, (size_t)0);
+  QG_LAUNCH_CHECK();
+  hipLaunchKernelGGL(k_bitrev_copy, dim3(div_up(n, 256)), dim3(256), 0, ctx->stream, g, ng, G,
+                     logn, 0, (size_t)0);
+  QG_LAUNCH_CHECK();
+  ntt_bitreversed(ctx, F, tw, logn);
+  ntt_bitreversed(ctx, G, tw, logn);
+  hipLaunchKernelGGL(k_s_combine, dim3(div_up(n, 256)), dim3(256), 0, ctx->stream, F, G, twM, n,
+                     H);
+  QG_LAUNCH_CHECK();
+  // inverse NTT: bit-reverse H into F, transform with w^{-1}
+  hipLaunchKernelGGL(k_bitrev_copy, dim3(div_up(n, 256)), dim3(256), 0, ctx->stream, H, n, F, logn,
+                     0, (size_t)0);
+  QG_LAUNCH_CHECK();
+  ntt_bitreversed(ctx, F, twi, logn);
+  // h has 2M-1 meaningful coefficients (< n); S = h[M .. 2M-1), scaled by 1/n
+  Fr ninv = finv(from_u64<FrP>(n));
+  hipLaunchKernelGGL(k_scale_copy, dim3(div_up(M - 1, 256)), dim3(256), 0, ctx->stream, F + M,
+                     ninv, M - 1, S);
+  QG_LAUNCH_CHECK();
+}
+
+__global__ void k_last_nonzero(const Fr* __restrict__ a, size_t n, unsigned long long* out) {
+  size_t i = (size_t)blockIdx.x * blockDim.x + threadIdx.x;
+  if (i >= n) return;
+  if (!a[i].is_zero()) atomicMax(out, (unsigned long long)(i + 1));
+}
+
+// trimmed length of a device vector
+static size_t trimmed_len(qg_ctx* ctx, const Fr* a, size_t n) {
+  if (n == 0) return 0;
+  unsigned long long* d = ctx->scratch_as<unsigned long long>("trim_len", 1);
+  QG_HIP(hipMemsetAsync(d, 0, sizeof(unsigned long long), ctx->stream));
+  hipLaunchKernelGGL(k_last_nonzero, dim3(div_up(n, 256)), dim3(256), 0, ctx->stream, a, n, d);
+  QG_LAUNCH_CHECK();
+  unsigned long long h = 0;
+  QG_HIP(hipMemcpyAsync(&h, d, sizeof(h), hipMemcpyDeviceToHost, ctx->stream));
+  ctx->sync();
+  return (size_t)h;
+}
+
+// KZG::open on a device polynomial; fills x, y, proof
+static void kzg_open_device(qg_ctx* ctx, const qg_srs* srs, const Fr* c, size_t L, const Fr& x,
+                            qg_kzg_opening* out) {
+  fr_export(x, out->x);
+  size_t Lt = trimmed_len(ctx, c, L);  // DensePolynomial::from_coefficients_slice trims
+  Fr y = Fr::zero();
+  G1Affine pi = G1Affine::infinity();
+  if (Lt > 0) {
+    Fr* s = ctx->scratch_as<Fr>("open_s", Lt);
+    {
+      QgTimed tm(ctx, "kzg_division");
+      suffix_horner(ctx, c, Lt, x, s);
+    }
+    QG_HIP(hipMemcpyAsync(&y, s, sizeof(Fr), hipMemcpyDeviceToHost, ctx->stream));
+    ctx->sync();
+    // q_i = s_{i+1}, i < Lt - 1; commit(q) (kzg.rs:88-89)
+    QG_CHECK(Lt - 1 <= srs->n, QG_ERR_INVALID, "Polynomial degree exceeds max degree");
+    pi = msm_device(ctx, srs, s + 1, Lt - 1);
+  }
+  fr_export(y, out->y);
+  g1_export(pi, out->proof_xy, &out->proof_inf);
+}
+
+}  // namespace qg
+
+extern "C" {
+
+int qg_inner_product(qg_ctx* ctx, const uint64_t* f, size_t nf, const uint64_t* g, size_t ng,
+                     uint64_t out[4]) {
+  if (!ctx || (!f && nf) || (!g && ng) || !out) return QG_ERR_INVALID;
+  return qg_guard(ctx, [&] {
+    QG_HIP(hipSetDevice(ctx->device));
+    size_t n = nf < ng ? nf : ng;
+    Fr* df = ctx->scratch_as<Fr>("ip_f", n ? n : 1);
+    Fr* dg = ctx->scratch_as<Fr>("ip_g", n ? n : 1);
+    fr_upload(ctx, df, f, n);
+    fr_upload(ctx, dg, g, n);
+    fr_export(dot_device(ctx, df, dg, n), out);
+  });
+}
+
+int qg_s_polynomial(qg_ctx* ctx, const uint64_t* f, size_t nf, const uint64_t* g, size_t ng,
+                    uint64_t* out) {
+  if (!ctx || (!f && nf) || (!g && ng) || (!out && (nf > 1 || ng > 1))) return QG_ERR_INVALID;
+  return qg_guard(ctx, [&] {
+    QG_HIP(hipSetDevice(ctx->device));
+    const size_t M = nf > ng ? nf : ng;
+    if (M <= 1) return;
+    Fr* df = ctx->scratch_as<Fr>("sp_f", nf ? nf : 1);
+    Fr* dg = ctx->scratch_as<Fr>("sp_g", ng ? ng : 1);
+    Fr* dS = ctx->scratch_as<Fr>("sp_S", M - 1);
+    fr_upload(ctx, df, f, nf);
+    fr_upload(ctx, dg, g, ng);
+    s_poly_device(ctx, df, nf, dg, ng, dS);
+    fr_download(ctx, out, dS, M - 1);
+    ctx->sync();
+  });
+}
+
+int qg_kzg_open(qg_ctx* ctx, const qg_srs* srs, const uint64_t* poly, size_t n, const uint64_t x[4],
+                qg_kzg_opening* out) {
+  if (!ctx || !srs || (!poly && n) || !x || !out) return QG_ERR_INVALID;
+  return qg_guard(ctx, [&] {
+    QG_HIP(hipSetDevice(ctx->device));
+    Fr* d = ctx->scratch_as<Fr>("open_in", n ? n : 1);
+    fr_upload(ctx, d, poly, n);
+    kzg_open_device(ctx, srs, d, n, fr_import(x), out);
+  });
+}
+
+int qg_mle_open(qg_ctx* ctx, const qg_srs* srs, const uint64_t* poly, size_t n,
+                const uint64_t* point, size_t nvars, uint8_t state[32], qg_mle_proof* out) {
+  if (!ctx || !srs || (!poly && n) || (!point && nvars) || !state || !out) return QG_ERR_INVALID;
+  return qg_guard(ctx, [&] {
+    QG_CHECK(nvars <= 30, QG_ERR_INVALID, "too many variables");
+    QG_HIP(hipSetDevice(ctx->device));
+    const size_t N = (size_t)1 << nvars;
+    Fr* dpoly = ctx->scratch_as<Fr>("mle_poly", n ? n : 1);
+    Fr* dz = ctx->scratch_as<Fr>("mle_z", nvars ? nvars : 1);
+    Fr* dpr = ctx->scratch_as<Fr>("mle_pr", N);
+    fr_upload(ctx, dpoly, poly, n);
+    fr_upload(ctx, dz, point, nvars);
+    // P_r coefficients = eq table (mlpcs.rs:68-78)
+    eq_table_device(ctx, dz, (uint32_t)nvars, dpr);
+    // evaluation = <poly, P_r> over the common prefix (mlpcs.rs:91-94)
+    Fr evaluation = dot_device(ctx, dpoly, dpr, n < N ? n : N);
+    // S polynomial and its commitment (mlpcs.rs:95-97)
+    const size_t M = n > N ? n : N;
+    Fr* dS = ctx->scratch_as<Fr>("mle_S", M > 1 ? M - 1 : 1);
+    size_t Slen = 0;
+    if (M > 1) {
+      s_poly_device(ctx, dpoly, n, dpr, N, dS);
+      Slen = trimmed_len(ctx, dS, M - 1);
+    }
+    QG_CHECK(Slen <= srs->n, QG_ERR_INVALID, "Polynomial degree exceeds max degree");
+    G1Affine s_comm = msm_device(ctx, srs, dS, Slen);
+    // transcript: point (Vec<Fr>), evaluation, s_comm; draw r (mlpcs.rs:100-107)
+    std::vector<uint8_t> msg(8 + 32 * nvars);
+    u64_to_bytes(nvars, msg.data());
+    for (size_t i = 0; i < nvars; i++) fr_to_bytes(fr_import(point + 4 * i), msg.data() + 8 + 32 * i);
+    transcript_append(state, msg.data(), msg.size());
+    uint8_t b32[32], b64[64];
+    fr_to_bytes(evaluation, b32);
+    transcript_append(state, b32, 32);
+    g1_serialize(s_comm, b64);
+    transcript_append(state, b64, 64);
+    Fr r = transcript_draw_fr(state);
+    QG_CHECK(!r.is_zero(), QG_ERR_ASSERT, "challenge r = 0");
+    Fr r_inv = finv(r);
+    fr_export(evaluation, out->evaluation);
+    g1_export(s_comm, out->s_comm_xy, &out->s_comm_inf);
+    // four KZG openings (mlpcs.rs:108-113)
+    kzg_open_device(ctx, srs, dpoly, n, r, &out->poly_opening);
+    kzg_open_device(ctx, srs, dpoly, n, r_inv, &out->poly_opening_inv);
+    kzg_open_device(ctx, srs, dS, Slen, r, &out->s_opening);
+    kzg_open_device(ctx, srs, dS, Slen, r_inv, &out->s_opening_inv);
+  });
+}
+
+}  // extern "C"

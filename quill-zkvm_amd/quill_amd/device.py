@@ -1,0 +1,182 @@
+"""Device context, SRS and device-resident Fr vectors (qg_ctx / qg_srs / qg_buf)."""
+from __future__ import annotations
+
+import ctypes as C
+
+import numpy as np
+
+from ._lib import check, lib
+from .field import fr_array, fr_c, fr_list, g1_from_abi, g1_to_abi, u64p
+
+
+class Device:
+    """One HIP device (qg_ctx_create).  Context for every GPU call."""
+
+    def __init__(self, device: int = 0):
+        self.h = C.c_void_p()
+        check(lib().qg_ctx_create(device, C.byref(self.h)))
+        self.device = device
+
+    def close(self):
+        if self.h:
+            lib().qg_ctx_destroy(self.h)
+            self.h = C.c_void_p()
+
+    def __del__(self):
+        try:
+            self.close()
+        except Exception:
+            pass
+
+    def attach_comm(self, rank: int, world: int, unique_id: bytes):
+        buf = (C.c_uint8 * 128).from_buffer_copy(unique_id)
+        check(lib().qg_ctx_attach_comm(self.h, rank, world, buf), self.h)
+
+    @staticmethod
+    def comm_unique_id() -> bytes:
+        buf = (C.c_uint8 * 128)()
+        check(lib().qg_comm_unique_id(buf))
+        return bytes(buf)
+
+    def enable_timing(self, on=True):
+        check(lib().qg_ctx_enable_timing(self.h, 1 if on else 0), self.h)
+
+    def microbench_fq_mul(self) -> float:
+        r = C.c_double()
+        check(lib().qg_microbench_fq_mul(self.h, C.byref(r)), self.h)
+        return r.value
+
+    def kernel_time(self, name: str):
+        ms = C.c_double()
+        n = C.c_uint32()
+        check(lib().qg_ctx_kernel_time(self.h, name.encode(), C.byref(ms), C.byref(n)), self.h)
+        return ms.value, n.value
+
+    # ---- device math building blocks (mlpcs.rs / ipa.rs / eq_eval.rs) ----
+    def eq_table(self, point):
+        n = len(point)
+        pt = fr_array(point)
+        out = np.zeros((1 << n, 4), dtype=np.uint64)
+        check(lib().qg_eq_table(self.h, u64p(pt), n, u64p(out)), self.h)
+        return fr_list(out)
+
+    def s_polynomial(self, f, g):
+        M = max(len(f), len(g))
+        fa, ga = fr_array(f), fr_array(g)
+        out = np.zeros((max(M - 1, 1), 4), dtype=np.uint64)
+        check(lib().qg_s_polynomial(self.h, u64p(fa), len(f), u64p(ga), len(g), u64p(out)), self.h)
+        return fr_list(out[:max(M - 1, 0)])
+
+    def inner_product(self, f, g):
+        fa, ga = fr_array(f), fr_array(g)
+        out = (C.c_uint64 * 4)()
+        check(lib().qg_inner_product(self.h, u64p(fa), len(f), u64p(ga), len(g), out), self.h)
+        from .field import fr_from_mont_limbs
+        return fr_from_mont_limbs(list(out))
+
+
+class DeviceVec:
+    """Fr vector resident in HBM (qg_buf)."""
+
+    def __init__(self, dev: Device, n: int):
+        self.dev = dev
+        self.n = n
+        self.h = C.c_void_p()
+        check(lib().qg_buf_create(dev.h, n, C.byref(self.h)), dev.h)
+
+    @classmethod
+    def from_list(cls, dev: Device, xs):
+        v = cls(dev, len(xs))
+        arr = fr_array(xs)
+        check(lib().qg_buf_upload(v.h, u64p(arr), len(xs)), dev.h)
+        return v
+
+    def fill_random(self, seed: int):
+        check(lib().qg_buf_fill_random(self.h, seed), self.dev.h)
+        return self
+
+    def to_list(self, n=None):
+        n = self.n if n is None else n
+        out = np.zeros((max(n, 1), 4), dtype=np.uint64)
+        check(lib().qg_buf_download(self.h, u64p(out), n), self.dev.h)
+        return fr_list(out[:n])
+
+    def close(self):
+        if self.h:
+            lib().qg_buf_destroy(self.h)
+            self.h = C.c_void_p()
+
+    def __del__(self):
+        try:
+            self.close()
+        except Exception:
+            pass
+
+
+class Srs:
+    """Device-resident G1 bases (KZG::g1_points) + MSM window tables."""
+
+    def __init__(self, dev: Device, handle):
+        self.dev = dev
+        self.h = handle
+
+    @classmethod
+    def generate(cls, dev: Device, tau: int, n: int, g=None, offset: int = 0):
+        """bases [tau^(offset+i)] g, i < n (g = BN254 generator by default)"""
+        h = C.c_void_p()
+        gxy = None
+        if g is not None:
+            gxy, _ = g1_to_abi(g)
+        check(lib().qg_srs_generate_range(dev.h, fr_c(tau), gxy, offset, n, C.byref(h)), dev.h)
+        return cls(dev, h)
+
+    @classmethod
+    def upload(cls, dev: Device, points):
+        n = len(points)
+        xy = np.zeros((n, 8), dtype=np.uint64)
+        inf = np.zeros(n, dtype=np.uint8)
+        for i, P in enumerate(points):
+            a, f = g1_to_abi(P)
+            xy[i, :] = list(a)
+            inf[i] = f
+        h = C.c_void_p()
+        check(lib().qg_srs_upload(dev.h, u64p(xy), inf.ctypes.data_as(C.POINTER(C.c_uint8)), n,
+                                  C.byref(h)), dev.h)
+        return cls(dev, h)
+
+    def __len__(self):
+        return lib().qg_srs_len(self.h)
+
+    def download(self, offset=0, n=None):
+        n = len(self) - offset if n is None else n
+        xy = np.zeros((max(n, 1), 8), dtype=np.uint64)
+        inf = np.zeros(max(n, 1), dtype=np.uint8)
+        check(lib().qg_srs_download(self.h, offset, n, u64p(xy),
+                                    inf.ctypes.data_as(C.POINTER(C.c_uint8))), self.dev.h)
+        return [g1_from_abi(xy[i], inf[i]) for i in range(n)]
+
+    def msm(self, scalars):
+        arr = fr_array(scalars) if len(scalars) else np.zeros((1, 4), dtype=np.uint64)
+        xy = (C.c_uint64 * 8)()
+        inf = C.c_uint8()
+        check(lib().qg_msm_g1(self.dev.h, self.h, u64p(arr), len(scalars), xy, C.byref(inf)),
+              self.dev.h)
+        return g1_from_abi(xy, inf.value)
+
+    def msm_dev(self, vec: DeviceVec, n=None):
+        n = vec.n if n is None else n
+        xy = (C.c_uint64 * 8)()
+        inf = C.c_uint8()
+        check(lib().qg_msm_g1_dev(self.dev.h, self.h, vec.h, n, xy, C.byref(inf)), self.dev.h)
+        return g1_from_abi(xy, inf.value)
+
+    def close(self):
+        if self.h:
+            lib().qg_srs_destroy(self.h)
+            self.h = C.c_void_p()
+
+    def __del__(self):
+        try:
+            self.close()
+        except Exception:
+            pass

@@ -1,0 +1,80 @@
+"""Conversions between canonical Python ints and the ABI's limb layout
+(4 x u64 little-endian Montgomery limbs, R = 2^256 — arkworks' in-memory form)."""
+from __future__ import annotations
+
+import ctypes as C
+
+import numpy as np
+
+R_MOD = 21888242871839275222246405745257275088548364400416034343698204186575808495617
+P_MOD = 21888242871839275222246405745257275088696311157297823662689037894645226208583
+_R = 1 << 256
+_M64 = (1 << 64) - 1
+_RINV_R = pow(_R, -1, R_MOD)
+_RINV_P = pow(_R, -1, P_MOD)
+
+
+def _limbs(v: int):
+    return [(v >> (64 * i)) & _M64 for i in range(4)]
+
+
+def fr_to_mont_limbs(x: int):
+    return _limbs((x % R_MOD) * _R % R_MOD)
+
+
+def fr_from_mont_limbs(l) -> int:
+    v = int(l[0]) | (int(l[1]) << 64) | (int(l[2]) << 128) | (int(l[3]) << 192)
+    return v * _RINV_R % R_MOD
+
+
+def fq_from_mont_limbs(l) -> int:
+    v = int(l[0]) | (int(l[1]) << 64) | (int(l[2]) << 128) | (int(l[3]) << 192)
+    return v * _RINV_P % P_MOD
+
+
+def fq_to_mont_limbs(x: int):
+    return _limbs((x % P_MOD) * _R % P_MOD)
+
+
+def fr_array(xs) -> np.ndarray:
+    """list of ints -> (n, 4) uint64 Montgomery array (C-contiguous)."""
+    out = np.empty((len(xs), 4), dtype=np.uint64)
+    for i, x in enumerate(xs):
+        m = (int(x) % R_MOD) * _R % R_MOD
+        out[i, 0] = m & _M64
+        out[i, 1] = (m >> 64) & _M64
+        out[i, 2] = (m >> 128) & _M64
+        out[i, 3] = m >> 192
+    return out
+
+
+def fr_list(arr) -> list:
+    a = np.asarray(arr, dtype=np.uint64).reshape(-1, 4)
+    return [fr_from_mont_limbs(row) for row in a]
+
+
+def u64p(arr: np.ndarray):
+    assert arr.dtype == np.uint64 and arr.flags["C_CONTIGUOUS"]
+    return arr.ctypes.data_as(C.POINTER(C.c_uint64))
+
+
+def fr_c(x: int):
+    return (C.c_uint64 * 4)(*fr_to_mont_limbs(x))
+
+
+def g1_from_abi(xy, inf):
+    """ABI affine (Montgomery limbs + flag) -> canonical (x, y) or None."""
+    if inf:
+        return None
+    return (fq_from_mont_limbs(list(xy)[:4]), fq_from_mont_limbs(list(xy)[4:8]))
+
+
+def g1_to_abi(P):
+    xy = (C.c_uint64 * 8)()
+    if P is None:
+        return xy, 1
+    lx, ly = fq_to_mont_limbs(P[0]), fq_to_mont_limbs(P[1])
+    for i in range(4):
+        xy[i] = lx[i]
+        xy[4 + i] = ly[i]
+    return xy, 0

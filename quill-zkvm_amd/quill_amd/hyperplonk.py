@@ -1,0 +1,235 @@
+"""hyperplonk mirror: VirtualPolyExpr / VirtualPolynomialStore
+(hyperplonk/src/utils/virtual_polynomial.rs), SumcheckProof
+(hyperplonk/src/piops/sumcheck.rs) and ZeroCheckProof
+(hyperplonk/src/piops/zerocheck.rs), proving on the gfx950 kernels through the
+C-ABI.  Canonical Python ints for field elements."""
+from __future__ import annotations
+
+import ctypes as C
+from dataclasses import dataclass
+
+import numpy as np
+
+from ._lib import ExprOp, check, lib
+from .device import Device, DeviceVec
+from .field import R_MOD, fr_array, fr_c, fr_list, u64p
+from .pcs import EvaluationClaim
+from .transcript import Transcript
+
+OP_INPUT, OP_CONST, OP_ADD, OP_MUL = 0, 1, 2, 3
+
+
+class VirtualPolyExpr:
+    """virtual_polynomial.rs:9-18 (Input / Const / Add / Mul); Sub is
+    Add(a, Mul(Const(-1), b)) as at :67-77."""
+
+    def __init__(self, kind, *args):
+        self.kind, self.args = kind, args
+
+    @staticmethod
+    def Input(i):
+        return VirtualPolyExpr("in", i)
+
+    @staticmethod
+    def Const(c):
+        return VirtualPolyExpr("const", c % R_MOD)
+
+    def __add__(self, o):
+        return VirtualPolyExpr("add", self, o)
+
+    def __mul__(self, o):
+        return VirtualPolyExpr("mul", self, o)
+
+    def __sub__(self, o):
+        return VirtualPolyExpr("add", self, VirtualPolyExpr("mul", VirtualPolyExpr.Const(-1), o))
+
+    def evaluate(self, g):
+        """virtual_polynomial.rs:22-37"""
+        if self.kind == "in":
+            return g[self.args[0]] % R_MOD
+        if self.kind == "const":
+            return self.args[0]
+        a, b = self.args[0].evaluate(g), self.args[1].evaluate(g)
+        return (a + b) % R_MOD if self.kind == "add" else a * b % R_MOD
+
+    def to_program(self):
+        """postfix program (qg_expr_op[]) + constant pool"""
+        ops, consts = [], []
+
+        def rec(e):
+            if e.kind == "in":
+                ops.append((OP_INPUT, e.args[0]))
+            elif e.kind == "const":
+                ops.append((OP_CONST, len(consts)))
+                consts.append(e.args[0])
+            else:
+                rec(e.args[0])
+                rec(e.args[1])
+                ops.append((OP_ADD if e.kind == "add" else OP_MUL, 0))
+
+        rec(self)
+        return ops, consts
+
+
+def _program_c(expr: VirtualPolyExpr):
+    ops, consts = expr.to_program()
+    prog = (ExprOp * len(ops))(*[ExprOp(o, a) for o, a in ops])
+    carr = fr_array(consts) if consts else np.zeros((1, 4), dtype=np.uint64)
+    return prog, len(ops), carr, len(consts)
+
+
+def expr_degree(expr: VirtualPolyExpr) -> int:
+    prog, n, _, _ = _program_c(expr)
+    d = C.c_uint32()
+    check(lib().qg_expr_degree(prog, n, C.byref(d)))
+    return d.value
+
+
+class VirtualPolynomialStore:
+    """virtual_polynomial.rs:142-331.  Tables are lists of canonical ints."""
+
+    def __init__(self, num_vars: int):
+        self.num_vars = num_vars
+        self.polynomials = []
+        self.virtual_polys = []
+
+    def allocate_polynomial(self, evals):
+        assert len(evals) == 1 << self.num_vars, \
+            "Input polynomial evaluations length does not match number of variables"
+        self.polynomials.append([int(e) % R_MOD for e in evals])
+        return len(self.polynomials) - 1
+
+    def new_virtual_from_input(self, g):
+        self.virtual_polys.append(VirtualPolyExpr.Input(g))
+        return len(self.virtual_polys) - 1
+
+    def new_virtual_from_virtual(self, v):
+        self.virtual_polys.append(self.virtual_polys[v])
+        return len(self.virtual_polys) - 1
+
+    def new_virtual_from_expr(self, e):
+        self.virtual_polys.append(e)
+        return len(self.virtual_polys) - 1
+
+    def add_in_place(self, f, g):
+        self.virtual_polys[f] = self.virtual_polys[f] + VirtualPolyExpr.Input(g)
+
+    def add_const_in_place(self, f, c):
+        self.virtual_polys[f] = self.virtual_polys[f] + VirtualPolyExpr.Const(c)
+
+    def sub_in_place(self, f, g):
+        self.virtual_polys[f] = self.virtual_polys[f] + (
+            VirtualPolyExpr.Const(-1) * VirtualPolyExpr.Input(g))
+
+    def mul_in_place(self, f, g):
+        self.virtual_polys[f] = self.virtual_polys[f] * VirtualPolyExpr.Input(g)
+
+    def mul_const_in_place(self, f, c):
+        self.virtual_polys[f] = self.virtual_polys[f] * VirtualPolyExpr.Const(c)
+
+    def evaluate_point(self, g_evals, h):
+        return self.virtual_polys[h].evaluate(g_evals)
+
+
+def _tables_c(tables):
+    arrs = [fr_array(t) for t in tables]
+    ptrs = (C.POINTER(C.c_uint64) * max(len(arrs), 1))(*[u64p(a) for a in arrs])
+    return arrs, ptrs
+
+
+def _unpack(nvars, width, coeffs, lens, point, ev):
+    from .field import fr_from_mont_limbs
+    r_polys = []
+    c = coeffs.reshape(nvars, width, 4)
+    for j in range(nvars):
+        r_polys.append([fr_from_mont_limbs(c[j, i]) for i in range(lens[j])])
+    pt = fr_list(point)
+    return r_polys, pt, fr_from_mont_limbs(list(ev))
+
+
+@dataclass
+class SumcheckProof:
+    """sumcheck.rs:15-19"""
+    num_vars: int
+    claimed_sum: int
+    r_polys: list
+
+    @staticmethod
+    def prove(num_vars, store: VirtualPolynomialStore, h, claimed_sum, transcript: Transcript,
+              dev: Device = None):
+        """sumcheck.rs:28-114 on the device; returns (proof, EvaluationClaim)."""
+        dev = dev or _default_device()
+        expr = store.virtual_polys[h]
+        prog, plen, carr, nc = _program_c(expr)
+        width = expr_degree(expr) + 1
+        arrs, ptrs = _tables_c(store.polynomials)
+        coeffs = np.zeros((num_vars * width, 4), dtype=np.uint64)
+        lens = np.zeros(num_vars, dtype=np.uint32)
+        point = np.zeros((num_vars, 4), dtype=np.uint64)
+        ev = (C.c_uint64 * 4)()
+        check(lib().qg_sumcheck_prove(
+            dev.h, num_vars, len(arrs), ptrs, prog, plen, u64p(carr), nc, fr_c(claimed_sum),
+            transcript.c_state(), u64p(coeffs), lens.ctypes.data_as(C.POINTER(C.c_uint32)),
+            u64p(point), ev), dev.h)
+        r_polys, pt, e = _unpack(num_vars, width, coeffs, lens, point, ev)
+        return SumcheckProof(num_vars, claimed_sum % R_MOD, r_polys), EvaluationClaim(pt, e)
+
+
+@dataclass
+class ZeroCheckProof:
+    """zerocheck.rs:8-11"""
+    num_vars: int
+    sumcheck_proof: SumcheckProof
+
+    @staticmethod
+    def prove(store: VirtualPolynomialStore, h, transcript: Transcript, dev: Device = None):
+        """zerocheck.rs:14-49 on the device.  Mutates `store` exactly like the
+        reference: appends the eq table and the virtual polynomial h * eq."""
+        dev = dev or _default_device()
+        n = store.num_vars
+        expr = store.virtual_polys[h]
+        prog, plen, carr, nc = _program_c(expr)
+        width = expr_degree(expr) + 2
+        arrs, ptrs = _tables_c(store.polynomials)
+        coeffs = np.zeros((n * width, 4), dtype=np.uint64)
+        lens = np.zeros(n, dtype=np.uint32)
+        point = np.zeros((n, 4), dtype=np.uint64)
+        eq = np.zeros((1 << n, 4), dtype=np.uint64)
+        ev = (C.c_uint64 * 4)()
+        check(lib().qg_zerocheck_prove(
+            dev.h, n, len(arrs), ptrs, prog, plen, u64p(carr), nc, transcript.c_state(),
+            u64p(coeffs), lens.ctypes.data_as(C.POINTER(C.c_uint32)), u64p(point), ev,
+            u64p(eq)), dev.h)
+        # store mutation of zerocheck.rs:27-29
+        eq_idx = store.allocate_polynomial(fr_list(eq))
+        h_hat = store.new_virtual_from_virtual(h)
+        store.mul_in_place(h_hat, eq_idx)
+        r_polys, pt, e = _unpack(n, width, coeffs, lens, point, ev)
+        return (ZeroCheckProof(n, SumcheckProof(n, 0, r_polys)), EvaluationClaim(pt, e))
+
+
+def sumcheck_prove_device(dev: Device, num_vars: int, tables, expr: VirtualPolyExpr,
+                          claimed_sum: int, transcript: Transcript):
+    """Device-resident variant (tables are DeviceVec): the bench entry point."""
+    prog, plen, carr, nc = _program_c(expr)
+    width = expr_degree(expr) + 1
+    ptrs = (C.c_void_p * len(tables))(*[t.h for t in tables])
+    coeffs = np.zeros((num_vars * width, 4), dtype=np.uint64)
+    lens = np.zeros(num_vars, dtype=np.uint32)
+    point = np.zeros((num_vars, 4), dtype=np.uint64)
+    ev = (C.c_uint64 * 4)()
+    check(lib().qg_sumcheck_prove_dev(
+        dev.h, num_vars, len(tables), ptrs, prog, plen, u64p(carr), nc, fr_c(claimed_sum),
+        transcript.c_state(), u64p(coeffs), lens.ctypes.data_as(C.POINTER(C.c_uint32)),
+        u64p(point), ev), dev.h)
+    return coeffs, lens, point, ev
+
+
+_DEV = None
+
+
+def _default_device():
+    global _DEV
+    if _DEV is None:
+        _DEV = Device(0)
+    return _DEV
