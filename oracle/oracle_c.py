@@ -1,0 +1,122 @@
+"""ctypes wrapper of the oracle's C restatement (oracle/oracle_c.c) —
+TEST INFRASTRUCTURE ONLY (checker + bench.py's cpu_baseline leg)."""
+from __future__ import annotations
+
+import ctypes as C
+import os
+import platform
+
+HERE = os.path.dirname(os.path.abspath(__file__))
+LIB = os.path.join(HERE, "_build", "liboracle_c.so")
+_lib = None
+
+R_MOD = 21888242871839275222246405745257275088548364400416034343698204186575808495617
+P_MOD = 21888242871839275222246405745257275088696311157297823662689037894645226208583
+_M64 = (1 << 64) - 1
+
+
+def lib():
+    global _lib
+    if _lib is None:
+        if not os.path.exists(LIB):
+            raise FileNotFoundError(f"{LIB} missing (make -C oracle)")
+        L = C.CDLL(LIB)
+        U64P = C.POINTER(C.c_uint64)
+        L.oc_msm.argtypes = [U64P, C.POINTER(C.c_uint8), U64P, C.c_size_t, U64P,
+                             C.POINTER(C.c_uint8)]
+        L.oc_bench_msm.argtypes = [C.c_int, C.c_uint64, C.POINTER(C.c_double),
+                                   C.POINTER(C.c_double), U64P]
+        L.oc_sumcheck_prod.argtypes = [C.c_int, C.c_int, U64P, U64P, C.POINTER(C.c_uint8), U64P,
+                                       C.POINTER(C.c_uint32), U64P, U64P]
+        L.oc_bench_sumcheck.argtypes = [C.c_int, C.c_uint64, C.POINTER(C.c_double)]
+        _lib = L
+    return _lib
+
+
+def _mont(x, m):
+    v = (x % m) * (1 << 256) % m
+    return [(v >> (64 * i)) & _M64 for i in range(4)]
+
+
+def _unmont(l, m):
+    v = sum(int(l[i]) << (64 * i) for i in range(4))
+    return v * pow(1 << 256, -1, m) % m
+
+
+def msm(bases, scalars):
+    """sum scalars[i] * bases[i] (affine canonical tuples / None) via the C Pippenger."""
+    n = min(len(bases), len(scalars))
+    xy = (C.c_uint64 * (8 * max(n, 1)))()
+    inf = (C.c_uint8 * max(n, 1))()
+    sc = (C.c_uint64 * (4 * max(n, 1)))()
+    for i in range(n):
+        P = bases[i]
+        if P is None:
+            inf[i] = 1
+        else:
+            for k, v in enumerate(_mont(P[0], P_MOD) + _mont(P[1], P_MOD)):
+                xy[8 * i + k] = v
+        for k, v in enumerate(_mont(scalars[i], R_MOD)):
+            sc[4 * i + k] = v
+    out = (C.c_uint64 * 8)()
+    oinf = C.c_uint8()
+    lib().oc_msm(xy, inf, sc, n, out, C.byref(oinf))
+    if oinf.value:
+        return None
+    return (_unmont(out[:4], P_MOD), _unmont(out[4:8], P_MOD))
+
+
+def sumcheck_prod(nvars, tables, claimed, state: bytes):
+    """h = prod tables; returns (r_polys, point, evaluation, new_state)."""
+    k = len(tables)
+    N = 1 << nvars
+    t = (C.c_uint64 * (4 * N * k))()
+    for i, tb in enumerate(tables):
+        for j, x in enumerate(tb):
+            for q, v in enumerate(_mont(x, R_MOD)):
+                t[4 * (i * N + j) + q] = v
+    st = (C.c_uint8 * 32).from_buffer_copy(state)
+    co = (C.c_uint64 * (4 * nvars * (k + 1)))()
+    lens = (C.c_uint32 * nvars)()
+    pt = (C.c_uint64 * (4 * nvars))()
+    ev = (C.c_uint64 * 4)()
+    cl = (C.c_uint64 * 4)(*_mont(claimed, R_MOD))
+    lib().oc_sumcheck_prod(nvars, k, t, cl, st, co, lens, pt, ev)
+    r_polys = [[_unmont(co[4 * (j * (k + 1) + i):4 * (j * (k + 1) + i) + 4], R_MOD)
+                for i in range(lens[j])] for j in range(nvars)]
+    point = [_unmont(pt[4 * j:4 * j + 4], R_MOD) for j in range(nvars)]
+    return r_polys, point, _unmont(ev[:], R_MOD), bytes(st)
+
+
+def cpu_model():
+    try:
+        with open("/proc/cpuinfo") as f:
+            for line in f:
+                if line.startswith("model name"):
+                    return line.split(":", 1)[1].strip()
+    except OSError:
+        pass
+    return platform.processor()
+
+
+def bench_msm_baseline(log_n: int = 18, seed: int = 0x5155494C4C):
+    """Single-thread arkworks-faithful Pippenger on a 2^log_n sample (the
+    reference has no rayon, so one core is the reference configuration)."""
+    tm, tc = C.c_double(), C.c_double()
+    out = (C.c_uint64 * 8)()
+    lib().oc_bench_msm(log_n, seed, C.byref(tm), C.byref(tc), out)
+    n = 1 << log_n
+    return {"value": n / tm.value, "unit": "scalars/s", "cores": 1, "kind": "port",
+            "sample": f"one MSM of 2^{log_n} uniform Fr scalars over [tau^i]g bases, "
+                      f"msm_unchecked only ({tm.value:.2f} s); KZG::commit as written "
+                      f"(+ into_affine of every SRS point) {n / tc.value:.4g} scalars/s",
+            "seconds": tm.value, "kzg_commit_as_written_scalars_per_s": n / tc.value,
+            "cpu_model": cpu_model()}
+
+
+def bench_sumcheck_baseline(log_n: int = 16, seed: int = 0x5155494C4C):
+    s = C.c_double()
+    lib().oc_bench_sumcheck(log_n, seed, C.byref(s))
+    return {"ms": s.value * 1e3, "cores": 1, "kind": "port",
+            "sample": f"evaluation-form sumcheck prover, h = g1*g2*g3 at 2^{log_n} vars "
+                      f"(lower bound on the reference's per-pair DensePolynomial structure)"}

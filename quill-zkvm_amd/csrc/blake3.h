@@ -223,6 +223,85 @@ using Blake3 = Blake3T<54>;
 #endif
 
 // ---------------------------------------------------------------------------
+// Word-oriented single-chunk BLAKE3 (input <= 1024 bytes, given as LE 32-bit
+// words, tail bytes of the last word zero).  This is the device fast path of
+// the transcript: no byte arrays, no private-memory buffers.
+// ---------------------------------------------------------------------------
+template <class Src>
+QG_HD void b3_chunk_words(const Src& src, uint32_t nbytes, uint32_t* out, int nout_words) {
+  uint32_t cv[8];
+#pragma unroll
+  for (int i = 0; i < 8; i++) cv[i] = b3_iv(i);
+  const uint32_t nblocks = nbytes ? (nbytes + 63) / 64 : 1;
+  for (uint32_t b = 0; b < nblocks; b++) {
+    uint32_t blk[16];
+    const uint32_t base = b * 16;
+    const uint32_t nw = (nbytes + 3) / 4;
+#pragma unroll
+    for (int i = 0; i < 16; i++) blk[i] = (base + i < nw) ? src(base + i) : 0u;
+    const uint32_t blen = (b + 1 < nblocks) ? 64u : nbytes - b * 64;
+    uint32_t flags = (b == 0 ? B3_CHUNK_START : 0u);
+    if (b + 1 < nblocks) {
+      uint32_t o[16];
+      b3_compress(cv, blk, 0, blen, flags, o);
+#pragma unroll
+      for (int i = 0; i < 8; i++) cv[i] = o[i];
+    } else {
+      flags |= B3_CHUNK_END | B3_ROOT;
+      for (int oc = 0; oc * 16 < nout_words; oc++) {
+        uint32_t o[16];
+        b3_compress(cv, blk, (uint64_t)oc, blen, flags, o);
+        for (int i = 0; i < 16 && oc * 16 + i < nout_words; i++) out[oc * 16 + i] = o[i];
+      }
+    }
+  }
+}
+
+struct B3ArrSrc {
+  const uint32_t* p;
+  QG_HD uint32_t operator()(uint32_t i) const { return p[i]; }
+};
+
+// Absorb a word message into an 8-word state: state = B3(state || msg)
+QG_HD void transcript_append_words(uint32_t st[8], const uint32_t* msg, uint32_t nbytes_msg) {
+  // nbytes_msg must be a multiple of 4 here
+  struct Src {
+    const uint32_t* s;
+    const uint32_t* m;
+    QG_HD uint32_t operator()(uint32_t i) const { return i < 8 ? s[i] : m[i - 8]; }
+  } src{st, msg};
+  uint32_t o[8];
+  b3_chunk_words(src, 32 + nbytes_msg, o, 8);
+#pragma unroll
+  for (int i = 0; i < 8; i++) st[i] = o[i];
+}
+
+// draw_field_element on a word state (transcript.rs:48-74)
+QG_HD Fr transcript_draw_fr_words(uint32_t st[8]) {
+  struct Src {
+    const uint32_t* s;
+    QG_HD uint32_t operator()(uint32_t i) const {
+      // state || "challenge" (9 bytes)
+      if (i < 8) return s[i];
+      if (i == 8) return 0x6c616863u;  // "chal"
+      if (i == 9) return 0x676e656cu;  // "leng"
+      return 0x00000065u;              // "e"
+    }
+  } src{st};
+  uint32_t ch[12];
+  b3_chunk_words(src, 41, ch, 12);
+  transcript_append_words(st, ch, 48);
+  Fr lo, hi;
+#pragma unroll
+  for (int i = 0; i < 8; i++) lo.v[i] = ch[i];
+#pragma unroll
+  for (int i = 0; i < 4; i++) hi.v[i] = ch[8 + i];
+#pragma unroll
+  for (int i = 4; i < 8; i++) hi.v[i] = 0;
+  return lo * Fr::from_raw(FrP::R2) + hi * Fr::from_raw(FrP::R3);
+}
+
+// ---------------------------------------------------------------------------
 // Transcript primitives over a 32-byte state
 // ---------------------------------------------------------------------------
 QG_HD void transcript_init(uint8_t state[32], const uint8_t* domain, size_t len) {

@@ -25,8 +25,7 @@ using namespace qg;
 
 namespace qg {
 
-static constexpr int MSM_E = 32;        // entries per accumulation thread
-static constexpr int MSM_SEG = 16;      // buckets per reduction segment
+static constexpr int MSM_SEG = 8;       // buckets per reduction segment
 static constexpr int MSM_BLOCK = 256;
 
 // window size for an SRS of n bases (tuned later)
@@ -67,21 +66,205 @@ QG_DEV void for_each_digit(const Fr& mont_scalar, int c, int W, Emit&& emit) {
   }
 }
 
-__global__ void k_msm_count(const Fr* __restrict__ scalars, size_t n, int c, int W,
-                            uint32_t* __restrict__ counts) {
-  size_t i = (size_t)blockIdx.x * blockDim.x + threadIdx.x;
-  if (i >= n) return;
-  for_each_digit(scalars[i], c, W, [&](int, uint32_t b, bool) { atomicAdd(&counts[b], 1u); });
+// ---- bucketing: two-pass LDS-histogram radix sort ------------------------
+// Bucket id b (BB = c-1 bits) = (g << LO) | l.  Pass A partitions digits by the
+// high part g with per-block LDS histograms (no per-digit global atomics);
+// pass B sorts every group by l in chunks of SORT_CHUNK entries, so a heavy
+// group (skewed scalars, the short top window) spreads over many blocks.
+static constexpr int SORT_BLOCK = 256;
+static constexpr int SORT_SPT = 8;                          // scalars per thread (pass A)
+static constexpr int SORT_TILE = SORT_BLOCK * SORT_SPT;     // scalars per block
+static constexpr int SORT_CHUNK = 8192;                     // entries per block (pass B)
+
+__global__ void __launch_bounds__(SORT_BLOCK)
+    k_sortA_hist(const Fr* __restrict__ scalars, size_t n, int c, int W, int LO, int H,
+                 uint32_t nblk, uint32_t* __restrict__ ghist) {
+  extern __shared__ uint32_t hist[];
+  for (int g = threadIdx.x; g < H; g += blockDim.x) hist[g] = 0;
+  __syncthreads();
+  const size_t base = (size_t)blockIdx.x * SORT_TILE;
+  for (int k = 0; k < SORT_SPT; k++) {
+    size_t i = base + (size_t)k * SORT_BLOCK + threadIdx.x;
+    if (i < n)
+      for_each_digit(scalars[i], c, W, [&](int, uint32_t b, bool) { atomicAdd(&hist[b >> LO], 1u); });
+  }
+  __syncthreads();
+  for (int g = threadIdx.x; g < H; g += blockDim.x) ghist[(size_t)g * nblk + blockIdx.x] = hist[g];
 }
 
-__global__ void k_msm_scatter(const Fr* __restrict__ scalars, size_t n, size_t N, int c, int W,
-                              uint32_t* __restrict__ cursor, uint32_t* __restrict__ entries) {
-  size_t i = (size_t)blockIdx.x * blockDim.x + threadIdx.x;
-  if (i >= n) return;
-  for_each_digit(scalars[i], c, W, [&](int w, uint32_t b, bool neg) {
-    uint32_t pos = atomicAdd(&cursor[b], 1u);
-    entries[pos] = (uint32_t)((size_t)w * N + i) | (neg ? 0x80000000u : 0u);
-  });
+__global__ void __launch_bounds__(SORT_BLOCK)
+    k_sortA_scatter(const Fr* __restrict__ scalars, size_t n, size_t N, int c, int W, int LO, int H,
+                    uint32_t nblk, const uint32_t* __restrict__ goff,
+                    unsigned long long* __restrict__ tmp) {
+  extern __shared__ uint32_t cur[];
+  for (int g = threadIdx.x; g < H; g += blockDim.x) cur[g] = goff[(size_t)g * nblk + blockIdx.x];
+  __syncthreads();
+  const size_t base = (size_t)blockIdx.x * SORT_TILE;
+  for (int k = 0; k < SORT_SPT; k++) {
+    size_t i = base + (size_t)k * SORT_BLOCK + threadIdx.x;
+    if (i < n)
+      for_each_digit(scalars[i], c, W, [&](int w, uint32_t b, bool neg) {
+        uint32_t pos = atomicAdd(&cur[b >> LO], 1u);
+        uint32_t ent = (uint32_t)((size_t)w * N + i) | (neg ? 0x80000000u : 0u);
+        tmp[pos] = ((unsigned long long)b << 32) | ent;
+      });
+  }
+}
+
+// groups -> chunks (single block): gstart[g] = goff[g*nblk], chunk bases, chunk->group map
+__global__ void __launch_bounds__(1024)
+    k_sort_chunks(const uint32_t* __restrict__ goff, uint32_t nblk, int H,
+                  uint32_t* __restrict__ gstart, uint32_t* __restrict__ cbase,
+                  uint32_t* __restrict__ chunk_group, uint32_t* __restrict__ nchunks_out) {
+  __shared__ uint32_t sh[1024];
+  const int g = threadIdx.x;
+  const uint32_t total = goff[(size_t)H * nblk];
+  uint32_t gs = 0, ge = 0, nch = 0;
+  if (g < H) {
+    gs = goff[(size_t)g * nblk];
+    ge = (g + 1 < H) ? goff[(size_t)(g + 1) * nblk] : total;
+    nch = (ge - gs + SORT_CHUNK - 1) / SORT_CHUNK;
+    gstart[g] = gs;
+  }
+  sh[threadIdx.x] = nch;
+  __syncthreads();
+  for (int off = 1; off < 1024; off <<= 1) {
+    uint32_t add = threadIdx.x >= (unsigned)off ? sh[threadIdx.x - off] : 0u;
+    __syncthreads();
+    sh[threadIdx.x] += add;
+    __syncthreads();
+  }
+  const uint32_t cb = sh[threadIdx.x] - nch;
+  if (g < H) {
+    cbase[g] = cb;
+    for (uint32_t k = 0; k < nch; k++) chunk_group[cb + k] = (uint32_t)g;
+  }
+  if (threadIdx.x == 1023) {
+    gstart[H] = total;
+    cbase[H] = sh[1023];
+    *nchunks_out = sh[1023];
+  }
+}
+
+__global__ void __launch_bounds__(SORT_BLOCK)
+    k_sortB_hist(const unsigned long long* __restrict__ tmp, const uint32_t* __restrict__ gstart,
+                 const uint32_t* __restrict__ cbase, const uint32_t* __restrict__ chunk_group,
+                 const uint32_t* __restrict__ nchunks, int NL, uint32_t* __restrict__ chist) {
+  extern __shared__ uint32_t hist[];
+  const uint32_t k = blockIdx.x;
+  if (k >= *nchunks) return;
+  const uint32_t g = chunk_group[k];
+  const uint32_t s = gstart[g] + (k - cbase[g]) * SORT_CHUNK;
+  const uint32_t e = min(s + SORT_CHUNK, gstart[g + 1]);
+  for (int l = threadIdx.x; l < NL; l += blockDim.x) hist[l] = 0;
+  __syncthreads();
+  for (uint32_t p = s + threadIdx.x; p < e; p += blockDim.x)
+    atomicAdd(&hist[(uint32_t)(tmp[p] >> 32) & (NL - 1)], 1u);
+  __syncthreads();
+  for (int l = threadIdx.x; l < NL; l += blockDim.x) chist[(size_t)k * NL + l] = hist[l];
+}
+
+// per bucket b = (g, l): total count over the group's chunks
+__global__ void k_sort_bucket_count(const uint32_t* __restrict__ cbase, const uint32_t* __restrict__ chist,
+                                    int LO, uint32_t nb, uint32_t* __restrict__ counts) {
+  const uint32_t b = blockIdx.x * blockDim.x + threadIdx.x;
+  if (b >= nb) return;
+  const uint32_t g = b >> LO, l = b & ((1u << LO) - 1);
+  uint32_t c = 0;
+  for (uint32_t k = cbase[g]; k < cbase[g + 1]; k++) c += chist[((size_t)k << LO) + l];
+  counts[b] = c;
+}
+
+__global__ void k_sort_chunk_offsets(const uint32_t* __restrict__ cbase, uint32_t* __restrict__ chist,
+                                     int LO, uint32_t nb, const uint32_t* __restrict__ bstart) {
+  const uint32_t b = blockIdx.x * blockDim.x + threadIdx.x;
+  if (b >= nb) return;
+  const uint32_t g = b >> LO, l = b & ((1u << LO) - 1);
+  uint32_t run = bstart[b];
+  for (uint32_t k = cbase[g]; k < cbase[g + 1]; k++) {
+    const size_t idx = ((size_t)k << LO) + l;
+    const uint32_t c = chist[idx];
+    chist[idx] = run;  // histogram -> chunk output offset (in place)
+    run += c;
+  }
+}
+
+__global__ void __launch_bounds__(SORT_BLOCK)
+    k_sortB_scatter(const unsigned long long* __restrict__ tmp, const uint32_t* __restrict__ gstart,
+                    const uint32_t* __restrict__ cbase, const uint32_t* __restrict__ chunk_group,
+                    const uint32_t* __restrict__ nchunks, int NL, const uint32_t* __restrict__ coff,
+                    uint32_t* __restrict__ entries) {
+  extern __shared__ uint32_t cur[];
+  const uint32_t k = blockIdx.x;
+  if (k >= *nchunks) return;
+  const uint32_t g = chunk_group[k];
+  const uint32_t s = gstart[g] + (k - cbase[g]) * SORT_CHUNK;
+  const uint32_t e = min(s + SORT_CHUNK, gstart[g + 1]);
+  for (int l = threadIdx.x; l < NL; l += blockDim.x) cur[l] = coff[(size_t)k * NL + l];
+  __syncthreads();
+  for (uint32_t p = s + threadIdx.x; p < e; p += blockDim.x) {
+    const unsigned long long v = tmp[p];
+    const uint32_t pos = atomicAdd(&cur[(uint32_t)(v >> 32) & (NL - 1)], 1u);
+    entries[pos] = (uint32_t)v;
+  }
+}
+
+// ---- generic exclusive scan of uint32 (out[n] = total) -------------------
+__global__ void k_scan32_tiles(const uint32_t* __restrict__ in, size_t n, uint32_t* __restrict__ out,
+                               uint32_t* __restrict__ tile_tot) {
+  __shared__ uint32_t sh[256];
+  const size_t base = ((size_t)blockIdx.x * 256 + threadIdx.x) * 8;
+  uint32_t v[8], tot = 0;
+  for (int k = 0; k < 8; k++) {
+    v[k] = base + k < n ? in[base + k] : 0u;
+    tot += v[k];
+  }
+  sh[threadIdx.x] = tot;
+  __syncthreads();
+  for (int off = 1; off < 256; off <<= 1) {
+    uint32_t add = threadIdx.x >= (unsigned)off ? sh[threadIdx.x - off] : 0u;
+    __syncthreads();
+    sh[threadIdx.x] += add;
+    __syncthreads();
+  }
+  uint32_t run = sh[threadIdx.x] - tot;
+  for (int k = 0; k < 8; k++) {
+    if (base + k < n) out[base + k] = run;
+    run += v[k];
+  }
+  if (threadIdx.x == 255) tile_tot[blockIdx.x] = sh[255];
+}
+
+__global__ void __launch_bounds__(1024)
+    k_scan32_top(uint32_t* __restrict__ tile_tot, int ntiles, uint32_t* __restrict__ out_total) {
+  __shared__ uint32_t sh[1024];
+  const int per = (ntiles + 1023) / 1024;
+  const int base = threadIdx.x * per;
+  uint32_t tot = 0;
+  for (int k = 0; k < per; k++)
+    if (base + k < ntiles) tot += tile_tot[base + k];
+  sh[threadIdx.x] = tot;
+  __syncthreads();
+  for (int off = 1; off < 1024; off <<= 1) {
+    uint32_t add = threadIdx.x >= (unsigned)off ? sh[threadIdx.x - off] : 0u;
+    __syncthreads();
+    sh[threadIdx.x] += add;
+    __syncthreads();
+  }
+  uint32_t run = sh[threadIdx.x] - tot;
+  for (int k = 0; k < per; k++) {
+    if (base + k < ntiles) {
+      uint32_t t = tile_tot[base + k];
+      tile_tot[base + k] = run;
+      run += t;
+    }
+  }
+  if (threadIdx.x == 1023) *out_total = sh[1023];
+}
+
+__global__ void k_scan32_add(const uint32_t* __restrict__ tile_off, size_t n, uint32_t* __restrict__ out) {
+  const size_t i = (size_t)blockIdx.x * blockDim.x + threadIdx.x;
+  if (i < n) out[i] += tile_off[i / 2048];
 }
 
 // ---- exclusive scan of (count, ceil(count/E)) over nb buckets -------------
@@ -89,24 +272,28 @@ static constexpr int SCAN_PER_THREAD = 8;
 static constexpr int SCAN_BLOCK = 256;
 static constexpr int SCAN_TILE = SCAN_PER_THREAD * SCAN_BLOCK;
 
-__device__ __forceinline__ uint2 scan_val(const uint32_t* counts, size_t i, size_t nb) {
+// entries per accumulation thread = 2^elog (chosen per call, see msm_device)
+__device__ __forceinline__ uint2 scan_val(const uint32_t* counts, size_t i, size_t nb, int elog) {
   uint32_t c = i < nb ? counts[i] : 0u;
-  return make_uint2(c, (c + MSM_E - 1) / MSM_E);
+  return make_uint2(c, (c + (1u << elog) - 1) >> elog);
 }
 
 // per-tile exclusive scan; writes tile totals
-__global__ void k_scan_tiles(const uint32_t* __restrict__ counts, size_t nb,
+__global__ void k_scan_tiles(const uint32_t* __restrict__ counts, size_t nb, int elog,
                              uint32_t* __restrict__ bstart, uint32_t* __restrict__ tstart,
-                             uint2* __restrict__ tile_tot) {
+                             uint2* __restrict__ tile_tot, uint32_t* __restrict__ max_tpb) {
   __shared__ uint2 sh[SCAN_BLOCK];
   size_t base = (size_t)blockIdx.x * SCAN_TILE + threadIdx.x * SCAN_PER_THREAD;
   uint2 v[SCAN_PER_THREAD];
   uint2 tot = make_uint2(0, 0);
+  uint32_t mx = 0;
   for (int k = 0; k < SCAN_PER_THREAD; k++) {
-    v[k] = scan_val(counts, base + k, nb);
+    v[k] = scan_val(counts, base + k, nb, elog);
     tot.x += v[k].x;
     tot.y += v[k].y;
+    mx = max(mx, v[k].y);
   }
+  if (mx > 1) atomicMax(max_tpb, mx);
   sh[threadIdx.x] = tot;
   __syncthreads();
   // Hillis-Steele inclusive scan of thread totals
@@ -182,7 +369,8 @@ __global__ void k_scan_add(const uint2* __restrict__ tile_off, size_t nb, uint32
 __global__ void __launch_bounds__(MSM_BLOCK)
     k_msm_accumulate(const G1Affine* __restrict__ table, const uint32_t* __restrict__ entries,
                      const uint32_t* __restrict__ bstart, const uint32_t* __restrict__ tstart,
-                     uint32_t nb, G1Xyzz* __restrict__ partial) {
+                     uint32_t nb, int elog, G1Xyzz* __restrict__ partial,
+                     uint32_t* __restrict__ owner) {
   const uint32_t t = blockIdx.x * blockDim.x + threadIdx.x;
   const uint32_t total = tstart[nb];
   if (t >= total) return;
@@ -194,8 +382,8 @@ __global__ void __launch_bounds__(MSM_BLOCK)
     else hi = mid;
   }
   const uint32_t b = lo;
-  const uint32_t e0 = bstart[b] + (t - tstart[b]) * MSM_E;
-  uint32_t e1 = e0 + MSM_E;
+  const uint32_t e0 = bstart[b] + ((t - tstart[b]) << elog);
+  uint32_t e1 = e0 + (1u << elog);
   const uint32_t bend = bstart[b + 1];
   if (e1 > bend) e1 = bend;
   G1Xyzz acc = G1Xyzz::infinity();
@@ -206,6 +394,19 @@ __global__ void __launch_bounds__(MSM_BLOCK)
     acc = xyzz_add_affine(acc, p);
   }
   partial[t] = acc;
+  owner[t] = b;
+}
+
+// Segmented pairwise tree over bucket partials: after the steps s = 1, 2, 4, ...
+// partial[tstart[j]] holds bucket j's sum.  Depth log2(max partials per bucket).
+__global__ void k_msm_tree_step(G1Xyzz* __restrict__ partial, const uint32_t* __restrict__ owner,
+                                const uint32_t* __restrict__ tstart, uint32_t nb, uint32_t s) {
+  const uint32_t t = blockIdx.x * blockDim.x + threadIdx.x;
+  if (t >= tstart[nb]) return;
+  const uint32_t b = owner[t];
+  const uint32_t off = t - tstart[b];
+  if ((off & (2 * s - 1)) == 0 && t + s < tstart[b + 1])
+    partial[t] = xyzz_add(partial[t], partial[t + s]);
 }
 
 // ---- reduction ------------------------------------------------------------
@@ -219,22 +420,31 @@ __device__ void block_reduce_xyzz(G1Xyzz v, G1Xyzz* sh, G1Xyzz* out) {
   if (threadIdx.x == 0) *out = sh[0];
 }
 
+// B_j = bucket j's tree-combined partial (empty bucket -> infinity)
+__global__ void k_msm_combine(const G1Xyzz* __restrict__ partial, const uint32_t* __restrict__ tstart,
+                              uint32_t nb, G1Xyzz* __restrict__ buckets) {
+  const uint32_t j = blockIdx.x * blockDim.x + threadIdx.x;
+  if (j >= nb) return;
+  const uint32_t t0 = tstart[j];
+  buckets[j] = t0 < tstart[j + 1] ? partial[t0] : G1Xyzz::infinity();
+}
+
+// Segment s of MSM_SEG buckets: V_s = sum_i (lo+i+1) B_{lo+i}
+//   = [sum_i (i+1) B_{lo+i}]  (running sums from the top)  +  lo * [sum_i B_{lo+i}]
+// then a block tree reduction.
 __global__ void __launch_bounds__(MSM_BLOCK)
-    k_msm_reduce(const G1Xyzz* __restrict__ partial, const uint32_t* __restrict__ tstart,
-                 uint32_t nb, G1Xyzz* __restrict__ block_out) {
+    k_msm_reduce(const G1Xyzz* __restrict__ buckets, uint32_t nb, G1Xyzz* __restrict__ block_out) {
   __shared__ G1Xyzz sh[MSM_BLOCK];
   const uint32_t seg = blockIdx.x * blockDim.x + threadIdx.x;
   const uint32_t lo = seg * MSM_SEG;
   G1Xyzz v = G1Xyzz::infinity();
   if (lo < nb) {
-    uint32_t hi = lo + MSM_SEG < nb ? lo + MSM_SEG : nb;
-    G1Xyzz run = G1Xyzz::infinity(), acc = G1Xyzz::infinity();
-    for (uint32_t j = hi; j-- > lo;) {
-      const uint32_t t0 = tstart[j], t1 = tstart[j + 1];
-      for (uint32_t t = t0; t < t1; t++) run = xyzz_add(run, partial[t]);
+    const uint32_t hi = lo + MSM_SEG < nb ? lo + MSM_SEG : nb;
+    G1Xyzz run = buckets[hi - 1], acc = run;
+    for (uint32_t j = hi - 1; j-- > lo;) {
+      run = xyzz_add(run, buckets[j]);
       acc = xyzz_add(acc, run);
     }
-    // bucket j has weight j+1 = (j - lo + 1) + lo
     v = xyzz_add(acc, xyzz_mul_small(run, lo));
   }
   block_reduce_xyzz(v, sh, &block_out[blockIdx.x]);
@@ -331,8 +541,11 @@ static qg_srs* srs_alloc(qg_ctx* ctx, size_t n) {
   qg_srs* srs = new qg_srs();
   srs->ctx = ctx;
   srs->n = n;
-  srs->c = msm_window_bits(n);
-  srs->W = (255 + srs->c - 1) / srs->c;
+  // balanced signed windows: W = ceil(255 / c_target), c = ceil(255 / W), so the
+  // top window is not a sliver that funnels every scalar into a few buckets
+  const int ct = msm_window_bits(n);
+  srs->W = (255 + ct - 1) / ct;
+  srs->c = (255 + srs->W - 1) / srs->W;
   hipError_t e = hipMalloc(&srs->d_table, (size_t)srs->W * n * sizeof(G1Affine));
   if (e != hipSuccess) {
     delete srs;
@@ -350,6 +563,21 @@ G1Affine msm_device(qg_ctx* ctx, const qg_srs* srs, const Fr* d_scalars, size_t 
     const size_t max_entries = n * (size_t)W;
     QG_CHECK((size_t)W * srs->n < 0x80000000ull, QG_ERR_UNSUPPORTED, "SRS table index overflow");
     QG_CHECK(max_entries < 0xffffffffull, QG_ERR_UNSUPPORTED, "too many MSM entries");
+    // bucket id b = (g << LO) | l
+    const int BB = c - 1, LO = (BB + 1) / 2, HI = BB - LO;
+    const int H = 1 << HI, NL = 1 << LO;
+    const uint32_t nblk = div_up(n, SORT_TILE);
+    const size_t nghist = (size_t)H * nblk;
+    const size_t max_chunks = max_entries / SORT_CHUNK + H + 1;
+    uint32_t* ghist = ctx->scratch_as<uint32_t>("msm_ghist", nghist + 1);
+    uint32_t* goff = ctx->scratch_as<uint32_t>("msm_goff", nghist + 1);
+    uint32_t* gtiles = ctx->scratch_as<uint32_t>("msm_gtiles", div_up(nghist, 2048) + 1);
+    uint32_t* gstart = ctx->scratch_as<uint32_t>("msm_gstart", H + 1);
+    uint32_t* cbase = ctx->scratch_as<uint32_t>("msm_cbase", H + 1);
+    uint32_t* cgroup = ctx->scratch_as<uint32_t>("msm_cgroup", max_chunks);
+    uint32_t* misc = ctx->scratch_as<uint32_t>("msm_misc", 4);  // [0] nchunks, [1] max tpb
+    uint32_t* chist = ctx->scratch_as<uint32_t>("msm_chist", max_chunks * NL);
+    unsigned long long* tmp = ctx->scratch_as<unsigned long long>("msm_tmp", max_entries + 1);
     uint32_t* counts = ctx->scratch_as<uint32_t>("msm_counts", nb);
     uint32_t* bstart = ctx->scratch_as<uint32_t>("msm_bstart", nb + 1);
     uint32_t* tstart = ctx->scratch_as<uint32_t>("msm_tstart", nb + 1);
@@ -357,21 +585,56 @@ G1Affine msm_device(qg_ctx* ctx, const qg_srs* srs, const Fr* d_scalars, size_t 
     uint32_t* entries = ctx->scratch_as<uint32_t>("msm_entries", max_entries + 1);
     const int ntiles = (int)div_up(nb, SCAN_TILE);
     uint2* tile_tot = ctx->scratch_as<uint2>("msm_tiles", ntiles);
-    const size_t max_threads = max_entries / MSM_E + nb + 1;
+    // entries per accumulation thread: ~half the mean bucket load, so a bucket
+    // has ~2 partials on average while keeping >> 256 CUs of threads
+    int elog = 4;
+    while (elog < 7 && ((size_t)2 << (elog + 1)) * nb <= max_entries) elog++;
+    const size_t max_threads = (max_entries >> elog) + nb + 1;
     G1Xyzz* partial = ctx->scratch_as<G1Xyzz>("msm_partial", max_threads);
+    uint32_t* owner = ctx->scratch_as<uint32_t>("msm_owner", max_threads);
+    G1Xyzz* buckets = ctx->scratch_as<G1Xyzz>("msm_buckets", nb);
     const uint32_t nseg = div_up(nb, MSM_SEG);
     const uint32_t nred = div_up(nseg, MSM_BLOCK);
     G1Xyzz* red = ctx->scratch_as<G1Xyzz>("msm_red", nred + 1);
-    QG_CHECK(ntiles <= 1024 * 64, QG_ERR_UNSUPPORTED, "bucket count too large");
+    QG_CHECK(ntiles <= 1024 * 64 && H <= 1024 && NL <= 4096, QG_ERR_UNSUPPORTED,
+             "bucket count too large");
+    QG_CHECK(max_threads < 0xffffffffull && max_chunks < 0xffffffffull, QG_ERR_UNSUPPORTED,
+             "MSM too large");
 
     {
       QgTimed tm(ctx, "msm_bucketing");
-      QG_HIP(hipMemsetAsync(counts, 0, nb * sizeof(uint32_t), ctx->stream));
-      hipLaunchKernelGGL(k_msm_count, dim3(div_up(n, 256)), dim3(256), 0, ctx->stream, d_scalars,
-                         n, c, W, counts);
+      // pass A: partition digits by the high bucket bits
+      hipLaunchKernelGGL(k_sortA_hist, dim3(nblk), dim3(SORT_BLOCK), H * sizeof(uint32_t),
+                         ctx->stream, d_scalars, n, c, W, LO, H, nblk, ghist);
+      QG_LAUNCH_CHECK();
+      const unsigned gt = div_up(nghist, 2048);
+      QG_CHECK(gt <= 1024u * 1024u, QG_ERR_UNSUPPORTED, "histogram too large");
+      hipLaunchKernelGGL(k_scan32_tiles, dim3(gt), dim3(256), 0, ctx->stream, ghist, nghist, goff,
+                         gtiles);
+      QG_LAUNCH_CHECK();
+      hipLaunchKernelGGL(k_scan32_top, dim3(1), dim3(1024), 0, ctx->stream, gtiles, (int)gt,
+                         goff + nghist);
+      QG_LAUNCH_CHECK();
+      hipLaunchKernelGGL(k_scan32_add, dim3(div_up(nghist, 256)), dim3(256), 0, ctx->stream, gtiles,
+                         nghist, goff);
+      QG_LAUNCH_CHECK();
+      hipLaunchKernelGGL(k_sortA_scatter, dim3(nblk), dim3(SORT_BLOCK), H * sizeof(uint32_t),
+                         ctx->stream, d_scalars, n, srs->n, c, W, LO, H, nblk, goff, tmp);
+      QG_LAUNCH_CHECK();
+      // pass B: sort every group by the low bits, in chunks
+      QG_HIP(hipMemsetAsync(misc, 0, 4 * sizeof(uint32_t), ctx->stream));
+      hipLaunchKernelGGL(k_sort_chunks, dim3(1), dim3(1024), 0, ctx->stream, goff, nblk, H,
+                         gstart, cbase, cgroup, misc);
+      QG_LAUNCH_CHECK();
+      hipLaunchKernelGGL(k_sortB_hist, dim3((unsigned)max_chunks), dim3(SORT_BLOCK),
+                         NL * sizeof(uint32_t), ctx->stream, tmp, gstart, cbase, cgroup, misc, NL,
+                         chist);
+      QG_LAUNCH_CHECK();
+      hipLaunchKernelGGL(k_sort_bucket_count, dim3(div_up(nb, 256)), dim3(256), 0, ctx->stream,
+                         cbase, chist, LO, nb, counts);
       QG_LAUNCH_CHECK();
       hipLaunchKernelGGL(k_scan_tiles, dim3(ntiles), dim3(SCAN_BLOCK), 0, ctx->stream, counts,
-                         (size_t)nb, bstart, tstart, tile_tot);
+                         (size_t)nb, elog, bstart, tstart, tile_tot, misc + 1);
       QG_LAUNCH_CHECK();
       hipLaunchKernelGGL(k_scan_top, dim3(1), dim3(1024), 0, ctx->stream, tile_tot, ntiles,
                          bstart, tstart, (size_t)nb);
@@ -379,20 +642,36 @@ G1Affine msm_device(qg_ctx* ctx, const qg_srs* srs, const Fr* d_scalars, size_t 
       hipLaunchKernelGGL(k_scan_add, dim3(div_up(nb, 256)), dim3(256), 0, ctx->stream, tile_tot,
                          (size_t)nb, bstart, tstart, cursor);
       QG_LAUNCH_CHECK();
-      hipLaunchKernelGGL(k_msm_scatter, dim3(div_up(n, 256)), dim3(256), 0, ctx->stream,
-                         d_scalars, n, srs->n, c, W, cursor, entries);
+      hipLaunchKernelGGL(k_sort_chunk_offsets, dim3(div_up(nb, 256)), dim3(256), 0, ctx->stream,
+                         cbase, chist, LO, nb, bstart);
+      QG_LAUNCH_CHECK();
+      hipLaunchKernelGGL(k_sortB_scatter, dim3((unsigned)max_chunks), dim3(SORT_BLOCK),
+                         NL * sizeof(uint32_t), ctx->stream, tmp, gstart, cbase, cgroup, misc, NL,
+                         chist, entries);
       QG_LAUNCH_CHECK();
     }
     {
       QgTimed tm(ctx, "msm_accumulate");
       hipLaunchKernelGGL(k_msm_accumulate, dim3(div_up(max_threads, MSM_BLOCK)), dim3(MSM_BLOCK),
-                         0, ctx->stream, srs->d_table, entries, bstart, tstart, nb, partial);
+                         0, ctx->stream, srs->d_table, entries, bstart, tstart, nb, elog, partial,
+                         owner);
       QG_LAUNCH_CHECK();
     }
+    uint32_t max_tpb = 0;
+    QG_HIP(hipMemcpyAsync(&max_tpb, misc + 1, sizeof(uint32_t), hipMemcpyDeviceToHost, ctx->stream));
+    QG_HIP(hipStreamSynchronize(ctx->stream));
     {
       QgTimed tm(ctx, "msm_reduce");
-      hipLaunchKernelGGL(k_msm_reduce, dim3(nred), dim3(MSM_BLOCK), 0, ctx->stream, partial,
-                         tstart, nb, red);
+      for (uint32_t st = 1; st < max_tpb; st <<= 1) {
+        hipLaunchKernelGGL(k_msm_tree_step, dim3(div_up(max_threads, MSM_BLOCK)), dim3(MSM_BLOCK),
+                           0, ctx->stream, partial, owner, tstart, nb, st);
+        QG_LAUNCH_CHECK();
+      }
+      hipLaunchKernelGGL(k_msm_combine, dim3(div_up(nb, MSM_BLOCK)), dim3(MSM_BLOCK), 0,
+                         ctx->stream, partial, tstart, nb, buckets);
+      QG_LAUNCH_CHECK();
+      hipLaunchKernelGGL(k_msm_reduce, dim3(nred), dim3(MSM_BLOCK), 0, ctx->stream, buckets, nb,
+                         red);
       QG_LAUNCH_CHECK();
       hipLaunchKernelGGL(k_msm_final, dim3(1), dim3(MSM_BLOCK), 0, ctx->stream, red, nred,
                          red + nred);

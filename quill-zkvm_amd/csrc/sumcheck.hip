@@ -333,40 +333,64 @@ __global__ void __launch_bounds__(SC_BLOCK)
   }
 }
 
-// Round bookkeeping shared by the finish and tail kernels (thread 0 only):
-// interpolate evals -> coefficients, trim, absorb, draw r_j.
+// Round bookkeeping shared by the finish and tail kernels (whole block):
+// interpolate evals -> coefficients (lane t computes coefficient t), trim,
+// serialize into an LDS word buffer, then one lane runs the word-oriented
+// BLAKE3 transcript (absorb message, draw r_j).
 struct RoundOut {
-  uint8_t* state;        // 32 B transcript state (device)
+  uint32_t* state;       // 8-word (32 B) transcript state (device)
   Fr* chal;              // nvars challenges
   Fr* coeffs;            // nvars x width
   uint32_t* lens;        // nvars
   uint32_t width;        // row width (>= np)
 };
 
-QG_DEV void finish_round(const SopDev* __restrict__ sp, const Fr* evals, const RoundOut& ro,
-                         uint32_t j) {
-  const uint32_t np = sp->np;
-  Fr co[16];
-  uint32_t len = 0;
-  for (uint32_t i = 0; i < np; i++) {
-    Fr acc = Fr::zero();
-    for (uint32_t t = 0; t < np; t++) acc = acc + sp->vinv[i * 16 + t] * evals[t];
-    co[i] = acc;
-    if (!acc.is_zero()) len = i + 1;
+struct FinishSmem {
+  Fr ev[16];
+  uint32_t msg[8 + 2 + 16 * 8];  // state || u64 len || coefficients (canonical LE)
+  uint32_t len;
+};
+
+QG_DEV void finish_round_block(const SopDev* __restrict__ sp, FinishSmem& sm, const RoundOut& ro,
+                               uint32_t j) {
+  const uint32_t np = sp->np, t = threadIdx.x;
+  if (t == 0) sm.len = 0;
+  if (t < 8) sm.msg[t] = ro.state[t];
+  __syncthreads();
+  if (t < ro.width) {
+    Fr co = Fr::zero();
+    if (t < np) {
+      for (uint32_t u = 0; u < np; u++) co = co + sp->vinv[t * 16 + u] * sm.ev[u];
+      Fr c = from_mont(co);
+#pragma unroll
+      for (int i = 0; i < 8; i++) sm.msg[10 + 8 * t + i] = c.v[i];
+      if (!co.is_zero()) atomicMax(&sm.len, t + 1);
+    }
+    ro.coeffs[(size_t)j * ro.width + t] = co;  // trailing entries are zero by construction
   }
-  // message = u64 len || len x 32 B canonical coefficients
-  uint8_t msg[8 + 16 * 32];
-  u64_to_bytes(len, msg);
-  for (uint32_t i = 0; i < len; i++) fr_to_bytes(co[i], msg + 8 + 32 * i);
-  uint8_t st[32];
-  for (int i = 0; i < 32; i++) st[i] = ro.state[i];
-  transcript_append(st, msg, 8 + 32 * (size_t)len);
-  Fr r = transcript_draw_fr(st);
-  for (int i = 0; i < 32; i++) ro.state[i] = st[i];
-  ro.chal[j] = r;
-  for (uint32_t i = 0; i < ro.width; i++)
-    ro.coeffs[(size_t)j * ro.width + i] = (i < len) ? co[i] : Fr::zero();
-  ro.lens[j] = len;
+  __syncthreads();
+  if (t == 0) {
+    const uint32_t len = sm.len;
+    sm.msg[8] = len;
+    sm.msg[9] = 0;
+    uint32_t st[8];
+    b3_chunk_words(B3ArrSrc{sm.msg}, 40 + 32 * len, st, 8);
+    Fr r = transcript_draw_fr_words(st);
+#pragma unroll
+    for (int i = 0; i < 8; i++) ro.state[i] = st[i];
+    ro.chal[j] = r;
+    ro.lens[j] = len;
+  }
+  __syncthreads();
+}
+
+template <int NPMAX>
+QG_DEV void stash_evals(const Fr (&s)[NPMAX], uint32_t np, FinishSmem& sm) {
+  if (threadIdx.x == 0) {
+#pragma unroll
+    for (int t = 0; t < NPMAX; t++)
+      if ((uint32_t)t < np) sm.ev[t] = s[t];
+  }
 }
 
 template <int NPMAX>
@@ -374,6 +398,7 @@ __global__ void __launch_bounds__(SC_BLOCK)
     k_sc_finish(const SopDev* __restrict__ sp, const Fr* __restrict__ partial, uint32_t nblocks,
                 RoundOut ro, uint32_t j) {
   __shared__ Fr lds[(SC_BLOCK / 64) * NPMAX];
+  __shared__ FinishSmem sm;
   const uint32_t np = sp->np;
   Fr s[NPMAX];
 #pragma unroll
@@ -384,7 +409,8 @@ __global__ void __launch_bounds__(SC_BLOCK)
       if ((uint32_t)t < np) s[t] = s[t] + partial[(size_t)b * NPMAX + t];
   }
   block_sum<NPMAX>(s, np, lds);
-  if (threadIdx.x == 0) finish_round(sp, s, ro, j);
+  stash_evals<NPMAX>(s, np, sm);
+  finish_round_block(sp, sm, ro, j);
 }
 
 // Remaining rounds j0..nvars-1 in one workgroup, then the final fold + claim.
@@ -395,6 +421,7 @@ __global__ void __launch_bounds__(SC_BLOCK)
               uint32_t nvars, uint32_t j0, int fold0, RoundOut ro, Fr* __restrict__ final_vals,
               Fr* __restrict__ evaluation) {
   __shared__ Fr lds[(SC_BLOCK / 64) * NPMAX];
+  __shared__ FinishSmem sm;
   const uint32_t nslots = sp->nslots, np = sp->np;
   TablePtrs cur = tp0;
   int fold = fold0;
@@ -410,8 +437,8 @@ __global__ void __launch_bounds__(SC_BLOCK)
       eval_pair<K, NPMAX>(sp, lo, df, sums);
     }
     block_sum<NPMAX>(sums, np, lds);
-    if (threadIdx.x == 0) finish_round(sp, sums, ro, j);
-    __syncthreads();
+    stash_evals<NPMAX>(sums, np, sm);
+    finish_round_block(sp, sm, ro, j);
     // the folded tables written this round become the next source
     TablePtrs nxt;
     const TablePtrs& w = ((j - j0) & 1) ? bufB : bufA;
@@ -604,7 +631,7 @@ static void sumcheck_run(qg_ctx* ctx, uint32_t nvars, uint32_t ntables,
   build_vinv(np, h_sp->vinv);
 
   SopDev* d_sp = ctx->scratch_as<SopDev>("sc_prog", 1);
-  uint8_t* d_state = ctx->scratch_as<uint8_t>("sc_state", 32);
+  uint32_t* d_state = ctx->scratch_as<uint32_t>("sc_state", 8);
   Fr* d_chal = ctx->scratch_as<Fr>("sc_chal", nvars);
   Fr* d_coeffs = ctx->scratch_as<Fr>("sc_coeffs", (size_t)nvars * width);
   uint32_t* d_lens = ctx->scratch_as<uint32_t>("sc_lens", nvars);
