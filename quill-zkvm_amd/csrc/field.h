@@ -143,10 +143,70 @@ QG_HD Fp<C> fdbl(const Fp<C>& a) {
   return a + a;
 }
 
-// Montgomery product a*b*R^{-1} mod P (CIOS, no-carry variant).
-// Valid for inputs with a*b < P*R (in particular a, b < P; also a < 2^256, b < P).
+#if defined(__HIP_DEVICE_COMPILE__)
+// (acc:64, hi:32) += a * b  — one v_mad_u64_u32 with its carry-out in VCC
+// folded into the third accumulator word by one v_addc.  hipcc does not emit
+// the carry-out form itself (it rebuilds 64-bit addends with v_mov pairs).
+__device__ __forceinline__ void mac96(uint64_t& acc, uint32_t& hi, uint32_t a, uint32_t b) {
+  uint64_t r;
+  asm("v_mad_u64_u32 %0, vcc, %2, %3, %4\n\t"
+      "v_addc_co_u32_e32 %1, vcc, 0, %1, vcc"
+      : "=&v"(r), "+v"(hi)
+      : "v"(a), "v"(b), "v"(acc)
+      : "vcc");
+  acc = r;
+}
+
+// Montgomery product, FIPS (finely integrated product scanning): column k of
+// a*b and m*P accumulate in a 96-bit register accumulator; m_k is formed from
+// the column's low word.  2 instructions per 32x32 product; measured 1.25e11
+// mul/s on MI355X vs 0.91e11 for the C CIOS (micro/fieldmul_bench.hip).
+template <class C>
+__device__ __forceinline__ Fp<C> mont_mul_dev(const Fp<C>& a, const Fp<C>& b) {
+  uint32_t m[8], t[8];
+  uint64_t acc = 0;
+  uint32_t hi = 0;
+#pragma unroll
+  for (int k = 0; k < 8; k++) {
+#pragma unroll
+    for (int j = 0; j < k; j++) {
+      mac96(acc, hi, a.v[j], b.v[k - j]);
+      mac96(acc, hi, m[j], C::P[k - j]);
+    }
+    mac96(acc, hi, a.v[k], b.v[0]);
+    m[k] = (uint32_t)acc * C::INV;
+    mac96(acc, hi, m[k], C::P[0]);
+    acc = (acc >> 32) | ((uint64_t)hi << 32);
+    hi = 0;
+  }
+#pragma unroll
+  for (int k = 8; k < 15; k++) {
+#pragma unroll
+    for (int j = k - 7; j < 8; j++) {
+      mac96(acc, hi, a.v[j], b.v[k - j]);
+      mac96(acc, hi, m[j], C::P[k - j]);
+    }
+    t[k - 8] = (uint32_t)acc;
+    acc = (acc >> 32) | ((uint64_t)hi << 32);
+    hi = 0;
+  }
+  t[7] = (uint32_t)acc;
+  Fp<C> r;
+#pragma unroll
+  for (int i = 0; i < 8; i++) r.v[i] = t[i];
+  reduce_once<C>(r.v);
+  return r;
+}
+#endif
+
+// Montgomery product a*b*R^{-1} mod P.  Device: FIPS (above).  Host: CIOS,
+// no-carry variant.  Valid for inputs with a*b < P*R (in particular a, b < P;
+// also a < 2^256, b < P).
 template <class C>
 QG_HD Fp<C> operator*(const Fp<C>& a, const Fp<C>& b) {
+#if defined(__HIP_DEVICE_COMPILE__)
+  return mont_mul_dev<C>(a, b);
+#endif
   uint32_t t[8];
 #pragma unroll
   for (int i = 0; i < 8; i++) t[i] = 0;

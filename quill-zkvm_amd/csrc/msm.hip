@@ -72,42 +72,92 @@ QG_DEV void for_each_digit(const Fr& mont_scalar, int c, int W, Emit&& emit) {
 // pass B sorts every group by l in chunks of SORT_CHUNK entries, so a heavy
 // group (skewed scalars, the short top window) spreads over many blocks.
 static constexpr int SORT_BLOCK = 256;
-static constexpr int SORT_SPT = 8;                          // scalars per thread (pass A)
-static constexpr int SORT_TILE = SORT_BLOCK * SORT_SPT;     // scalars per block
+static constexpr int SORT_TILE_MAX = 1024;                  // scalars per block (pass A)
+static constexpr size_t SORT_LDS_A = 120 * 1024;            // LDS budget for staged entries
 static constexpr int SORT_CHUNK = 8192;                     // entries per block (pass B)
 
 __global__ void __launch_bounds__(SORT_BLOCK)
     k_sortA_hist(const Fr* __restrict__ scalars, size_t n, int c, int W, int LO, int H,
-                 uint32_t nblk, uint32_t* __restrict__ ghist) {
+                 uint32_t nblk, uint32_t tile, uint32_t* __restrict__ ghist) {
   extern __shared__ uint32_t hist[];
   for (int g = threadIdx.x; g < H; g += blockDim.x) hist[g] = 0;
   __syncthreads();
-  const size_t base = (size_t)blockIdx.x * SORT_TILE;
-  for (int k = 0; k < SORT_SPT; k++) {
-    size_t i = base + (size_t)k * SORT_BLOCK + threadIdx.x;
-    if (i < n)
-      for_each_digit(scalars[i], c, W, [&](int, uint32_t b, bool) { atomicAdd(&hist[b >> LO], 1u); });
-  }
+  const size_t base = (size_t)blockIdx.x * tile;
+  const size_t end = base + tile < n ? base + tile : n;
+  for (size_t i = base + threadIdx.x; i < end; i += blockDim.x)
+    for_each_digit(scalars[i], c, W, [&](int, uint32_t b, bool) { atomicAdd(&hist[b >> LO], 1u); });
   __syncthreads();
   for (int g = threadIdx.x; g < H; g += blockDim.x) ghist[(size_t)g * nblk + blockIdx.x] = hist[g];
 }
 
+// Block-local exclusive scan of n <= 4 * SORT_BLOCK counts in LDS (in place).
+__device__ void lds_exscan(uint32_t* a, int n, uint32_t* tmp /* SORT_BLOCK words */) {
+  const int per = (n + SORT_BLOCK - 1) / SORT_BLOCK;
+  const int b = threadIdx.x * per;
+  uint32_t tot = 0;
+  for (int k = 0; k < per; k++)
+    if (b + k < n) tot += a[b + k];
+  tmp[threadIdx.x] = tot;
+  __syncthreads();
+  for (int off = 1; off < SORT_BLOCK; off <<= 1) {
+    uint32_t add = threadIdx.x >= (unsigned)off ? tmp[threadIdx.x - off] : 0u;
+    __syncthreads();
+    tmp[threadIdx.x] += add;
+    __syncthreads();
+  }
+  uint32_t run = tmp[threadIdx.x] - tot;
+  for (int k = 0; k < per; k++) {
+    if (b + k < n) {
+      uint32_t v = a[b + k];
+      a[b + k] = run;
+      run += v;
+    }
+  }
+  __syncthreads();
+}
+
+// largest g with off[g] <= p (off ascending, n entries)
+__device__ __forceinline__ int lds_upper(const uint32_t* off, int n, uint32_t p) {
+  int lo = 0, hi = n;
+  while (hi - lo > 1) {
+    int mid = (lo + hi) >> 1;
+    if (off[mid] <= p) lo = mid;
+    else hi = mid;
+  }
+  return lo;
+}
+
+// Pass A scatter: digits of the block's tile are bucketed by group in LDS,
+// then written out as contiguous per-group runs (coalesced stores).
 __global__ void __launch_bounds__(SORT_BLOCK)
     k_sortA_scatter(const Fr* __restrict__ scalars, size_t n, size_t N, int c, int W, int LO, int H,
-                    uint32_t nblk, const uint32_t* __restrict__ goff,
-                    unsigned long long* __restrict__ tmp) {
-  extern __shared__ uint32_t cur[];
-  for (int g = threadIdx.x; g < H; g += blockDim.x) cur[g] = goff[(size_t)g * nblk + blockIdx.x];
+                    uint32_t nblk, uint32_t tile, const uint32_t* __restrict__ ghist,
+                    const uint32_t* __restrict__ goff, unsigned long long* __restrict__ tmp) {
+  extern __shared__ __attribute__((aligned(16))) unsigned char smem[];
+  unsigned long long* ent = reinterpret_cast<unsigned long long*>(smem);
+  uint32_t* loff = reinterpret_cast<uint32_t*>(ent + (size_t)tile * W);
+  uint32_t* cur = loff + H;
+  uint32_t* scr = cur + H;
+  for (int g = threadIdx.x; g < H; g += blockDim.x) {
+    loff[g] = ghist[(size_t)g * nblk + blockIdx.x];
+    cur[g] = 0;
+  }
   __syncthreads();
-  const size_t base = (size_t)blockIdx.x * SORT_TILE;
-  for (int k = 0; k < SORT_SPT; k++) {
-    size_t i = base + (size_t)k * SORT_BLOCK + threadIdx.x;
-    if (i < n)
-      for_each_digit(scalars[i], c, W, [&](int w, uint32_t b, bool neg) {
-        uint32_t pos = atomicAdd(&cur[b >> LO], 1u);
-        uint32_t ent = (uint32_t)((size_t)w * N + i) | (neg ? 0x80000000u : 0u);
-        tmp[pos] = ((unsigned long long)b << 32) | ent;
-      });
+  lds_exscan(loff, H, scr);
+  const size_t base = (size_t)blockIdx.x * tile;
+  const size_t end = base + tile < n ? base + tile : n;
+  for (size_t i = base + threadIdx.x; i < end; i += blockDim.x)
+    for_each_digit(scalars[i], c, W, [&](int w, uint32_t b, bool neg) {
+      const uint32_t g = b >> LO;
+      const uint32_t slot = loff[g] + atomicAdd(&cur[g], 1u);
+      const uint32_t e = (uint32_t)((size_t)w * N + i) | (neg ? 0x80000000u : 0u);
+      ent[slot] = ((unsigned long long)b << 32) | e;
+    });
+  __syncthreads();
+  const uint32_t total = loff[H - 1] + cur[H - 1];
+  for (uint32_t p = threadIdx.x; p < total; p += blockDim.x) {
+    const int g = lds_upper(loff, H, p);
+    tmp[goff[(size_t)g * nblk + blockIdx.x] + (p - loff[g])] = ent[p];
   }
 }
 
@@ -189,23 +239,44 @@ __global__ void k_sort_chunk_offsets(const uint32_t* __restrict__ cbase, uint32_
   }
 }
 
+// Pass B scatter: the chunk is counting-sorted by the low bucket bits in LDS,
+// then each bucket run is written contiguously at its chunk offset.
 __global__ void __launch_bounds__(SORT_BLOCK)
     k_sortB_scatter(const unsigned long long* __restrict__ tmp, const uint32_t* __restrict__ gstart,
                     const uint32_t* __restrict__ cbase, const uint32_t* __restrict__ chunk_group,
                     const uint32_t* __restrict__ nchunks, int NL, const uint32_t* __restrict__ coff,
                     uint32_t* __restrict__ entries) {
-  extern __shared__ uint32_t cur[];
+  extern __shared__ __attribute__((aligned(16))) unsigned char smem[];
+  uint32_t* e32 = reinterpret_cast<uint32_t*>(smem);
+  uint16_t* bins = reinterpret_cast<uint16_t*>(e32 + SORT_CHUNK);
+  uint32_t* loff = reinterpret_cast<uint32_t*>(bins + SORT_CHUNK);
+  uint32_t* cur = loff + NL;
+  uint32_t* scr = cur + NL;
   const uint32_t k = blockIdx.x;
   if (k >= *nchunks) return;
   const uint32_t g = chunk_group[k];
   const uint32_t s = gstart[g] + (k - cbase[g]) * SORT_CHUNK;
   const uint32_t e = min(s + SORT_CHUNK, gstart[g + 1]);
-  for (int l = threadIdx.x; l < NL; l += blockDim.x) cur[l] = coff[(size_t)k * NL + l];
+  for (int l = threadIdx.x; l < NL; l += blockDim.x) {
+    loff[l] = 0;
+    cur[l] = 0;
+  }
   __syncthreads();
+  for (uint32_t p = s + threadIdx.x; p < e; p += blockDim.x)
+    atomicAdd(&loff[(uint32_t)(tmp[p] >> 32) & (NL - 1)], 1u);
+  __syncthreads();
+  lds_exscan(loff, NL, scr);
   for (uint32_t p = s + threadIdx.x; p < e; p += blockDim.x) {
     const unsigned long long v = tmp[p];
-    const uint32_t pos = atomicAdd(&cur[(uint32_t)(v >> 32) & (NL - 1)], 1u);
-    entries[pos] = (uint32_t)v;
+    const uint32_t l = (uint32_t)(v >> 32) & (NL - 1);
+    const uint32_t slot = loff[l] + atomicAdd(&cur[l], 1u);
+    e32[slot] = (uint32_t)v;
+    bins[slot] = (uint16_t)l;
+  }
+  __syncthreads();
+  for (uint32_t q = threadIdx.x; q < e - s; q += blockDim.x) {
+    const uint32_t l = bins[q];
+    entries[coff[(size_t)k * NL + l] + (q - loff[l])] = e32[q];
   }
 }
 
@@ -566,7 +637,10 @@ G1Affine msm_device(qg_ctx* ctx, const qg_srs* srs, const Fr* d_scalars, size_t 
     // bucket id b = (g << LO) | l
     const int BB = c - 1, LO = (BB + 1) / 2, HI = BB - LO;
     const int H = 1 << HI, NL = 1 << LO;
-    const uint32_t nblk = div_up(n, SORT_TILE);
+    // pass-A tile: as many scalars as fit their W digits (8 B each) in LDS
+    uint32_t tile = SORT_TILE_MAX;
+    while (tile > 64 && (size_t)tile * W * 8 > SORT_LDS_A) tile >>= 1;
+    const uint32_t nblk = div_up(n, tile);
     const size_t nghist = (size_t)H * nblk;
     const size_t max_chunks = max_entries / SORT_CHUNK + H + 1;
     uint32_t* ghist = ctx->scratch_as<uint32_t>("msm_ghist", nghist + 1);
@@ -605,7 +679,7 @@ G1Affine msm_device(qg_ctx* ctx, const qg_srs* srs, const Fr* d_scalars, size_t 
       QgTimed tm(ctx, "msm_bucketing");
       // pass A: partition digits by the high bucket bits
       hipLaunchKernelGGL(k_sortA_hist, dim3(nblk), dim3(SORT_BLOCK), H * sizeof(uint32_t),
-                         ctx->stream, d_scalars, n, c, W, LO, H, nblk, ghist);
+                         ctx->stream, d_scalars, n, c, W, LO, H, nblk, tile, ghist);
       QG_LAUNCH_CHECK();
       const unsigned gt = div_up(nghist, 2048);
       QG_CHECK(gt <= 1024u * 1024u, QG_ERR_UNSUPPORTED, "histogram too large");
@@ -618,8 +692,18 @@ G1Affine msm_device(qg_ctx* ctx, const qg_srs* srs, const Fr* d_scalars, size_t 
       hipLaunchKernelGGL(k_scan32_add, dim3(div_up(nghist, 256)), dim3(256), 0, ctx->stream, gtiles,
                          nghist, goff);
       QG_LAUNCH_CHECK();
-      hipLaunchKernelGGL(k_sortA_scatter, dim3(nblk), dim3(SORT_BLOCK), H * sizeof(uint32_t),
-                         ctx->stream, d_scalars, n, srs->n, c, W, LO, H, nblk, goff, tmp);
+      const size_t smemA = (size_t)tile * W * 8 + (2 * (size_t)H + SORT_BLOCK) * 4;
+      QG_CHECK(smemA <= 160 * 1024, QG_ERR_UNSUPPORTED, "pass-A tile exceeds LDS");
+      static bool attr_set = false;
+      if (!attr_set) {
+        QG_HIP(hipFuncSetAttribute(reinterpret_cast<const void*>(&k_sortA_scatter),
+                                   hipFuncAttributeMaxDynamicSharedMemorySize, 160 * 1024));
+        QG_HIP(hipFuncSetAttribute(reinterpret_cast<const void*>(&k_sortB_scatter),
+                                   hipFuncAttributeMaxDynamicSharedMemorySize, 160 * 1024));
+        attr_set = true;
+      }
+      hipLaunchKernelGGL(k_sortA_scatter, dim3(nblk), dim3(SORT_BLOCK), smemA, ctx->stream,
+                         d_scalars, n, srs->n, c, W, LO, H, nblk, tile, ghist, goff, tmp);
       QG_LAUNCH_CHECK();
       // pass B: sort every group by the low bits, in chunks
       QG_HIP(hipMemsetAsync(misc, 0, 4 * sizeof(uint32_t), ctx->stream));
@@ -645,9 +729,9 @@ G1Affine msm_device(qg_ctx* ctx, const qg_srs* srs, const Fr* d_scalars, size_t 
       hipLaunchKernelGGL(k_sort_chunk_offsets, dim3(div_up(nb, 256)), dim3(256), 0, ctx->stream,
                          cbase, chist, LO, nb, bstart);
       QG_LAUNCH_CHECK();
-      hipLaunchKernelGGL(k_sortB_scatter, dim3((unsigned)max_chunks), dim3(SORT_BLOCK),
-                         NL * sizeof(uint32_t), ctx->stream, tmp, gstart, cbase, cgroup, misc, NL,
-                         chist, entries);
+      const size_t smemB = (size_t)SORT_CHUNK * 6 + (2 * (size_t)NL + SORT_BLOCK) * 4;
+      hipLaunchKernelGGL(k_sortB_scatter, dim3((unsigned)max_chunks), dim3(SORT_BLOCK), smemB,
+                         ctx->stream, tmp, gstart, cbase, cgroup, misc, NL, chist, entries);
       QG_LAUNCH_CHECK();
     }
     {

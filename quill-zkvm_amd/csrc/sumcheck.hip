@@ -39,7 +39,7 @@ namespace qg {
 
 static constexpr int SC_BLOCK = 256;
 static constexpr int SC_MAX_BLOCKS = 1024;
-static constexpr int TAIL_LOG = 12;
+static constexpr int TAIL_LOG = 8;   // single-workgroup tail once tables have <= 2^8 entries
 
 // ---------------------------------------------------------------- programs
 struct Mono {
@@ -193,13 +193,22 @@ static void build_vinv(uint32_t np, Fr* out) {
 }
 
 // ---------------------------------------------------------------- device math
+// v[i] for a wave-uniform slot index i.  readfirstlane makes the index scalar
+// so the switch lowers to scalar branches; a runtime-indexed register array
+// would otherwise be demoted to scratch memory.
 template <int K>
 QG_DEV Fr sel(const Fr (&v)[K], uint32_t i) {
-  Fr r = v[0];
-#pragma unroll
-  for (int k = 1; k < K; k++)
-    if (i == (uint32_t)k) r = v[k];
-  return r;
+  i = __builtin_amdgcn_readfirstlane(i);
+  switch (i) {
+    case 0: return v[0];
+    case 1: if constexpr (K > 1) return v[1]; else return v[0];
+    case 2: if constexpr (K > 2) return v[2]; else return v[0];
+    case 3: if constexpr (K > 3) return v[3]; else return v[0];
+    case 4: if constexpr (K > 4) return v[4]; else return v[0];
+    case 5: if constexpr (K > 5) return v[5]; else return v[0];
+    case 6: if constexpr (K > 6) return v[6]; else return v[0];
+    default: if constexpr (K > 7) return v[7]; else return v[0];
+  }
 }
 
 // h(values) via the monomial program
@@ -258,20 +267,28 @@ QG_DEV void load_pair(const TablePtrs& tp, uint32_t nslots, size_t p, bool fold,
   }
 }
 
-template <int K, int NPMAX>
-QG_DEV void eval_pair(const SopDev* __restrict__ sp, Fr (&lo)[K], const Fr (&df)[K],
-                      Fr (&sums)[NPMAX]) {
-  const uint32_t np = sp->np;
-#pragma unroll
-  for (int t = 0; t < NPMAX; t++) {
-    if ((uint32_t)t < np) {
-      if (t > 0) {
+// Evaluation points t = T..NPMAX-1 by template recursion, so sums[] is only
+// ever indexed by compile-time constants (a runtime-indexed accumulator array
+// is demoted to scratch memory).
+template <int T, int K, int NPMAX>
+QG_DEV void eval_points(const SopDev* __restrict__ sp, uint32_t np, Fr (&lo)[K], const Fr (&df)[K],
+                        Fr (&sums)[NPMAX]) {
+  if constexpr (T < NPMAX) {
+    if ((uint32_t)T < np) {
+      if constexpr (T > 0) {
 #pragma unroll
         for (int i = 0; i < K; i++) lo[i] = lo[i] + df[i];
       }
-      sums[t] = sums[t] + sop_eval<K>(sp, lo);
+      sums[T] = sums[T] + sop_eval<K>(sp, lo);
+      eval_points<T + 1, K, NPMAX>(sp, np, lo, df, sums);
     }
   }
+}
+
+template <int K, int NPMAX>
+QG_DEV void eval_pair(const SopDev* __restrict__ sp, Fr (&lo)[K], const Fr (&df)[K],
+                      Fr (&sums)[NPMAX]) {
+  eval_points<0, K, NPMAX>(sp, sp->np, lo, df, sums);
 }
 
 QG_DEV Fr shfl_xor_fr(const Fr& a, int m) {
@@ -329,7 +346,9 @@ __global__ void __launch_bounds__(SC_BLOCK)
   }
   block_sum<NPMAX>(sums, np, lds);
   if (threadIdx.x == 0) {
-    for (uint32_t t = 0; t < np; t++) partial[(size_t)blockIdx.x * NPMAX + t] = sums[t];
+#pragma unroll
+    for (int t = 0; t < NPMAX; t++)
+      if ((uint32_t)t < np) partial[(size_t)blockIdx.x * NPMAX + t] = sums[t];
   }
 }
 
@@ -348,7 +367,15 @@ struct RoundOut {
 struct FinishSmem {
   Fr ev[16];
   uint32_t msg[8 + 2 + 16 * 8];  // state || u64 len || coefficients (canonical LE)
+  uint32_t chin[12];             // new state || "challenge"
+  uint32_t ab[20];               // new state || 48 challenge bytes
   uint32_t len;
+};
+
+// LDS word source for b3_chunk_words (dynamic indices stay in LDS, not scratch)
+struct LdsSrc {
+  const uint32_t* p;
+  QG_DEV uint32_t operator()(uint32_t i) const { return p[i]; }
 };
 
 QG_DEV void finish_round_block(const SopDev* __restrict__ sp, FinishSmem& sm, const RoundOut& ro,
@@ -373,12 +400,27 @@ QG_DEV void finish_round_block(const SopDev* __restrict__ sp, FinishSmem& sm, co
     const uint32_t len = sm.len;
     sm.msg[8] = len;
     sm.msg[9] = 0;
-    uint32_t st[8];
-    b3_chunk_words(B3ArrSrc{sm.msg}, 40 + 32 * len, st, 8);
-    Fr r = transcript_draw_fr_words(st);
+    // state' = B3(state || msg)
+    b3_chunk_words(LdsSrc{sm.msg}, 40 + 32 * len, sm.chin, 8);
+    // challenge = B3-XOF(state' || "challenge")[0..48]
+    sm.chin[8] = 0x6c616863u;  // "chal"
+    sm.chin[9] = 0x676e656cu;  // "leng"
+    sm.chin[10] = 0x00000065u; // "e"
 #pragma unroll
-    for (int i = 0; i < 8; i++) ro.state[i] = st[i];
-    ro.chal[j] = r;
+    for (int i = 0; i < 8; i++) sm.ab[i] = sm.chin[i];
+    b3_chunk_words(LdsSrc{sm.chin}, 41, sm.ab + 8, 12);
+    // state'' = B3(state' || challenge)
+    b3_chunk_words(LdsSrc{sm.ab}, 80, sm.chin, 8);
+#pragma unroll
+    for (int i = 0; i < 8; i++) ro.state[i] = sm.chin[i];
+    Fr lo, hi;
+#pragma unroll
+    for (int i = 0; i < 8; i++) lo.v[i] = sm.ab[8 + i];
+#pragma unroll
+    for (int i = 0; i < 4; i++) hi.v[i] = sm.ab[16 + i];
+#pragma unroll
+    for (int i = 4; i < 8; i++) hi.v[i] = 0;
+    ro.chal[j] = lo * Fr::from_raw(FrP::R2) + hi * Fr::from_raw(FrP::R3);
     ro.lens[j] = len;
   }
   __syncthreads();
