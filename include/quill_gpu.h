@@ -62,6 +62,13 @@ const char* qg_version(void);
  * (high index bits = rank). */
 int qg_comm_unique_id(uint8_t out_id[128]);
 int qg_ctx_attach_comm(qg_ctx* ctx, int rank, int world, const uint8_t unique_id[128]);
+/* In-process loopback group: `world` contexts, each driven by its own host
+ * thread (possibly on one device), exchange through device-to-device copies
+ * instead of RCCL.  Exercises every sharded path on a single GPU. */
+typedef struct qg_loopback qg_loopback;
+int qg_loopback_create(int world, qg_loopback** out);
+int qg_loopback_destroy(qg_loopback* lb);
+int qg_ctx_attach_loopback(qg_ctx* ctx, qg_loopback* lb, int rank);
 
 /* ---------------------------------------------------------------- transcript */
 /* Transcript::new(domain)                  transcript/src/transcript.rs:14-22 */
@@ -184,7 +191,10 @@ typedef struct qg_expr_op {
 
 /* SumcheckProof::prove (hyperplonk/src/piops/sumcheck.rs:28-114) for
  * h(g_0..g_{k-1}) = program.  tables[i] = 2^nvars Fr evaluations of g_i
- * (host pointers).  Absorbs num_vars and claimed_sum, then per round the
+ * (host pointers).  With an attached communicator (qg_ctx_attach_comm),
+ * `nvars` is the GLOBAL variable count and each rank passes its block of
+ * 2^(nvars - log2(world)) entries per table (high index bits = rank); every
+ * rank returns the same proof.  Absorbs num_vars and claimed_sum, then per round the
  * trimmed coefficient-form message; binds index bit 0 first.
  * Outputs (caller-allocated):
  *   round_coeffs : nvars * (max_degree+1) * 4 uint64, row j = message j

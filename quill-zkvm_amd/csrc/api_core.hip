@@ -151,6 +151,7 @@ int qg_ctx_destroy(qg_ctx* ctx) {
   if (!ctx) return QG_OK;
   (void)hipSetDevice(ctx->device);
   if (ctx->stream) (void)hipStreamSynchronize(ctx->stream);
+  comm_release(ctx);
   for (auto& kv : ctx->scratch) (void)hipFree(kv.second.first);
   for (auto& e : ctx->pending) {
     (void)hipEventDestroy(e.a);

@@ -8,12 +8,41 @@
 //    bits; one allgather of the (d+1) round sums per round.
 #include <string.h>
 
+#include <condition_variable>
+#include <mutex>
+#include <vector>
+
 #include <rccl/rccl.h>
 
 #include "common.h"
 
+// In-process loopback group: `world` contexts driven by `world` host threads
+// on one device.  Same collective hook as RCCL; used to exercise every sharded
+// code path on a single GPU (tests/test_gpu_multirank.py).
+struct qg_loopback {
+  int world = 0;
+  std::mutex mu;
+  std::condition_variable cv;
+  int arrived = 0;
+  uint64_t generation = 0;
+  std::vector<const void*> sends;
+
+  void barrier() {
+    std::unique_lock<std::mutex> lk(mu);
+    const uint64_t gen = generation;
+    if (++arrived == world) {
+      arrived = 0;
+      generation++;
+      cv.notify_all();
+    } else {
+      cv.wait(lk, [&] { return generation != gen; });
+    }
+  }
+};
+
 struct qg_comm_state {
   ncclComm_t comm = nullptr;
+  qg_loopback* lb = nullptr;
 };
 
 namespace qg {
@@ -30,8 +59,28 @@ void comm_allgather_bytes(qg_ctx* ctx, const void* d_send, void* d_recv, size_t 
     QG_HIP(hipMemcpyAsync(d_recv, d_send, bytes, hipMemcpyDeviceToDevice, ctx->stream));
     return;
   }
-  QG_CHECK(ctx->comm && ctx->comm->comm, QG_ERR_COMM, "no communicator attached");
+  QG_CHECK(ctx->comm, QG_ERR_COMM, "no communicator attached");
+  if (ctx->comm->lb) {
+    qg_loopback* lb = ctx->comm->lb;
+    QG_HIP(hipStreamSynchronize(ctx->stream));  // send buffer complete
+    lb->sends[ctx->rank] = d_send;
+    lb->barrier();
+    for (int r = 0; r < ctx->world; r++)
+      QG_HIP(hipMemcpyAsync((uint8_t*)d_recv + (size_t)r * bytes, lb->sends[r], bytes,
+                            hipMemcpyDeviceToDevice, ctx->stream));
+    QG_HIP(hipStreamSynchronize(ctx->stream));
+    lb->barrier();  // nobody reuses its send buffer before every rank has copied it
+    return;
+  }
+  QG_CHECK(ctx->comm->comm, QG_ERR_COMM, "no communicator attached");
   QG_NCCL(ncclAllGather(d_send, d_recv, bytes, ncclUint8, ctx->comm->comm, ctx->stream));
+}
+
+void comm_release(qg_ctx* ctx) {
+  if (!ctx->comm) return;
+  if (ctx->comm->comm) (void)ncclCommDestroy(ctx->comm->comm);
+  delete ctx->comm;  // a loopback group is owned by its creator
+  ctx->comm = nullptr;
 }
 
 }  // namespace qg
@@ -57,6 +106,8 @@ int qg_ctx_attach_comm(qg_ctx* ctx, int rank, int world, const uint8_t unique_id
       delete ctx->comm;
       ctx->comm = nullptr;
     }
+    ctx->rank = 0;
+    ctx->world = 1;
     ctx->rank = rank;
     ctx->world = world;
     if (world == 1) return;
@@ -64,6 +115,34 @@ int qg_ctx_attach_comm(qg_ctx* ctx, int rank, int world, const uint8_t unique_id
     memcpy(&id, unique_id, 128);
     ctx->comm = new qg_comm_state();
     QG_NCCL(ncclCommInitRank(&ctx->comm->comm, world, id, rank));
+  });
+}
+
+int qg_loopback_create(int world, qg_loopback** out) {
+  if (!out || world < 1) return QG_ERR_INVALID;
+  qg_loopback* lb = new qg_loopback();
+  lb->world = world;
+  lb->sends.assign(world, nullptr);
+  *out = lb;
+  return QG_OK;
+}
+
+int qg_loopback_destroy(qg_loopback* lb) {
+  delete lb;
+  return QG_OK;
+}
+
+int qg_ctx_attach_loopback(qg_ctx* ctx, qg_loopback* lb, int rank) {
+  if (!ctx || !lb || rank < 0 || rank >= lb->world) return QG_ERR_INVALID;
+  return qg_guard(ctx, [&] {
+    if (ctx->comm) {
+      if (ctx->comm->comm) (void)ncclCommDestroy(ctx->comm->comm);
+      delete ctx->comm;
+    }
+    ctx->comm = new qg_comm_state();
+    ctx->comm->lb = lb;
+    ctx->rank = rank;
+    ctx->world = lb->world;
   });
 }
 

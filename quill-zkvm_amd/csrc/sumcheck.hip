@@ -530,6 +530,52 @@ __global__ void k_eq_combine(const Fr* __restrict__ low, const Fr* __restrict__ 
   out[i] = low[i & (((size_t)1 << lbits) - 1)] * high[i >> lbits];
 }
 
+// multi-GPU: sum this rank's block partials -> loc[0..np)
+template <int NPMAX>
+__global__ void __launch_bounds__(SC_BLOCK)
+    k_sc_local_sum(const SopDev* __restrict__ sp, const Fr* __restrict__ partial, uint32_t nblocks,
+                   Fr* __restrict__ loc) {
+  __shared__ Fr lds[(SC_BLOCK / 64) * NPMAX];
+  const uint32_t np = sp->np;
+  Fr s[NPMAX];
+#pragma unroll
+  for (int t = 0; t < NPMAX; t++) s[t] = Fr::zero();
+  for (uint32_t b = threadIdx.x; b < nblocks; b += blockDim.x) {
+#pragma unroll
+    for (int t = 0; t < NPMAX; t++)
+      if ((uint32_t)t < np) s[t] = s[t] + partial[(size_t)b * NPMAX + t];
+  }
+  block_sum<NPMAX>(s, np, lds);
+  if (threadIdx.x == 0) {
+#pragma unroll
+    for (int t = 0; t < NPMAX; t++) loc[t] = (uint32_t)t < np ? s[t] : Fr::zero();
+  }
+}
+
+// multi-GPU: fold each slot's last local pair with r (size 2 -> 1)
+__global__ void k_sc_fold_last(TablePtrs cur, uint32_t nslots, const Fr* __restrict__ chal,
+                               Fr* __restrict__ out) {
+  const uint32_t i = threadIdx.x;
+  if (i >= nslots) return;
+  const Fr r = *chal;
+  const Fr a = cur.src[i][0], b = cur.src[i][1];
+  out[i] = a + r * (b - a);
+}
+
+// gathered [rank][slot] -> per-slot tables [slot][rank]
+__global__ void k_sc_transpose(const Fr* __restrict__ in, uint32_t world, uint32_t nslots,
+                               Fr* __restrict__ out) {
+  const uint32_t idx = blockIdx.x * blockDim.x + threadIdx.x;
+  if (idx >= world * nslots) return;
+  const uint32_t rk = idx / nslots, sl = idx % nslots;
+  out[(size_t)sl * world + rk] = in[(size_t)rk * 8 + sl];
+}
+
+__global__ void k_scale(Fr* __restrict__ a, size_t n, const Fr* __restrict__ s) {
+  const size_t i = (size_t)blockIdx.x * blockDim.x + threadIdx.x;
+  if (i < n) a[i] = a[i] * (*s);
+}
+
 }  // namespace qg
 
 // ---------------------------------------------------------------- host driver
@@ -635,6 +681,102 @@ static void run_rounds(qg_ctx* ctx, uint32_t nvars, const std::vector<const Fr*>
   }
 }
 
+// Sharded rounds: this rank holds the block of every table whose
+// high log2(world) index bits equal its rank.  Rounds 0..m-1 (m = local bits)
+// pair local entries only: one allgather of the (d+1) round sums per round, then
+// every rank runs the identical device transcript.  The last log2(world) rounds
+// run redundantly on the allgathered single values.
+template <int K, int NPMAX>
+static void run_rounds_dist(qg_ctx* ctx, uint32_t nvars, const std::vector<const Fr*>& src,
+                            const SopDev* d_sp, uint32_t nslots, RoundOut ro, Fr* d_final,
+                            Fr* d_eval) {
+  const uint32_t world = (uint32_t)ctx->world;
+  uint32_t lw = 0;
+  while ((1u << lw) < world) lw++;
+  QG_CHECK((1u << lw) == world, QG_ERR_INVALID, "sharded sumcheck needs a power-of-two world");
+  QG_CHECK(nvars > lw, QG_ERR_INVALID, "sharded sumcheck needs nvars > log2(world)");
+  const uint32_t m = nvars - lw;
+  const size_t NL = (size_t)1 << m;
+  Fr* X = ctx->scratch_as<Fr>("sc_x", std::max<size_t>(1, (NL / 2) * std::max(nslots, 1u)));
+  Fr* Y = ctx->scratch_as<Fr>("sc_y", std::max<size_t>(1, (NL / 4) * std::max(nslots, 1u)));
+  Fr* partial = ctx->scratch_as<Fr>("sc_partial", (size_t)SC_MAX_BLOCKS * NPMAX);
+  Fr* loc = ctx->scratch_as<Fr>("sc_loc", NPMAX);
+  Fr* all = ctx->scratch_as<Fr>("sc_all", (size_t)world * NPMAX);
+  Fr* last = ctx->scratch_as<Fr>("sc_last", 8);
+  Fr* graw = ctx->scratch_as<Fr>("sc_graw", (size_t)world * 8);
+  Fr* gt = ctx->scratch_as<Fr>("sc_gt", (size_t)world * 8);
+  Fr* gA = ctx->scratch_as<Fr>("sc_gA", (size_t)world * 8);
+  Fr* gB = ctx->scratch_as<Fr>("sc_gB", (size_t)world * 8);
+  TablePtrs cur{};
+  for (uint32_t i = 0; i < 8; i++) cur.src[i] = i < nslots ? src[i] : nullptr;
+  auto bufs = [&](Fr* base, size_t per) {
+    TablePtrs t{};
+    for (uint32_t i = 0; i < 8; i++) t.dst[i] = i < nslots ? base + per * i : nullptr;
+    return t;
+  };
+  TablePtrs tX = bufs(X, NL / 2), tY = bufs(Y, std::max<size_t>(1, NL / 4));
+  int fold = 0, parity = 0;
+  {
+    QgTimed tm(ctx, "sumcheck_round");
+    for (uint32_t j = 0; j < m; j++) {
+      const size_t npairs = (NL >> j) / 2;
+      const unsigned blocks = (unsigned)std::min<size_t>(SC_MAX_BLOCKS, div_up(npairs, SC_BLOCK));
+      TablePtrs tp = cur;
+      if (fold) {
+        const TablePtrs& d = parity ? tY : tX;
+        for (int i = 0; i < 8; i++) tp.dst[i] = d.dst[i];
+      }
+      hipLaunchKernelGGL((k_sc_round<K, NPMAX>), dim3(blocks), dim3(SC_BLOCK), 0, ctx->stream, tp,
+                         d_sp, npairs, fold, fold ? ro.chal + (j - 1) : ro.chal, partial);
+      QG_LAUNCH_CHECK();
+      hipLaunchKernelGGL((k_sc_local_sum<NPMAX>), dim3(1), dim3(SC_BLOCK), 0, ctx->stream, d_sp,
+                         partial, blocks, loc);
+      QG_LAUNCH_CHECK();
+      comm_allgather_bytes(ctx, loc, all, sizeof(Fr) * NPMAX);
+      hipLaunchKernelGGL((k_sc_finish<NPMAX>), dim3(1), dim3(SC_BLOCK), 0, ctx->stream, d_sp, all,
+                         world, ro, j);
+      QG_LAUNCH_CHECK();
+      if (fold) {
+        for (int i = 0; i < 8; i++) cur.src[i] = tp.dst[i];
+        parity ^= 1;
+      }
+      fold = 1;
+    }
+  }
+  {
+    QgTimed tm(ctx, "sumcheck_tail");
+    // local tables have 2 entries (folded through r_{m-2}); fold with r_{m-1}
+    if (nslots) {
+      hipLaunchKernelGGL(k_sc_fold_last, dim3(1), dim3(64), 0, ctx->stream, cur, nslots,
+                         ro.chal + (m - 1), last);
+      QG_LAUNCH_CHECK();
+    }
+    comm_allgather_bytes(ctx, last, graw, sizeof(Fr) * 8);
+    if (nslots) {
+      hipLaunchKernelGGL(k_sc_transpose, dim3(div_up((size_t)world * nslots, 64)), dim3(64), 0,
+                         ctx->stream, graw, world, nslots, gt);
+      QG_LAUNCH_CHECK();
+    }
+    TablePtrs t0{}, bufA{}, bufB{};
+    for (uint32_t i = 0; i < 8; i++) {
+      t0.src[i] = i < nslots ? gt + (size_t)world * i : nullptr;
+      bufA.dst[i] = i < nslots ? gA + (size_t)world * i : nullptr;
+      bufB.dst[i] = i < nslots ? gB + (size_t)world * i : nullptr;
+    }
+    hipLaunchKernelGGL((k_sc_tail<K, NPMAX>), dim3(1), dim3(SC_BLOCK), 0, ctx->stream, t0, bufA,
+                       bufB, d_sp, nvars, m, 0, ro, d_final, d_eval);
+    QG_LAUNCH_CHECK();
+  }
+}
+
+template <int K, int NPMAX>
+static void run_rounds_any(qg_ctx* ctx, uint32_t nvars, const std::vector<const Fr*>& src,
+                           const SopDev* d_sp, uint32_t nslots, RoundOut ro, Fr* d_final,
+                           Fr* d_eval) {
+  if (ctx->world > 1) run_rounds_dist<K, NPMAX>(ctx, nvars, src, d_sp, nslots, ro, d_final, d_eval);
+  else run_rounds<K, NPMAX>(ctx, nvars, src, d_sp, nslots, ro, d_final, d_eval);
+}
+
 static void sumcheck_run(qg_ctx* ctx, uint32_t nvars, uint32_t ntables,
                          const std::vector<const Fr*>& d_tables, const qg_expr_op* prog,
                          size_t prog_len, const uint64_t* consts, size_t nconsts,
@@ -693,13 +835,13 @@ static void sumcheck_run(qg_ctx* ctx, uint32_t nvars, uint32_t ntables,
   const uint32_t nslots_launch = (uint32_t)sp.used.size();
   // (with no used slots, nslots = 0 and loads are skipped)
   if (np <= 4) {
-    if (src.size() <= 4) run_rounds<4, 4>(ctx, nvars, src, d_sp, nslots_launch, ro, d_final, d_eval);
-    else run_rounds<8, 4>(ctx, nvars, src, d_sp, nslots_launch, ro, d_final, d_eval);
+    if (src.size() <= 4) run_rounds_any<4, 4>(ctx, nvars, src, d_sp, nslots_launch, ro, d_final, d_eval);
+    else run_rounds_any<8, 4>(ctx, nvars, src, d_sp, nslots_launch, ro, d_final, d_eval);
   } else if (np <= 8) {
-    if (src.size() <= 4) run_rounds<4, 8>(ctx, nvars, src, d_sp, nslots_launch, ro, d_final, d_eval);
-    else run_rounds<8, 8>(ctx, nvars, src, d_sp, nslots_launch, ro, d_final, d_eval);
+    if (src.size() <= 4) run_rounds_any<4, 8>(ctx, nvars, src, d_sp, nslots_launch, ro, d_final, d_eval);
+    else run_rounds_any<8, 8>(ctx, nvars, src, d_sp, nslots_launch, ro, d_final, d_eval);
   } else {
-    run_rounds<8, 16>(ctx, nvars, src, d_sp, nslots_launch, ro, d_final, d_eval);
+    run_rounds_any<8, 16>(ctx, nvars, src, d_sp, nslots_launch, ro, d_final, d_eval);
   }
 
   std::vector<Fr> h_coeffs((size_t)nvars * width), h_chal(nvars);
@@ -719,9 +861,19 @@ static void sumcheck_run(qg_ctx* ctx, uint32_t nvars, uint32_t ntables,
   fr_export(h_eval, evaluation);
 }
 
+// entries per table held by this rank: 2^nvars, or 2^(nvars - log2(world)) when
+// the tables are sharded over an attached communicator
+static size_t local_table_size(const qg_ctx* ctx, uint32_t nvars) {
+  uint32_t lw = 0;
+  while ((1 << lw) < ctx->world) lw++;
+  QG_CHECK((1 << lw) == ctx->world, QG_ERR_INVALID, "world size must be a power of two");
+  QG_CHECK(nvars > lw, QG_ERR_INVALID, "nvars must exceed log2(world)");
+  return (size_t)1 << (nvars - lw);
+}
+
 static std::vector<const Fr*> upload_tables(qg_ctx* ctx, uint32_t nvars, uint32_t ntables,
                                             const uint64_t* const* tables) {
-  const size_t N = (size_t)1 << nvars;
+  const size_t N = local_table_size(ctx, nvars);
   Fr* d = ctx->scratch_as<Fr>("sc_in", std::max<size_t>(1, N * ntables));
   std::vector<const Fr*> out;
   for (uint32_t i = 0; i < ntables; i++) {
@@ -741,11 +893,24 @@ static void zerocheck_run(qg_ctx* ctx, uint32_t nvars, uint32_t ntables,
   QG_CHECK(nvars >= 1 && nvars <= 40, QG_ERR_INVALID, "nvars out of range");
   std::vector<Fr> z(nvars);
   for (uint32_t i = 0; i < nvars; i++) z[i] = transcript_draw_fr(state);  // zerocheck.rs:20-22
-  const size_t N = (size_t)1 << nvars;
+  const size_t N = local_table_size(ctx, nvars);
+  uint32_t m = 0;
+  while (((size_t)1 << m) < N) m++;
   Fr* d_z = ctx->scratch_as<Fr>("zc_z", nvars);
   Fr* d_eq = ctx->scratch_as<Fr>("zc_eq", N);
   QG_HIP(hipMemcpyAsync(d_z, z.data(), sizeof(Fr) * nvars, hipMemcpyHostToDevice, ctx->stream));
-  eq_table_device(ctx, d_z, nvars, d_eq);
+  eq_table_device(ctx, d_z, m, d_eq);
+  if (ctx->world > 1) {
+    // this rank's block: the high index bits are the rank (eq_eval.rs bit j <-> z_j)
+    Fr f = Fr::one();
+    for (uint32_t j = m; j < nvars; j++)
+      f = f * ((((uint32_t)ctx->rank >> (j - m)) & 1u) ? z[j] : Fr::one() - z[j]);
+    Fr* d_f = ctx->scratch_as<Fr>("zc_f", 1);
+    QG_HIP(hipMemcpyAsync(d_f, &f, sizeof(Fr), hipMemcpyHostToDevice, ctx->stream));
+    hipLaunchKernelGGL(k_scale, dim3(div_up(N, 256)), dim3(256), 0, ctx->stream, d_eq, N, d_f);
+    QG_LAUNCH_CHECK();
+    ctx->sync();  // f lives on the host stack
+  }
   if (eq_out) fr_download(ctx, eq_out, d_eq, N);
   d_tables.push_back(d_eq);
   std::vector<qg_expr_op> p2(prog, prog + prog_len);
@@ -817,8 +982,8 @@ int qg_sumcheck_prove_dev(qg_ctx* ctx, uint32_t nvars, uint32_t ntables,
     QG_HIP(hipSetDevice(ctx->device));
     std::vector<const Fr*> d;
     for (uint32_t i = 0; i < ntables; i++) {
-      QG_CHECK(tables[i] && tables[i]->n >= ((size_t)1 << nvars), QG_ERR_INVALID,
-               "device table shorter than 2^nvars");
+      QG_CHECK(tables[i] && tables[i]->n >= local_table_size(ctx, nvars), QG_ERR_INVALID,
+               "device table shorter than its (local) hypercube size");
       d.push_back(tables[i]->d);
     }
     sumcheck_run(ctx, nvars, ntables, d, prog, prog_len, consts, nconsts, claimed_sum, state,
@@ -856,8 +1021,8 @@ int qg_zerocheck_prove_dev(qg_ctx* ctx, uint32_t nvars, uint32_t ntables,
     QG_HIP(hipSetDevice(ctx->device));
     std::vector<const Fr*> d;
     for (uint32_t i = 0; i < ntables; i++) {
-      QG_CHECK(tables[i] && tables[i]->n >= ((size_t)1 << nvars), QG_ERR_INVALID,
-               "device table shorter than 2^nvars");
+      QG_CHECK(tables[i] && tables[i]->n >= local_table_size(ctx, nvars), QG_ERR_INVALID,
+               "device table shorter than its (local) hypercube size");
       d.push_back(tables[i]->d);
     }
     zerocheck_run(ctx, nvars, ntables, d, prog, prog_len, consts, nconsts, state, round_coeffs,

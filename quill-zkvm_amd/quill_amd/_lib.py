@@ -58,6 +58,9 @@ PROTOTYPES = {
     "qg_last_error": (C.c_char_p, [P]),
     "qg_comm_unique_id": (C.c_int, [U8P]),
     "qg_ctx_attach_comm": (C.c_int, [P, C.c_int, C.c_int, U8P]),
+    "qg_loopback_create": (C.c_int, [C.c_int, C.POINTER(P)]),
+    "qg_loopback_destroy": (C.c_int, [P]),
+    "qg_ctx_attach_loopback": (C.c_int, [P, P, C.c_int]),
     "qg_transcript_new": (C.c_int, [C.c_char_p, SZ, U8P]),
     "qg_transcript_append": (C.c_int, [U8P, C.c_char_p, SZ]),
     "qg_transcript_draw": (C.c_int, [U8P, U8P, SZ]),

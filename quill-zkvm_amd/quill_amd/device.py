@@ -32,6 +32,15 @@ class Device:
         buf = (C.c_uint8 * 128).from_buffer_copy(unique_id)
         check(lib().qg_ctx_attach_comm(self.h, rank, world, buf), self.h)
 
+    def attach_loopback(self, group, rank: int):
+        check(lib().qg_ctx_attach_loopback(self.h, group, rank), self.h)
+
+    @staticmethod
+    def loopback_group(world: int):
+        g = C.c_void_p()
+        check(lib().qg_loopback_create(world, C.byref(g)))
+        return g
+
     @staticmethod
     def comm_unique_id() -> bytes:
         buf = (C.c_uint8 * 128)()

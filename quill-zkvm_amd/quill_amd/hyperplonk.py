@@ -208,6 +208,31 @@ class ZeroCheckProof:
         return (ZeroCheckProof(n, SumcheckProof(n, 0, r_polys)), EvaluationClaim(pt, e))
 
 
+def sumcheck_prove_tables(dev: Device, num_vars: int, tables, expr: VirtualPolyExpr,
+                          claimed_sum: int, transcript: Transcript, zerocheck: bool = False):
+    """qg_sumcheck_prove / qg_zerocheck_prove on host tables (lists of ints).
+    With a communicator attached, `num_vars` is global and `tables` are this
+    rank's blocks.  Returns (r_polys, point, evaluation)."""
+    prog, plen, carr, nc = _program_c(expr)
+    width = expr_degree(expr) + (2 if zerocheck else 1)
+    arrs, ptrs = _tables_c(tables)
+    coeffs = np.zeros((num_vars * width, 4), dtype=np.uint64)
+    lens = np.zeros(num_vars, dtype=np.uint32)
+    point = np.zeros((num_vars, 4), dtype=np.uint64)
+    ev = (C.c_uint64 * 4)()
+    L = lib()
+    if zerocheck:
+        rc = L.qg_zerocheck_prove(dev.h, num_vars, len(arrs), ptrs, prog, plen, u64p(carr), nc,
+                                  transcript.c_state(), u64p(coeffs),
+                                  lens.ctypes.data_as(C.POINTER(C.c_uint32)), u64p(point), ev, None)
+    else:
+        rc = L.qg_sumcheck_prove(dev.h, num_vars, len(arrs), ptrs, prog, plen, u64p(carr), nc,
+                                 fr_c(claimed_sum), transcript.c_state(), u64p(coeffs),
+                                 lens.ctypes.data_as(C.POINTER(C.c_uint32)), u64p(point), ev)
+    check(rc, dev.h)
+    return _unpack(num_vars, width, coeffs, lens, point, ev)
+
+
 def sumcheck_prove_device(dev: Device, num_vars: int, tables, expr: VirtualPolyExpr,
                           claimed_sum: int, transcript: Transcript):
     """Device-resident variant (tables are DeviceVec): the bench entry point."""
