@@ -40,16 +40,63 @@ def parse():
     ap.add_argument("--log-sumcheck", type=int, default=20)
     ap.add_argument("--no-sumcheck", action="store_true")
     ap.add_argument("--no-cpu-baseline", action="store_true")
-    ap.add_argument("--cpu-sample-log", type=int, default=16,
-                    help="log2 size of the CPU-baseline MSM sample")
+    ap.add_argument("--cpu-sample-log", type=int, default=20,
+                    help="log2 size of the CPU-baseline MSM sample (a prefix of the workload)")
+    ap.add_argument("--no-traffic", action="store_true",
+                    help="skip the two rocprofv3 PMC passes that measure HBM traffic")
+    ap.add_argument("--traffic-probe", action="store_true", help=argparse.SUPPRESS)
     return ap.parse_args()
+
+
+SC_KERNELS = ("k_sc_round", "k_sc_finish", "k_sc_tail", "k_sc_local_sum", "k_sc_fold_last",
+              "k_sc_transpose")
+
+
+def traffic_probe(args):
+    """Child of the PMC passes (pmc_traffic.py): one MSM, then one sumcheck."""
+    import quill_amd as q
+    from quill_amd.hyperplonk import VirtualPolyExpr as E, sumcheck_prove_device
+    dev = q.Device(0)
+    n = 1 << args.log_msm
+    srs = q.Srs.generate(dev, TAU, n)
+    scalars = q.DeviceVec(dev, n).fill_random(0x5155494C4C + 2)
+    srs.msm_dev(scalars)
+    srs.close()
+    scalars.close()
+    if not args.no_sumcheck:
+        N = 1 << args.log_sumcheck
+        tabs = [q.DeviceVec(dev, N).fill_random(0x5155494C4C + 3 + 7 * i) for i in range(3)]
+        sumcheck_prove_device(dev, args.log_sumcheck, tabs, E.Input(0) * E.Input(1) * E.Input(2),
+                              0, q.Transcript(b"sumcheck_bench"))
+        for t in tabs:
+            t.close()
+    dev.close()
+
+
+def measure_traffic(args):
+    import pmc_traffic
+    probe = ["--log-msm", str(args.log_msm), "--log-sumcheck", str(args.log_sumcheck)]
+    if args.no_sumcheck:
+        probe.append("--no-sumcheck")
+    try:
+        return pmc_traffic.collect(probe)
+    except Exception as e:  # reported, never substituted
+        return {"error": str(e)[-600:]}
+
+
+TAU = 0x5155494C4C2D53525321  # fixed synthetic trapdoor
 
 
 def main():
     args = parse()
+    if args.traffic_probe:
+        return traffic_probe(args)
     world = int(os.environ.get("WORLD_SIZE", "1"))
     rank = int(os.environ.get("RANK", "0"))
     local_rank = int(os.environ.get("LOCAL_RANK", "0"))
+    traffic = None
+    if world == 1 and not args.no_traffic:
+        traffic = measure_traffic(args)  # child processes, before this one touches the GPU
     dist = None
     if world > 1:
         import torch
@@ -81,9 +128,8 @@ def main():
         dev.attach_comm(rank, world, obj[0])
 
     n = 1 << args.log_msm
-    tau = 0x5155494C4C2D53525321  # fixed synthetic trapdoor
     t0 = time.perf_counter()
-    srs = q.Srs.generate(dev, tau, n, offset=rank * n)
+    srs = q.Srs.generate(dev, TAU, n, offset=rank * n)
     scalars = q.DeviceVec(dev, n).fill_random(0x5155494C4C + 2 + rank)
     setup_s = time.perf_counter() - t0
 
@@ -107,6 +153,10 @@ def main():
     acc_ms = max_over_ranks(kern["msm_accumulate"]["ms_avg"])
     achieved = MSM_BYTES_PER_SCALAR * n / (acc_ms * 1e-3) / 1e9
     fq_peak = dev.microbench_fq_mul()
+    c_bits, n_win = srs.window_info()
+    # executed: one mixed XYZZ add (8M + 2S = 10 Fq mults) per nonzero digit,
+    # W digits per scalar, in msm_accumulate (bucketing/reduce excluded)
+    exec_mults = 10 * n_win * n
 
     out = {
         "metric": "G1 MSM scalars/sec at 2^24 + sumcheck-prover ms at 2^20 vars (1/8 GPU)",
@@ -125,21 +175,34 @@ def main():
                    "log_msm": args.log_msm, "parallelism": f"msm-shard-by-base-index x{world}"},
         "roofline": {"bound": "hbm", "kernel": "msm_accumulate", "achieved": achieved,
                      "peak": HBM_PEAK_GBPS, "unit": "GB/s", "frac": achieved / HBM_PEAK_GBPS,
-                     "traffic": None,
+                     "traffic": _kernel_traffic(traffic, "k_msm_accumulate"),
+                     "algorithmic_bytes": MSM_BYTES_PER_SCALAR * n,
                      "note": "MSM is integer-VALU bound (no MFMA form): see compute"},
         "compute": {"fq_mul_per_s_peak_microbench": fq_peak,
-                    "fq_mul_equiv_per_scalar": MSM_FQMUL_PER_SCALAR,
-                    "achieved_fq_mul_per_s": MSM_FQMUL_PER_SCALAR * n / (ms_per_step * 1e-3),
-                    "frac": MSM_FQMUL_PER_SCALAR * n / (ms_per_step * 1e-3) / fq_peak},
+                    "survey_fq_mul_equiv_per_scalar": MSM_FQMUL_PER_SCALAR,
+                    "survey_equiv_fq_mul_per_s_whole_step": MSM_FQMUL_PER_SCALAR * n / (ms_per_step * 1e-3),
+                    "windows": n_win, "window_bits": c_bits,
+                    "accumulate_fq_mul_per_s": exec_mults / (acc_ms * 1e-3),
+                    "frac": exec_mults / (acc_ms * 1e-3) / fq_peak,
+                    "frac_note": "msm_accumulate's executed Fq mults (10 per digit x W digits "
+                                 "per scalar) / microbenchmarked Fq-mul peak"},
         "kernels_ms": kern,
         "setup_s": setup_s,
         "commitment_x_low64": hex(0 if res is None else res[0] & ((1 << 64) - 1)),
     }
 
+    if traffic is not None:
+        out["pmc"] = traffic
     if not args.no_sumcheck:
         out["sumcheck"] = bench_sumcheck(q, dev, args, barrier_sync, max_over_ranks, rank)
+        if traffic is not None and "error" not in traffic:
+            tot = sum((traffic[k]["read_bytes_per_launch"] + traffic[k]["write_bytes_per_launch"])
+                      * traffic[k]["launches"] for k in SC_KERNELS if k in traffic)
+            out["sumcheck"]["roofline"]["traffic"] = tot
     if rank == 0 and not args.no_cpu_baseline:
-        out["cpu_baseline"] = cpu_baseline(args)
+        out["cpu_baseline"] = cpu_baseline(args, srs, scalars)
+        if not args.no_sumcheck:
+            out["sumcheck"]["cpu_baseline"] = cpu_baseline_sumcheck(args)
     if rank == 0:
         print(json.dumps(out))
     srs.close()
@@ -185,14 +248,51 @@ def bench_sumcheck(q, dev, args, barrier_sync, max_over_ranks, rank):
             "tail_kernel_ms_per_call": tl_ms / max(args.steps, 1)}
 
 
-def cpu_baseline(args):
-    """Oracle C restatement of arkworks' single-thread Pippenger (oracle/_build)."""
+def _kernel_traffic(traffic, kernel):
+    """HBM bytes per launch (PMC, corrected) or None"""
+    if not traffic or "error" in traffic or kernel not in traffic:
+        return None
+    d = traffic[kernel]
+    return d["read_bytes_per_launch"] + d["write_bytes_per_launch"]
+
+
+def _oracle_c():
     sys.path.insert(0, os.path.join(ROOT, "oracle"))
+    import oracle_c
+    oracle_c.lib()
+    return oracle_c
+
+
+def cpu_baseline(args, srs, scalars):
+    """Oracle C restatement of arkworks' single-thread Pippenger (oracle/_build),
+    on a prefix of this run's own SRS and scalars; the GPU MSM of the same
+    prefix must give the same point."""
     try:
-        import oracle_c
+        oc = _oracle_c()
     except Exception as e:  # the checker is missing: report, do not substitute
         return {"value": None, "unit": "scalars/s", "error": f"oracle C library unavailable: {e}"}
-    return oracle_c.bench_msm_baseline(args.cpu_sample_log)
+    ns = min(1 << args.cpu_sample_log, len(srs))
+    xy, inf = srs.download_raw(0, ns)
+    sc = scalars.to_numpy(ns)
+    tm, tc, (cxy, cinf) = oc.bench_msm_arrays(xy, inf, sc)
+    from quill_amd.field import g1_from_abi
+    gpu = srs.msm_dev(scalars, ns)
+    return {"value": ns / tm, "unit": "scalars/s", "cores": 1, "kind": "port",
+            "sample": f"the first 2^{args.cpu_sample_log} bases and scalars of the timed "
+                      f"workload, one msm_unchecked ({tm:.2f} s, single thread like the "
+                      f"reference); KZG::commit as written (+ into_affine of every SRS point) "
+                      f"{ns / tc:.4g} scalars/s",
+            "seconds": tm, "kzg_commit_as_written_scalars_per_s": ns / tc,
+            "matches_gpu_msm_of_sample": g1_from_abi(cxy, cinf) == gpu,
+            "cpu_model": oc.cpu_model()}
+
+
+def cpu_baseline_sumcheck(args):
+    try:
+        oc = _oracle_c()
+    except Exception as e:
+        return {"ms": None, "error": f"oracle C library unavailable: {e}"}
+    return oc.bench_sumcheck_baseline(args.log_sumcheck)
 
 
 if __name__ == "__main__":

@@ -102,6 +102,9 @@ int qg_srs_generate_range(qg_ctx* ctx, const uint64_t tau[4], const uint64_t* g_
                           uint64_t offset, size_t n, qg_srs** out);
 int qg_srs_destroy(qg_srs* srs);
 size_t qg_srs_len(const qg_srs* srs);
+/* MSM window geometry of this SRS: signed-digit window bits c and window
+ * count W (the tables hold W shifted copies of the bases). */
+int qg_srs_window_info(const qg_srs* srs, int* c, int* windows);
 /* Copy bases [offset, offset+n) back to the host (affine, Montgomery). */
 int qg_srs_download(const qg_srs* srs, size_t offset, size_t n, uint64_t* affine_xy,
                     uint8_t* infinity);

@@ -347,6 +347,42 @@ int oc_msm(const uint64_t* bases_xy, const uint8_t* inf, const uint64_t* scalars
   return 0;
 }
 
+/* CPU baseline on caller-provided arrays (e.g. a prefix of the GPU bench's own
+ * SRS and scalars): times msm_ark alone and KZG::commit as written, i.e. plus
+ * the per-call into_affine of every (projective) SRS point (kzg.rs:67-71). */
+int oc_bench_msm_arrays(const uint64_t* bases_xy, const uint8_t* inf, const uint64_t* scalars,
+                        size_t n, double* t_msm, double* t_commit, uint64_t out_xy[8],
+                        uint8_t* out_inf) {
+  g1a* b = (g1a*)malloc(sizeof(g1a) * (n ? n : 1));
+  g1j* proj = (g1j*)malloc(sizeof(g1j) * (n ? n : 1));
+  fp z = f_add(&FQ, f_one(&FQ), f_one(&FQ));
+  fp z2 = f_mul(&FQ, z, z), z3 = f_mul(&FQ, z2, z);
+  for (size_t i = 0; i < n; i++) {
+    memcpy(b[i].x.v, bases_xy + 8 * i, 32);
+    memcpy(b[i].y.v, bases_xy + 8 * i + 4, 32);
+    b[i].inf = inf ? inf[i] : 0;
+    proj[i].x = f_mul(&FQ, b[i].x, z2);
+    proj[i].y = f_mul(&FQ, b[i].y, z3);
+    proj[i].z = b[i].inf ? (fp){{0, 0, 0, 0}} : z;
+  }
+  double a = now_s();
+  g1j r = msm_ark(b, (const fp*)scalars, n);
+  double m = now_s();
+  g1a* conv = (g1a*)malloc(sizeof(g1a) * (n ? n : 1));
+  for (size_t i = 0; i < n; i++) conv[i] = j_to_affine(&proj[i]);
+  double c = now_s();
+  *t_msm = m - a;
+  *t_commit = c - a;
+  g1a ra = j_to_affine(&r);
+  memcpy(out_xy, ra.x.v, 32);
+  memcpy(out_xy + 4, ra.y.v, 32);
+  *out_inf = (uint8_t)ra.inf;
+  free(b);
+  free(proj);
+  free(conv);
+  return 0;
+}
+
 /* [tau^i] g for i < n via a 32 x 256 fixed-base comb on g (bases for the baseline) */
 static void gen_srs(fp tau_mont, size_t n, g1a* out) {
   const modulus* m = &FQ;

@@ -28,6 +28,9 @@ def lib():
                                    C.POINTER(C.c_double), U64P]
         L.oc_sumcheck_prod.argtypes = [C.c_int, C.c_int, U64P, U64P, C.POINTER(C.c_uint8), U64P,
                                        C.POINTER(C.c_uint32), U64P, U64P]
+        L.oc_bench_msm_arrays.argtypes = [U64P, C.POINTER(C.c_uint8), U64P, C.c_size_t,
+                                          C.POINTER(C.c_double), C.POINTER(C.c_double), U64P,
+                                          C.POINTER(C.c_uint8)]
         L.oc_bench_sumcheck.argtypes = [C.c_int, C.c_uint64, C.POINTER(C.c_double)]
         _lib = L
     return _lib
@@ -112,6 +115,25 @@ def bench_msm_baseline(log_n: int = 18, seed: int = 0x5155494C4C):
                       f"(+ into_affine of every SRS point) {n / tc.value:.4g} scalars/s",
             "seconds": tm.value, "kzg_commit_as_written_scalars_per_s": n / tc.value,
             "cpu_model": cpu_model()}
+
+
+def bench_msm_arrays(xy, inf, scalars):
+    """Single-thread arkworks-faithful Pippenger on caller arrays: xy (n, 8)
+    uint64 affine Montgomery, inf (n,) uint8, scalars (n, 4) uint64 Montgomery.
+    Returns (seconds_msm, seconds_commit_as_written, (xy limbs, inf))."""
+    import numpy as np
+    n = len(inf)
+    xy = np.ascontiguousarray(xy, dtype=np.uint64)
+    inf = np.ascontiguousarray(inf, dtype=np.uint8)
+    sc = np.ascontiguousarray(scalars, dtype=np.uint64)
+    tm, tc = C.c_double(), C.c_double()
+    out = (C.c_uint64 * 8)()
+    oinf = C.c_uint8()
+    P64, P8 = C.POINTER(C.c_uint64), C.POINTER(C.c_uint8)
+    lib().oc_bench_msm_arrays(xy.ctypes.data_as(P64), inf.ctypes.data_as(P8),
+                              sc.ctypes.data_as(P64), C.c_size_t(n), C.byref(tm), C.byref(tc),
+                              out, C.byref(oinf))
+    return tm.value, tc.value, (list(out), oinf.value)
 
 
 def bench_sumcheck_baseline(log_n: int = 16, seed: int = 0x5155494C4C):

@@ -301,6 +301,111 @@ QG_HD Fr transcript_draw_fr_words(uint32_t st[8]) {
   return lo * Fr::from_raw(FrP::R2) + hi * Fr::from_raw(FrP::R3);
 }
 
+
+#if defined(__HIPCC__) || defined(__HIP__)
+// ---------------------------------------------------------------------------
+// Quad-lane BLAKE3 for the device transcript's critical path.  The 4x4 state
+// is split by columns over the 4 lanes of a DPP quad: lane l holds
+// (v[l], v[4+l], v[8+l], v[12+l]).  The column step is one G per lane; the
+// diagonal step rotates rows b, c, d by 1, 2, 3 lanes with DPP quad_perm moves
+// and back.  Latency is one G chain per half-round instead of four.
+// Every quad of the calling wave computes the same hash (inputs uniform).
+// ---------------------------------------------------------------------------
+struct B3Sched {
+  int s[7][16];
+};
+
+constexpr B3Sched b3_make_sched() {
+  B3Sched r{};
+  const int perm[16] = {2, 6, 3, 10, 7, 0, 4, 13, 1, 11, 12, 5, 9, 14, 15, 8};
+  for (int i = 0; i < 16; i++) r.s[0][i] = i;
+  for (int k = 1; k < 7; k++)
+    for (int i = 0; i < 16; i++) r.s[k][i] = r.s[k - 1][perm[i]];
+  return r;
+}
+
+// word for lane l of a quad: (w0, w1, w2, w3)[l]   (l uniform per lane)
+QG_DEV uint32_t b3_pick4(uint32_t l, uint32_t w0, uint32_t w1, uint32_t w2, uint32_t w3) {
+  const uint32_t lo = (l & 1) ? w1 : w0, hi = (l & 1) ? w3 : w2;
+  return (l & 2) ? hi : lo;
+}
+
+template <int CTRL>
+QG_DEV uint32_t b3_qperm(uint32_t x) {
+  return (uint32_t)__builtin_amdgcn_mov_dpp((int)x, CTRL, 0xF, 0xF, false);
+}
+
+QG_DEV void b3_g1(uint32_t& a, uint32_t& b, uint32_t& c, uint32_t& d, uint32_t mx, uint32_t my) {
+  a = a + b + mx;
+  d = b3_rotr(d ^ a, 16);
+  c = c + d;
+  b = b3_rotr(b ^ c, 12);
+  a = a + b + my;
+  d = b3_rotr(d ^ a, 8);
+  c = c + d;
+  b = b3_rotr(b ^ c, 7);
+}
+
+// One compression.  cvl/cvh: this lane's chaining words cv[l], cv[4+l];
+// m: the (uniform) 16 message words.  Returns this lane's output words
+// o0 = out[l], o1 = out[4+l], o2 = out[8+l], o3 = out[12+l].
+QG_DEV void b3_compress_quad(uint32_t l, uint32_t cvl, uint32_t cvh, const uint32_t (&m)[16],
+                             uint64_t counter, uint32_t blen, uint32_t flags, uint32_t& o0,
+                             uint32_t& o1, uint32_t& o2, uint32_t& o3) {
+  constexpr B3Sched S = b3_make_sched();
+  uint32_t a = cvl, b = cvh;
+  uint32_t c = b3_pick4(l, 0x6A09E667u, 0xBB67AE85u, 0x3C6EF372u, 0xA54FF53Au);
+  uint32_t d = b3_pick4(l, (uint32_t)counter, (uint32_t)(counter >> 32), blen, flags);
+#pragma unroll
+  for (int r = 0; r < 7; r++) {
+    b3_g1(a, b, c, d, b3_pick4(l, m[S.s[r][0]], m[S.s[r][2]], m[S.s[r][4]], m[S.s[r][6]]),
+          b3_pick4(l, m[S.s[r][1]], m[S.s[r][3]], m[S.s[r][5]], m[S.s[r][7]]));
+    // diagonalize: b <- lane l+1, c <- lane l+2, d <- lane l+3 (mod 4)
+    b = b3_qperm<0x39>(b);
+    c = b3_qperm<0x4E>(c);
+    d = b3_qperm<0x93>(d);
+    b3_g1(a, b, c, d, b3_pick4(l, m[S.s[r][8]], m[S.s[r][10]], m[S.s[r][12]], m[S.s[r][14]]),
+          b3_pick4(l, m[S.s[r][9]], m[S.s[r][11]], m[S.s[r][13]], m[S.s[r][15]]));
+    b = b3_qperm<0x93>(b);
+    c = b3_qperm<0x4E>(c);
+    d = b3_qperm<0x39>(d);
+  }
+  o0 = a ^ c;
+  o1 = b ^ d;
+  o2 = c ^ cvl;
+  o3 = d ^ cvh;
+}
+
+// BLAKE3 of a word message in LDS (<= 1024 bytes; bytes past nbytes up to the
+// next 64-byte boundary must be zero), root output words [0, nout) (nout <= 16)
+// written to out (LDS or global) by lanes 0..3.  Call with the whole wave.
+QG_DEV void b3_hash_quad(const uint32_t* msg, uint32_t nbytes, uint32_t* out, int nout) {
+  const uint32_t lane = __lane_id(), l = lane & 3;
+  uint32_t cvl = b3_pick4(l, 0x6A09E667u, 0xBB67AE85u, 0x3C6EF372u, 0xA54FF53Au);
+  uint32_t cvh = b3_pick4(l, 0x510E527Fu, 0x9B05688Cu, 0x1F83D9ABu, 0x5BE0CD19u);
+  const uint32_t nblocks = nbytes ? (nbytes + 63) / 64 : 1;
+  for (uint32_t bi = 0; bi < nblocks; bi++) {
+    uint32_t m[16];
+#pragma unroll
+    for (int i = 0; i < 16; i++) m[i] = msg[bi * 16 + i];
+    const bool last = bi + 1 == nblocks;
+    const uint32_t blen = last ? nbytes - bi * 64 : 64u;
+    const uint32_t flags = (bi == 0 ? B3_CHUNK_START : 0u) | (last ? (B3_CHUNK_END | B3_ROOT) : 0u);
+    uint32_t o0, o1, o2, o3;
+    b3_compress_quad(l, cvl, cvh, m, 0, blen, flags, o0, o1, o2, o3);
+    if (!last) {
+      cvl = o0;
+      cvh = o1;
+    } else if (lane < 4) {
+      if ((int)l < nout) out[l] = o0;
+      if ((int)(4 + l) < nout) out[4 + l] = o1;
+      if ((int)(8 + l) < nout) out[8 + l] = o2;
+      if ((int)(12 + l) < nout) out[12 + l] = o3;
+    }
+  }
+}
+#endif
+
 // ---------------------------------------------------------------------------
 // Transcript primitives over a 32-byte state
 // ---------------------------------------------------------------------------

@@ -56,9 +56,17 @@ struct qg_ctx {
   std::vector<Ev> pending;
   std::map<std::string, std::pair<double, uint32_t>> ktime;
   std::vector<hipEvent_t> event_pool;
+  // small per-context memo (e.g. which program image the device copy holds)
+  std::map<std::string, std::string> memo;
   // RCCL
   qg_comm_state* comm = nullptr;
   int rank = 0, world = 1;
+
+  int cus = 0;  // compute units of `device` (cached)
+  int num_cus() {
+    if (!cus) QG_HIP(hipDeviceGetAttribute(&cus, hipDeviceAttributeMultiprocessorCount, device));
+    return cus;
+  }
 
   void* scratch_get(const std::string& slot, size_t bytes) {
     auto it = scratch.find(slot);

@@ -918,6 +918,13 @@ int qg_srs_destroy(qg_srs* srs) {
 
 size_t qg_srs_len(const qg_srs* srs) { return srs ? srs->n : 0; }
 
+int qg_srs_window_info(const qg_srs* srs, int* c, int* windows) {
+  if (!srs) return QG_ERR_INVALID;
+  if (c) *c = srs->c;
+  if (windows) *windows = srs->W;
+  return QG_OK;
+}
+
 int qg_srs_download(const qg_srs* srs, size_t offset, size_t n, uint64_t* affine_xy,
                     uint8_t* infinity) {
   if (!srs || (!affine_xy && n) || offset + n > srs->n) return QG_ERR_INVALID;

@@ -21,13 +21,17 @@
 //    interpolates (inverse Vandermonde on t = 0..d), trims, serializes, runs the
 //    BLAKE3 transcript on the device and writes r_j for the next fold.  No host
 //    round trip inside the protocol.
-//  * Once a table has <= 2^TAIL_LOG entries the remaining rounds run inside one
+//  * Once a table has <= 2^PERS_LOG entries the remaining rounds run inside one
 //    workgroup (fold + evaluate + transcript per round, synchronized by
 //    barriers), removing 2 launches per round.
+#include <stddef.h>
 #include <string.h>
 
 #include <algorithm>
+#include <atomic>
 #include <map>
+#include <memory>
+#include <mutex>
 #include <vector>
 
 #include "blake3.h"
@@ -37,9 +41,24 @@ using namespace qg;
 
 namespace qg {
 
+// Phase timestamps (s_memrealtime, 100 MHz) for latency work: build with
+// -DQG_SC_TRACE (make trace) and read them with qg_debug_sc_trace.
+#ifdef QG_SC_TRACE
+__device__ unsigned long long g_sc_trace[2048];
+#define SC_TR(idx)                                                   \
+  do {                                                               \
+    if (threadIdx.x == 0 && (idx) < 2048) g_sc_trace[idx] = wall_clock64(); \
+  } while (0)
+#else
+#define SC_TR(idx) \
+  do {             \
+  } while (0)
+#endif
+
 static constexpr int SC_BLOCK = 256;
-static constexpr int SC_MAX_BLOCKS = 1024;
-static constexpr int TAIL_LOG = 8;   // single-workgroup tail once tables have <= 2^8 entries
+static constexpr int SC_MAX_BLOCKS = 2048;
+static constexpr int TAIL_BLOCK = 512;  // persistent-kernel block
+static constexpr int PERS_LOG = 16;     // tables of <= 2^16 entries: rounds run in one persistent launch
 
 // ---------------------------------------------------------------- programs
 struct Mono {
@@ -156,22 +175,32 @@ static SopProgram compile_program(const qg_expr_op* prog, size_t len, const uint
   return sp;
 }
 
-// device-side program image (read with uniform loads)
+// device-side program image.  The byte arrays and the header are copied into
+// LDS by every block (one parallel load, no dependent scalar-cache misses on the
+// evaluation path); coefficients and the inverse Vandermonde rows follow.
+static constexpr int SOP_MAXM = 256, SOP_MAXF = 1024;
+static constexpr uint32_t SOP_HDR_WORDS = (16 + 2 * SOP_MAXM + SOP_MAXF) / 4;
+
 struct SopDev {
-  uint32_t nmono;
-  uint32_t nslots;
-  uint32_t np;  // evaluation points = degree + 1
-  uint32_t pad;
-  uint32_t mono_len[256];
-  uint8_t fac[1024];
-  uint8_t is_one[256];
-  Fr coeff[256];
-  Fr vinv[16 * 16];  // inverse Vandermonde on nodes 0..np-1 (row = coefficient)
+  uint32_t nmono, nslots, np, nfac;
+  uint8_t mono_len[SOP_MAXM];
+  uint8_t is_one[SOP_MAXM];
+  uint8_t fac[SOP_MAXF];
+  Fr coeff[SOP_MAXM];
+  // inverse Vandermonde on nodes 0..np-1: coefficient t = sum_u V[t][u] ev[u].
+  Fr vinv_m[16 * 16];  // Montgomery form
+  Fr vinv_c[16 * 16];  // plain integers: mont_mul(vinv_c, ev) is the canonical product
+};
+static_assert(offsetof(SopDev, coeff) == SOP_HDR_WORDS * 4, "SopDev layout");
+
+// program header passed by value (no dependent loads before the LDS copy)
+struct SopHdr {
+  uint32_t nmono, nslots, np, pad;
 };
 
-static void build_vinv(uint32_t np, Fr* out) {
+static void build_vinv(uint32_t np, Fr* out_m, Fr* out_c) {
   // coefficients of L_j(X) = prod_{m != j} (X - m) / (j - m), out[i*16 + j] = coeff_i(L_j)
-  for (uint32_t i = 0; i < 16 * 16; i++) out[i] = Fr::zero();
+  for (uint32_t i = 0; i < 16 * 16; i++) out_m[i] = out_c[i] = Fr::zero();
   for (uint32_t j = 0; j < np; j++) {
     std::vector<Fr> poly(1, Fr::one());
     Fr den = Fr::one();
@@ -188,7 +217,38 @@ static void build_vinv(uint32_t np, Fr* out) {
       den = den * diff;
     }
     Fr dinv = finv(den);
-    for (uint32_t i = 0; i < np; i++) out[i * 16 + j] = poly[i] * dinv;
+    for (uint32_t i = 0; i < np; i++) {
+      out_m[i * 16 + j] = poly[i] * dinv;
+      out_c[i * 16 + j] = from_mont(out_m[i * 16 + j]);
+    }
+  }
+}
+
+template <int NP>
+struct SopLds {
+  uint32_t w[SOP_HDR_WORDS];
+  Fr coeff[SOP_MAXM];
+  Fr vm[NP * NP];
+  Fr vc[NP * NP];
+  QG_DEV uint32_t nmono() const { return w[0]; }
+  QG_DEV uint32_t mono_len(uint32_t m) const { return ((const uint8_t*)w)[16 + m]; }
+  QG_DEV uint32_t is_one(uint32_t m) const { return ((const uint8_t*)w)[16 + SOP_MAXM + m]; }
+  QG_DEV uint32_t fac(uint32_t f) const { return ((const uint8_t*)w)[16 + 2 * SOP_MAXM + f]; }
+};
+
+template <int NP>
+QG_DEV void sop_load(SopLds<NP>& s, const SopDev* __restrict__ g, const SopHdr& h, bool vinv) {
+  const uint32_t* gw = reinterpret_cast<const uint32_t*>(g);
+  for (uint32_t i = threadIdx.x; i < SOP_HDR_WORDS; i += blockDim.x) s.w[i] = gw[i];
+  const uint32_t* gc = reinterpret_cast<const uint32_t*>(g->coeff);
+  uint32_t* lc = reinterpret_cast<uint32_t*>(s.coeff);
+  for (uint32_t i = threadIdx.x; i < h.nmono * 8; i += blockDim.x) lc[i] = gc[i];
+  if (vinv) {
+    for (uint32_t i = threadIdx.x; i < h.np * h.np * 8; i += blockDim.x) {
+      const uint32_t e = i >> 3, k = i & 7, t = e / h.np, u = e % h.np;
+      s.vm[t * NP + u].v[k] = g->vinv_m[t * 16 + u].v[k];
+      s.vc[t * NP + u].v[k] = g->vinv_c[t * 16 + u].v[k];
+    }
   }
 }
 
@@ -211,21 +271,21 @@ QG_DEV Fr sel(const Fr (&v)[K], uint32_t i) {
   }
 }
 
-// h(values) via the monomial program
-template <int K>
-QG_DEV Fr sop_eval(const SopDev* __restrict__ sp, const Fr (&val)[K]) {
+// h(values) via the monomial program (single point)
+template <int K, int NP>
+QG_DEV Fr sop_eval(const SopLds<NP>& sp, const Fr (&val)[K]) {
   Fr acc = Fr::zero();
   uint32_t f = 0;
-  const uint32_t nmono = sp->nmono;
+  const uint32_t nmono = sp.nmono();
   for (uint32_t m = 0; m < nmono; m++) {
-    const uint32_t len = sp->mono_len[m];
+    const uint32_t len = sp.mono_len(m);
     Fr prod;
     if (len == 0) {
-      prod = sp->coeff[m];
+      prod = sp.coeff[m];
     } else {
-      prod = sel<K>(val, sp->fac[f]);
-      for (uint32_t q = 1; q < len; q++) prod = prod * sel<K>(val, sp->fac[f + q]);
-      if (!sp->is_one[m]) prod = prod * sp->coeff[m];
+      prod = sel<K>(val, sp.fac(f));
+      for (uint32_t q = 1; q < len; q++) prod = prod * sel<K>(val, sp.fac(f + q));
+      if (!sp.is_one(m)) prod = prod * sp.coeff[m];
     }
     f += len;
     acc = acc + prod;
@@ -238,59 +298,6 @@ struct TablePtrs {
   Fr* dst[8];
 };
 
-// Load pair p (fold or not) of every slot -> low/diff
-template <int K>
-QG_DEV void load_pair(const TablePtrs& tp, uint32_t nslots, size_t p, bool fold, const Fr& r,
-                      Fr (&lo)[K], Fr (&df)[K]) {
-#pragma unroll
-  for (int i = 0; i < K; i++) {
-    if ((uint32_t)i < nslots) {
-      Fr a, b;
-      if (fold) {
-        const Fr* s = tp.src[i] + 4 * p;
-        Fr x0 = s[0], x1 = s[1], x2 = s[2], x3 = s[3];
-        a = x0 + r * (x1 - x0);
-        b = x2 + r * (x3 - x2);
-        tp.dst[i][2 * p] = a;
-        tp.dst[i][2 * p + 1] = b;
-      } else {
-        const Fr* s = tp.src[i] + 2 * p;
-        a = s[0];
-        b = s[1];
-      }
-      lo[i] = a;
-      df[i] = b - a;
-    } else {
-      lo[i] = Fr::zero();
-      df[i] = Fr::zero();
-    }
-  }
-}
-
-// Evaluation points t = T..NPMAX-1 by template recursion, so sums[] is only
-// ever indexed by compile-time constants (a runtime-indexed accumulator array
-// is demoted to scratch memory).
-template <int T, int K, int NPMAX>
-QG_DEV void eval_points(const SopDev* __restrict__ sp, uint32_t np, Fr (&lo)[K], const Fr (&df)[K],
-                        Fr (&sums)[NPMAX]) {
-  if constexpr (T < NPMAX) {
-    if ((uint32_t)T < np) {
-      if constexpr (T > 0) {
-#pragma unroll
-        for (int i = 0; i < K; i++) lo[i] = lo[i] + df[i];
-      }
-      sums[T] = sums[T] + sop_eval<K>(sp, lo);
-      eval_points<T + 1, K, NPMAX>(sp, np, lo, df, sums);
-    }
-  }
-}
-
-template <int K, int NPMAX>
-QG_DEV void eval_pair(const SopDev* __restrict__ sp, Fr (&lo)[K], const Fr (&df)[K],
-                      Fr (&sums)[NPMAX]) {
-  eval_points<0, K, NPMAX>(sp, sp->np, lo, df, sums);
-}
-
 QG_DEV Fr shfl_xor_fr(const Fr& a, int m) {
   Fr r;
 #pragma unroll
@@ -298,189 +305,404 @@ QG_DEV Fr shfl_xor_fr(const Fr& a, int m) {
   return r;
 }
 
-// block-wide sum of NPMAX field values (LDS scratch: (blockDim/64) * NPMAX Fr)
-template <int NPMAX>
-QG_DEV void block_sum(Fr (&s)[NPMAX], uint32_t np, Fr* lds) {
+// t * x for a small per-lane integer t < NP (branch-free double-and-add)
+template <int NP>
+QG_DEV Fr mul_small(const Fr& x, uint32_t t) {
+  Fr acc = (t & 1u) ? x : Fr::zero();
+  Fr y = x;
 #pragma unroll
-  for (int t = 0; t < NPMAX; t++) {
-    if ((uint32_t)t < np) {
-      for (int m = 32; m > 0; m >>= 1) s[t] = s[t] + shfl_xor_fr(s[t], m);
-    }
+  for (int b = 1; (1 << b) < NP; b++) {
+    y = y + y;
+    acc = acc + (((t >> b) & 1u) ? y : Fr::zero());
   }
-  const int lane = threadIdx.x & 63, wid = threadIdx.x >> 6, nw = blockDim.x >> 6;
-  if (lane == 0) {
+  return acc;
+}
+
+// ---------------------------------------------------------------------------
+// Work layout of a round.  A block handles PB = BLOCK / NP pairs per step:
+//   phase F: items (slot, pair, half) — fold (x0 + r (x1 - x0)) or copy one
+//            entry of the next table into LDS (and HBM when folding);
+//   phase E: thread (pair = tid / NP, point t = tid % NP) evaluates h at
+//            lo + t (hi - lo) and accumulates its own point's sum.
+// Every thread carries one field accumulator, so registers stay low (high
+// occupancy on the large rounds) and the dependent chain per round is one
+// fold multiply plus deg-1 product multiplies (low latency on the small ones).
+// ---------------------------------------------------------------------------
+template <int K, int NP, int BLOCK>
+struct RoundLds {
+  Fr F[K * (BLOCK / NP) * 2];  // [slot][pair][half]
+  const Fr* src[8];
+  Fr* dst[8];
+};
+
+template <int K, int NP, int BLOCK>
+QG_DEV void round_sweep(RoundLds<K, NP, BLOCK>& L, const SopLds<NP>& sp, const SopHdr& h,
+                        size_t npairs, bool fold, const Fr& r, size_t base0, size_t stride,
+                        Fr& acc) {
+  constexpr uint32_t PB = BLOCK / NP;
+  const uint32_t tid = threadIdx.x, t = tid % NP, pl = tid / NP;
+  const uint32_t nitems = h.nslots * PB * 2;
+  for (size_t base = base0; base < npairs; base += stride) {
+    for (uint32_t it = tid; it < nitems; it += BLOCK) {
+      const uint32_t s = it / (PB * 2), e = it % (PB * 2);
+      const size_t p = base + (e >> 1);
+      Fr v = Fr::zero();
+      if (p < npairs) {
+        if (fold) {
+          const Fr* src = L.src[s] + 4 * p + 2 * (e & 1);
+          const Fr x0 = src[0], x1 = src[1];
+          v = x0 + r * (x1 - x0);
+          L.dst[s][2 * p + (e & 1)] = v;
+        } else {
+          v = L.src[s][2 * p + (e & 1)];
+        }
+      }
+      L.F[s * PB * 2 + e] = v;
+    }
+    __syncthreads();
+    if (t < h.np && base + pl < npairs) {
+      Fr sum = Fr::zero();
+      uint32_t f = 0;
+      for (uint32_t m = 0; m < h.nmono; m++) {
+        const uint32_t len = sp.mono_len(m);
+        Fr prod;
+        if (len == 0) {
+          prod = sp.coeff[m];
+        } else {
+          for (uint32_t q = 0; q < len; q++) {
+            const uint32_t s = sp.fac(f + q);
+            const Fr lo = L.F[(s * PB + pl) * 2], hi = L.F[(s * PB + pl) * 2 + 1];
+            const Fr v = lo + mul_small<NP>(hi - lo, t);
+            prod = q == 0 ? v : prod * v;
+          }
+          if (!sp.is_one(m)) prod = prod * sp.coeff[m];
+        }
+        f += len;
+        sum = sum + prod;
+      }
+      acc = acc + sum;
+    }
+    __syncthreads();
+  }
+}
+
+// Sum of acc over the threads of each point t (t = tid % NP) -> res[t] (LDS),
+// visible to all threads on return.  red: (BLOCK / 64) * NP LDS scratch.
+template <int NP>
+QG_DEV void block_reduce_pts(Fr acc, uint32_t np, Fr* red, Fr* res) {
 #pragma unroll
-    for (int t = 0; t < NPMAX; t++)
-      if ((uint32_t)t < np) lds[wid * NPMAX + t] = s[t];
+  for (int m = 32; m >= NP; m >>= 1) acc = acc + shfl_xor_fr(acc, m);
+  const uint32_t lane = threadIdx.x & 63, wid = threadIdx.x >> 6, nw = blockDim.x >> 6;
+  if (lane < NP) red[wid * NP + lane] = acc;
+  __syncthreads();
+  if (threadIdx.x < np) {
+    Fr a = red[threadIdx.x];
+    for (uint32_t w = 1; w < nw; w++) a = a + red[w * NP + threadIdx.x];
+    res[threadIdx.x] = a;
   }
   __syncthreads();
-  if (threadIdx.x == 0) {
+}
+
+// Round bookkeeping.  The transcript state, the deferred absorb and the
+// last-block election counter live in one small device struct.
+struct ScState {
+  uint32_t state[8];  // absorbed transcript state
+  uint32_t pend[20];  // state' || 48 challenge bytes of the last round, not yet absorbed
+  uint32_t ticket;    // blocks of the current round that have published partials
+  uint32_t pad[3];
+};
+
+struct RoundOut {
+  ScState* st;
+  Fr* chal;          // nvars challenges
+  Fr* coeffs;        // nvars x width (Montgomery)
+  uint32_t* lens;    // nvars
+  uint32_t width;    // row width (>= np)
+};
+
+struct FinSmem {
+  uint32_t msg[144];  // state || u64 len || coefficients (canonical LE) || zero pad
+  uint32_t chin[16];  // state' || "challenge" || zero pad
+  uint32_t xof[16];   // B3-XOF(state' || "challenge")[0..64)
+  uint32_t ab[32];    // state' || challenge bytes || zero pad (absorb)
+  Fr r;               // the round challenge (Montgomery)
+};
+
+// Round message, transcript and challenge from the np round sums ev[] (LDS).
+// Whole block calls (barriers); wave 0 works.  Interpolation is lane-parallel
+// over (coefficient t, node u): each lane multiplies by the inverse
+// Vandermonde entry in Montgomery form (proof output) and as a plain integer
+// (the canonical transcript bytes, no separate from_mont), then a shuffle sum
+// over u.  Trim by ballot; BLAKE3 on one DPP quad; r from two lanes.
+// Absorbing the 48 challenge bytes is deferred when pend_out != nullptr.
+template <int NP>
+QG_DEV void finish_core(const SopLds<NP>& sp, uint32_t np, const Fr* ev, const RoundOut& ro,
+                        uint32_t j, FinSmem& fs, const uint32_t* state_in, uint32_t* pend_out,
+                        uint32_t* state_out, uint32_t tr = 4096, bool writer = true) {
+  constexpr uint32_t U = NP <= 8 ? NP : 4;  // lanes per coefficient
+  const uint32_t tid = threadIdx.x;
+  const bool w0 = tid < 64;
+  const uint32_t ct = tid / U, cu = tid % U;
+  Fr cm = Fr::zero(), cc = Fr::zero();
+  if (w0 && ct < np) {
+    for (uint32_t u = cu; u < np; u += U) {
+      const Fr e = ev[u];
+      cm = cm + sp.vm[ct * NP + u] * e;
+      cc = cc + sp.vc[ct * NP + u] * e;
+    }
+  }
 #pragma unroll
-    for (int t = 0; t < NPMAX; t++) {
-      if ((uint32_t)t < np) {
-        Fr acc = lds[t];
-        for (int w = 1; w < nw; w++) acc = acc + lds[w * NPMAX + t];
-        s[t] = acc;
+  for (uint32_t m = 1; m < U; m <<= 1) {
+    cm = cm + shfl_xor_fr(cm, m);
+    cc = cc + shfl_xor_fr(cc, m);
+  }
+  const bool lead = w0 && cu == 0 && ct < np;
+  if (writer) {
+    if (lead) ro.coeffs[(size_t)j * ro.width + ct] = cm;
+    for (uint32_t i = np + tid; i < ro.width; i += blockDim.x)
+      ro.coeffs[(size_t)j * ro.width + i] = Fr::zero();
+  }
+  const uint64_t nz = __ballot(lead && !cc.is_zero());
+  // highest nonzero coefficient: lane index / U + 1 (wave 0's ballot)
+  const uint32_t len = nz ? (63u - (uint32_t)__clzll(nz)) / U + 1u : 0u;
+  if (tid < 8) fs.msg[tid] = state_in[tid];
+  if (lead) {
+#pragma unroll
+    for (int i = 0; i < 8; i++) fs.msg[10 + 8 * ct + i] = cc.v[i];
+  }
+  for (uint32_t i = 10 + 8 * np + tid; i < 144; i += blockDim.x) fs.msg[i] = 0;
+  if (tid == 0) {
+    fs.msg[8] = len;
+    fs.msg[9] = 0;
+    fs.chin[8] = 0x6c616863u;  // "chal"
+    fs.chin[9] = 0x676e656cu;  // "leng"
+    fs.chin[10] = 0x00000065u; // "e"
+  }
+  if (tid >= 11 && tid < 16) fs.chin[tid] = 0;
+  SC_TR(tr + 3);
+  __syncthreads();
+  // state' = B3(state || len || coefficients)
+  if (w0) b3_hash_quad(fs.msg, 40 + 32 * len, fs.chin, 8);
+  __syncthreads();
+  SC_TR(tr + 4);
+  // challenge bytes = B3-XOF(state' || "challenge")[0..48)
+  if (w0) b3_hash_quad(fs.chin, 41, fs.xof, 16);
+  __syncthreads();
+  SC_TR(tr + 5);
+  if (w0) {
+    // r = LE(48 B) mod r: lo * R^2 + hi * R^3 (Montgomery), lanes 0 and 1
+    Fr x, c;
+#pragma unroll
+    for (int i = 0; i < 8; i++) {
+      x.v[i] = (tid & 1) ? (i < 4 ? fs.xof[8 + i] : 0u) : fs.xof[i];
+      c.v[i] = (tid & 1) ? FrP::R3[i] : FrP::R2[i];
+    }
+    const Fr p = x * c;
+    const Fr rr = p + shfl_xor_fr(p, 1);
+    if (tid == 0) {
+      if (writer) {
+        ro.chal[j] = rr;
+        ro.lens[j] = len;
+      }
+      fs.r = rr;
+    }
+  }
+  if (pend_out) {
+    if (tid < 20) pend_out[tid] = tid < 8 ? fs.chin[tid] : fs.xof[tid - 8];
+  } else {
+    if (tid < 32) fs.ab[tid] = tid < 8 ? fs.chin[tid] : (tid < 20 ? fs.xof[tid - 8] : 0u);
+  }
+  __syncthreads();
+  SC_TR(tr + 6);
+  if (!pend_out && w0) b3_hash_quad(fs.ab, 80, state_out, 8);
+}
+
+// round kernel: fused fold(r_{j-1}) + evaluate at t = 0..np-1, per-block
+// partial sums; the last block to publish (ticket election) sums the partials
+// and, with loc == nullptr, runs the round's transcript step itself; with
+// loc != nullptr (sharded) it writes this rank's local sums for the allgather.
+template <int K, int NP>
+__global__ void __launch_bounds__(SC_BLOCK)
+    k_sc_round(TablePtrs tp, const SopDev* __restrict__ spg, SopHdr h, size_t npairs, int fold,
+               RoundOut ro, uint32_t j, int pending, Fr* __restrict__ partial, Fr* __restrict__ loc) {
+  __shared__ SopLds<NP> sp;
+  __shared__ RoundLds<K, NP, SC_BLOCK> L;
+  __shared__ Fr red[(SC_BLOCK / 64) * NP];
+  __shared__ Fr res[NP];
+  __shared__ FinSmem fs;
+  __shared__ uint32_t last;
+  const uint32_t tid = threadIdx.x;
+  const uint32_t tr = 1024 + 16 * j;
+  if (blockIdx.x == 0) SC_TR(tr + 0);
+  sop_load<NP>(sp, spg, h, loc == nullptr);
+#pragma unroll
+  for (int i = 0; i < 8; i++) {
+    if (tid == (uint32_t)i) {
+      L.src[i] = tp.src[i];
+      L.dst[i] = tp.dst[i];
+    }
+  }
+  const Fr r = fold ? ro.chal[j - 1] : Fr::zero();
+  if (pending && blockIdx.x == 0 && tid >= 64 && tid < 128) {
+    // deferred absorb of round j-1's challenge bytes (wave 1 of block 0)
+    if (tid - 64 < 32) fs.ab[tid - 64] = tid - 64 < 20 ? ro.st->pend[tid - 64] : 0u;
+    __builtin_amdgcn_s_waitcnt(0);
+    __builtin_amdgcn_wave_barrier();
+    b3_hash_quad(fs.ab, 80, ro.st->state, 8);
+    __builtin_amdgcn_fence(__ATOMIC_RELEASE, "agent");
+  }
+  __syncthreads();
+  constexpr uint32_t PB = SC_BLOCK / NP;
+  Fr acc = Fr::zero();
+  round_sweep<K, NP, SC_BLOCK>(L, sp, h, npairs, fold != 0, r, (size_t)blockIdx.x * PB,
+                               (size_t)gridDim.x * PB, acc);
+  if (blockIdx.x == 0) SC_TR(tr + 1);
+  block_reduce_pts<NP>(acc, h.np, red, res);
+  if (tid < h.np) partial[(size_t)blockIdx.x * NP + tid] = res[tid];
+  __syncthreads();
+  if (tid == 0) {
+    __builtin_amdgcn_fence(__ATOMIC_RELEASE, "agent");
+    const uint32_t old =
+        __hip_atomic_fetch_add(&ro.st->ticket, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+    last = old + 1 == gridDim.x;
+    if (last) __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "agent");
+  }
+  __syncthreads();
+  if (!last) return;
+  SC_TR(tr + 2);
+  acc = Fr::zero();
+  {
+    const uint32_t t = tid % NP;
+    if (t < h.np)
+      for (uint32_t b = tid / NP; b < gridDim.x; b += SC_BLOCK / NP)
+        acc = acc + partial[(size_t)b * NP + t];
+  }
+  block_reduce_pts<NP>(acc, h.np, red, res);
+  if (tid == 0) ro.st->ticket = 0;
+  if (loc) {
+    if (tid < NP) loc[tid] = tid < h.np ? res[tid] : Fr::zero();
+    return;
+  }
+  finish_core<NP>(sp, h.np, res, ro, j, fs, ro.st->state, ro.st->pend, nullptr, tr);
+  SC_TR(tr + 7);
+}
+
+// sharded: the transcript step over the allgathered [rank][NP] local sums
+template <int NP>
+__global__ void __launch_bounds__(SC_BLOCK)
+    k_sc_finish(const SopDev* __restrict__ spg, SopHdr h, const Fr* __restrict__ rows,
+                uint32_t nrows, RoundOut ro, uint32_t j) {
+  __shared__ SopLds<NP> sp;
+  __shared__ Fr red[(SC_BLOCK / 64) * NP];
+  __shared__ Fr res[NP];
+  __shared__ FinSmem fs;
+  __shared__ uint32_t st[8];
+  const uint32_t tid = threadIdx.x;
+  sop_load<NP>(sp, spg, h, true);
+  if (tid < 8) st[tid] = ro.st->state[tid];
+  Fr acc = Fr::zero();
+  {
+    const uint32_t t = tid % NP;
+    if (t < h.np)
+      for (uint32_t b = tid / NP; b < nrows; b += SC_BLOCK / NP)
+        acc = acc + rows[(size_t)b * NP + t];
+  }
+  __syncthreads();
+  block_reduce_pts<NP>(acc, h.np, red, res);
+  finish_core<NP>(sp, h.np, res, ro, j, fs, st, nullptr, ro.st->state);
+}
+
+// Grid barrier among the first n blocks (monotonic per-round counter).  Every
+// wave drains its stores, thread 0 publishes with an agent-scope release and
+// acquires after the count completes (MI355X_MICROARCH.md, inter-workgroup
+// visibility).  The spin is bounded: on timeout the error flag is raised and
+// the kernel runs on to its end (the host reports QG_ERR_DEVICE).
+QG_DEV void grid_barrier(uint32_t* ctr, uint32_t n, uint32_t* err) {
+  __builtin_amdgcn_s_waitcnt(0);
+  __syncthreads();
+  if (threadIdx.x == 0) {
+    __builtin_amdgcn_fence(__ATOMIC_RELEASE, "agent");
+    __hip_atomic_fetch_add(ctr, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+    uint32_t spins = 0;
+    while (__hip_atomic_load(ctr, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) < n) {
+      __builtin_amdgcn_s_sleep(1);
+      if (++spins > (1u << 26)) {
+        __hip_atomic_store(err, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+        break;
       }
     }
+    __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "agent");
   }
   __syncthreads();
 }
 
-// round kernel: fused fold(r_{j-1}) + evaluate, per-block partial sums
-template <int K, int NPMAX>
-__global__ void __launch_bounds__(SC_BLOCK)
-    k_sc_round(TablePtrs tp, const SopDev* __restrict__ sp, size_t npairs, int fold,
-               const Fr* __restrict__ chal, Fr* __restrict__ partial) {
-  __shared__ Fr lds[(SC_BLOCK / 64) * NPMAX];
-  const uint32_t nslots = sp->nslots, np = sp->np;
-  Fr r = fold ? *chal : Fr::zero();
-  Fr sums[NPMAX];
-#pragma unroll
-  for (int t = 0; t < NPMAX; t++) sums[t] = Fr::zero();
-  for (size_t p = (size_t)blockIdx.x * blockDim.x + threadIdx.x; p < npairs;
-       p += (size_t)gridDim.x * blockDim.x) {
-    Fr lo[K], df[K];
-    load_pair<K>(tp, nslots, p, fold != 0, r, lo, df);
-    eval_pair<K, NPMAX>(sp, lo, df, sums);
-  }
-  block_sum<NPMAX>(sums, np, lds);
-  if (threadIdx.x == 0) {
-#pragma unroll
-    for (int t = 0; t < NPMAX; t++)
-      if ((uint32_t)t < np) partial[(size_t)blockIdx.x * NPMAX + t] = sums[t];
-  }
-}
-
-// Round bookkeeping shared by the finish and tail kernels (whole block):
-// interpolate evals -> coefficients (lane t computes coefficient t), trim,
-// serialize into an LDS word buffer, then one lane runs the word-oriented
-// BLAKE3 transcript (absorb message, draw r_j).
-struct RoundOut {
-  uint32_t* state;       // 8-word (32 B) transcript state (device)
-  Fr* chal;              // nvars challenges
-  Fr* coeffs;            // nvars x width
-  uint32_t* lens;        // nvars
-  uint32_t width;        // row width (>= np)
-};
-
-struct FinishSmem {
-  Fr ev[16];
-  uint32_t msg[8 + 2 + 16 * 8];  // state || u64 len || coefficients (canonical LE)
-  uint32_t chin[12];             // new state || "challenge"
-  uint32_t ab[20];               // new state || 48 challenge bytes
-  uint32_t len;
-};
-
-// LDS word source for b3_chunk_words (dynamic indices stay in LDS, not scratch)
-struct LdsSrc {
-  const uint32_t* p;
-  QG_DEV uint32_t operator()(uint32_t i) const { return p[i]; }
-};
-
-QG_DEV void finish_round_block(const SopDev* __restrict__ sp, FinishSmem& sm, const RoundOut& ro,
-                               uint32_t j) {
-  const uint32_t np = sp->np, t = threadIdx.x;
-  if (t == 0) sm.len = 0;
-  if (t < 8) sm.msg[t] = ro.state[t];
-  __syncthreads();
-  if (t < ro.width) {
-    Fr co = Fr::zero();
-    if (t < np) {
-      for (uint32_t u = 0; u < np; u++) co = co + sp->vinv[t * 16 + u] * sm.ev[u];
-      Fr c = from_mont(co);
-#pragma unroll
-      for (int i = 0; i < 8; i++) sm.msg[10 + 8 * t + i] = c.v[i];
-      if (!co.is_zero()) atomicMax(&sm.len, t + 1);
-    }
-    ro.coeffs[(size_t)j * ro.width + t] = co;  // trailing entries are zero by construction
-  }
-  __syncthreads();
-  if (t == 0) {
-    const uint32_t len = sm.len;
-    sm.msg[8] = len;
-    sm.msg[9] = 0;
-    // state' = B3(state || msg)
-    b3_chunk_words(LdsSrc{sm.msg}, 40 + 32 * len, sm.chin, 8);
-    // challenge = B3-XOF(state' || "challenge")[0..48]
-    sm.chin[8] = 0x6c616863u;  // "chal"
-    sm.chin[9] = 0x676e656cu;  // "leng"
-    sm.chin[10] = 0x00000065u; // "e"
-#pragma unroll
-    for (int i = 0; i < 8; i++) sm.ab[i] = sm.chin[i];
-    b3_chunk_words(LdsSrc{sm.chin}, 41, sm.ab + 8, 12);
-    // state'' = B3(state' || challenge)
-    b3_chunk_words(LdsSrc{sm.ab}, 80, sm.chin, 8);
-#pragma unroll
-    for (int i = 0; i < 8; i++) ro.state[i] = sm.chin[i];
-    Fr lo, hi;
-#pragma unroll
-    for (int i = 0; i < 8; i++) lo.v[i] = sm.ab[8 + i];
-#pragma unroll
-    for (int i = 0; i < 4; i++) hi.v[i] = sm.ab[16 + i];
-#pragma unroll
-    for (int i = 4; i < 8; i++) hi.v[i] = 0;
-    ro.chal[j] = lo * Fr::from_raw(FrP::R2) + hi * Fr::from_raw(FrP::R3);
-    ro.lens[j] = len;
-  }
-  __syncthreads();
-}
-
-template <int NPMAX>
-QG_DEV void stash_evals(const Fr (&s)[NPMAX], uint32_t np, FinishSmem& sm) {
-  if (threadIdx.x == 0) {
-#pragma unroll
-    for (int t = 0; t < NPMAX; t++)
-      if ((uint32_t)t < np) sm.ev[t] = s[t];
-  }
-}
-
-template <int NPMAX>
-__global__ void __launch_bounds__(SC_BLOCK)
-    k_sc_finish(const SopDev* __restrict__ sp, const Fr* __restrict__ partial, uint32_t nblocks,
-                RoundOut ro, uint32_t j) {
-  __shared__ Fr lds[(SC_BLOCK / 64) * NPMAX];
-  __shared__ FinishSmem sm;
-  const uint32_t np = sp->np;
-  Fr s[NPMAX];
-#pragma unroll
-  for (int t = 0; t < NPMAX; t++) s[t] = Fr::zero();
-  for (uint32_t b = threadIdx.x; b < nblocks; b += blockDim.x) {
-#pragma unroll
-    for (int t = 0; t < NPMAX; t++)
-      if ((uint32_t)t < np) s[t] = s[t] + partial[(size_t)b * NPMAX + t];
-  }
-  block_sum<NPMAX>(s, np, lds);
-  stash_evals<NPMAX>(s, np, sm);
-  finish_round_block(sp, sm, ro, j);
-}
-
-// Remaining rounds j0..nvars-1 in one workgroup, then the final fold + claim.
+// Rounds j0..nvars-1 in one persistent launch.  Round j keeps the first
+// nb_j = ceil(pairs / PB) blocks (the others retire: work only shrinks); each
+// block sweeps its pairs, publishes its per-point sums, meets the others at a
+// grid barrier, then every block sums all partials and runs the (identical)
+// transcript step itself, so no second barrier or broadcast is needed.  Block
+// 0 writes the proof outputs.  Once nb_j == 1, block 0 continues alone.  The
+// transcript state, the pending absorb and r stay in LDS between rounds, and
+// the code stays hot in the instruction cache (a fresh launch per small round
+// would refetch ~45 KB of code cold).  Final fold + claim by block 0.
 // bufs: ping-pong scratch per slot (a: size >= 2^(n-j0-1), b: >= 2^(n-j0-2)).
-template <int K, int NPMAX>
-__global__ void __launch_bounds__(SC_BLOCK)
-    k_sc_tail(TablePtrs tp0, TablePtrs bufA, TablePtrs bufB, const SopDev* __restrict__ sp,
-              uint32_t nvars, uint32_t j0, int fold0, RoundOut ro, Fr* __restrict__ final_vals,
-              Fr* __restrict__ evaluation) {
-  __shared__ Fr lds[(SC_BLOCK / 64) * NPMAX];
-  __shared__ FinishSmem sm;
-  const uint32_t nslots = sp->nslots, np = sp->np;
+template <int K, int NP>
+__global__ void __launch_bounds__(TAIL_BLOCK)
+    k_sc_persist(TablePtrs tp0, TablePtrs bufA, TablePtrs bufB, const SopDev* __restrict__ spg,
+                 SopHdr h, uint32_t nvars, uint32_t j0, int fold0, int pending0, RoundOut ro,
+                 Fr* __restrict__ partial, uint32_t* __restrict__ bar, Fr* __restrict__ final_vals,
+                 Fr* __restrict__ evaluation) {
+  constexpr uint32_t PB = TAIL_BLOCK / NP;
+  __shared__ SopLds<NP> sp;
+  __shared__ RoundLds<K, NP, TAIL_BLOCK> L;
+  __shared__ Fr red[(TAIL_BLOCK / 64) * NP];
+  __shared__ Fr res[NP];
+  __shared__ FinSmem fs;
+  __shared__ uint32_t st[8];
+  __shared__ uint32_t pend[32];
+  const uint32_t tid = threadIdx.x, blk = blockIdx.x;
+  const uint32_t nslots = h.nslots, np = h.np;
+  const bool writer = blk == 0;
+  sop_load<NP>(sp, spg, h, true);
+  if (tid < 8) st[tid] = ro.st->state[tid];
+  if (tid < 32) pend[tid] = (pending0 && tid < 20) ? ro.st->pend[tid] : 0u;
+  Fr r = fold0 ? ro.chal[j0 - 1] : Fr::zero();
   TablePtrs cur = tp0;
-  int fold = fold0;
+  int fold = fold0, pending = pending0;
   for (uint32_t j = j0; j < nvars; j++) {
     const size_t npairs = (size_t)1 << (nvars - 1 - j);
-    Fr r = fold ? ro.chal[j - 1] : Fr::zero();
-    Fr sums[NPMAX];
+    const uint32_t nb = (uint32_t)std::min<size_t>(gridDim.x, (npairs + PB - 1) / PB);
+    if (blk >= nb) return;  // retired: every later round has fewer pairs
 #pragma unroll
-    for (int t = 0; t < NPMAX; t++) sums[t] = Fr::zero();
-    for (size_t p = threadIdx.x; p < npairs; p += blockDim.x) {
-      Fr lo[K], df[K];
-      load_pair<K>(cur, nslots, p, fold != 0, r, lo, df);
-      eval_pair<K, NPMAX>(sp, lo, df, sums);
+    for (int i = 0; i < 8; i++) {
+      if (tid == (uint32_t)i) {
+        L.src[i] = cur.src[i];
+        L.dst[i] = cur.dst[i];
+      }
     }
-    block_sum<NPMAX>(sums, np, lds);
-    stash_evals<NPMAX>(sums, np, sm);
-    finish_round_block(sp, sm, ro, j);
+    __syncthreads();
+    if (writer) SC_TR(16 * j + 0);
+    if (pending && tid >= 64 && tid < 128) b3_hash_quad(pend, 80, st, 8);  // wave 1
+    Fr acc = Fr::zero();
+    round_sweep<K, NP, TAIL_BLOCK>(L, sp, h, npairs, fold != 0, r, (size_t)blk * PB,
+                                   (size_t)nb * PB, acc);
+    if (writer) SC_TR(16 * j + 1);
+    block_reduce_pts<NP>(acc, np, red, res);
+    if (nb > 1) {
+      Fr* part = partial + (size_t)(j & 1) * gridDim.x * NP;
+      if (tid < np) part[(size_t)blk * NP + tid] = res[tid];
+      grid_barrier(bar + j, nb, &ro.st->pad[0]);
+      acc = Fr::zero();
+      const uint32_t t = tid % NP;
+      if (t < np)
+        for (uint32_t b = tid / NP; b < nb; b += PB) acc = acc + part[(size_t)b * NP + t];
+      block_reduce_pts<NP>(acc, np, red, res);
+    }
+    if (writer) SC_TR(16 * j + 2);
+    finish_core<NP>(sp, np, res, ro, j, fs, st, pend, nullptr, writer ? 16 * j : 4096, writer);
+    __syncthreads();
+    r = fs.r;
+    pending = 1;
     // the folded tables written this round become the next source
     TablePtrs nxt;
     const TablePtrs& w = ((j - j0) & 1) ? bufB : bufA;
@@ -492,9 +714,8 @@ __global__ void __launch_bounds__(SC_BLOCK)
     cur = nxt;
     fold = 1;
   }
-  // final fold with r_{n-1}: cur.src has 2 entries per slot
-  if (threadIdx.x == 0) {
-    Fr r = ro.chal[nvars - 1];
+  // final fold with r_{n-1}: cur.src has 2 entries per slot (block 0 only here)
+  if (tid == 0) {
     Fr val[K];
 #pragma unroll
     for (int i = 0; i < K; i++) {
@@ -506,8 +727,10 @@ __global__ void __launch_bounds__(SC_BLOCK)
         val[i] = Fr::zero();
       }
     }
-    *evaluation = sop_eval<K>(sp, val);
+    *evaluation = sop_eval<K, NP>(sp, val);
   }
+  // absorb the last challenge bytes
+  if (pending && tid >= 64 && tid < 128) b3_hash_quad(pend, 80, ro.st->state, 8);
 }
 
 // eq(bin(i), z) for i < 2^nbits over z[off .. off+nbits)   (eq_eval.rs:6-31)
@@ -528,28 +751,6 @@ __global__ void k_eq_combine(const Fr* __restrict__ low, const Fr* __restrict__ 
   size_t i = (size_t)blockIdx.x * blockDim.x + threadIdx.x;
   if (i >= n) return;
   out[i] = low[i & (((size_t)1 << lbits) - 1)] * high[i >> lbits];
-}
-
-// multi-GPU: sum this rank's block partials -> loc[0..np)
-template <int NPMAX>
-__global__ void __launch_bounds__(SC_BLOCK)
-    k_sc_local_sum(const SopDev* __restrict__ sp, const Fr* __restrict__ partial, uint32_t nblocks,
-                   Fr* __restrict__ loc) {
-  __shared__ Fr lds[(SC_BLOCK / 64) * NPMAX];
-  const uint32_t np = sp->np;
-  Fr s[NPMAX];
-#pragma unroll
-  for (int t = 0; t < NPMAX; t++) s[t] = Fr::zero();
-  for (uint32_t b = threadIdx.x; b < nblocks; b += blockDim.x) {
-#pragma unroll
-    for (int t = 0; t < NPMAX; t++)
-      if ((uint32_t)t < np) s[t] = s[t] + partial[(size_t)b * NPMAX + t];
-  }
-  block_sum<NPMAX>(s, np, lds);
-  if (threadIdx.x == 0) {
-#pragma unroll
-    for (int t = 0; t < NPMAX; t++) loc[t] = (uint32_t)t < np ? s[t] : Fr::zero();
-  }
 }
 
 // multi-GPU: fold each slot's last local pair with r (size 2 -> 1)
@@ -604,57 +805,107 @@ void eq_table_device(qg_ctx* ctx, const Fr* d_z, uint32_t nvars, Fr* d_out) {
   QG_LAUNCH_CHECK();
 }
 
-struct SumcheckResult {
-  std::vector<uint64_t> coeffs;  // nvars * width * 4
-  std::vector<uint32_t> lens;
-  std::vector<Fr> point;
-  Fr evaluation;
+// Compiled programs are cached by their exact bytes (the device image carries
+// the inverse Vandermonde, whose host construction costs field inversions).
+struct ScProgram {
+  uint64_t id = 0;  // unique per compiled program (device-copy memo key)
+  SopDev img;
+  SopHdr hdr;
+  uint32_t nused = 0;
+  std::vector<uint32_t> used;
+  uint32_t width = 0;  // syntactic degree + 1 (proof row width)
 };
 
-template <int K, int NPMAX>
+static std::mutex g_prog_mu;
+static std::map<std::string, std::shared_ptr<const ScProgram>> g_prog_cache;
+
+static std::shared_ptr<const ScProgram> get_program(const qg_expr_op* prog, size_t prog_len,
+                                                    const uint64_t* consts, size_t nconsts,
+                                                    uint32_t ntables) {
+  std::string key((const char*)&ntables, 4);
+  key.append((const char*)prog, prog_len * sizeof(qg_expr_op));
+  key.push_back('|');
+  if (nconsts) key.append((const char*)consts, nconsts * 32);
+  {
+    std::lock_guard<std::mutex> lk(g_prog_mu);
+    auto it = g_prog_cache.find(key);
+    if (it != g_prog_cache.end()) return it->second;
+  }
+  static std::atomic<uint64_t> next_id{1};
+  auto p = std::make_shared<ScProgram>();
+  p->id = next_id++;
+  p->width = expr_degree(prog, prog_len) + 1;
+  SopProgram sp = compile_program(prog, prog_len, consts, nconsts, ntables);
+  QG_CHECK(sp.mono_len.size() <= (size_t)SOP_MAXM && sp.fac.size() <= (size_t)SOP_MAXF,
+           QG_ERR_UNSUPPORTED, "expression too large");
+  QG_CHECK(sp.used.size() <= 8, QG_ERR_UNSUPPORTED, "expression uses more than 8 tables");
+  QG_CHECK(sp.degree <= 15, QG_ERR_UNSUPPORTED, "expression degree above 15");
+  const uint32_t np = sp.degree + 1;
+  QG_CHECK(np <= p->width, QG_ERR_ASSERT, "degree bookkeeping");
+  SopDev& d = p->img;
+  memset(&d, 0, sizeof(SopDev));
+  d.nmono = (uint32_t)sp.mono_len.size();
+  d.nslots = (uint32_t)sp.used.size();
+  d.np = np;
+  d.nfac = (uint32_t)sp.fac.size();
+  for (size_t m = 0; m < sp.mono_len.size(); m++) {
+    d.mono_len[m] = (uint8_t)sp.mono_len[m];
+    d.is_one[m] = sp.is_one[m];
+    d.coeff[m] = sp.coeff[m];
+  }
+  for (size_t f = 0; f < sp.fac.size(); f++) d.fac[f] = (uint8_t)sp.fac[f];
+  build_vinv(np, d.vinv_m, d.vinv_c);
+  p->hdr = {d.nmono, d.nslots, np, 0};
+  p->used = sp.used;
+  p->nused = (uint32_t)sp.used.size();
+  std::lock_guard<std::mutex> lk(g_prog_mu);
+  if (g_prog_cache.size() >= 256) g_prog_cache.clear();
+  g_prog_cache[key] = p;
+  return p;
+}
+
+template <int K, int NP>
 static void run_rounds(qg_ctx* ctx, uint32_t nvars, const std::vector<const Fr*>& src,
-                       const SopDev* d_sp, uint32_t nslots, RoundOut ro, Fr* d_final,
+                       const SopDev* d_sp, SopHdr h, RoundOut ro, uint32_t* bar, Fr* d_final,
                        Fr* d_eval) {
+  const uint32_t nslots = h.nslots;
   const size_t N = (size_t)1 << nvars;
   // ping-pong scratch: X holds N/2 per slot, Y holds N/4 per slot
   Fr* X = ctx->scratch_as<Fr>("sc_x", std::max<size_t>(1, (N / 2) * nslots));
   Fr* Y = ctx->scratch_as<Fr>("sc_y", std::max<size_t>(1, (N / 4) * nslots));
-  Fr* partial = ctx->scratch_as<Fr>("sc_partial", (size_t)SC_MAX_BLOCKS * NPMAX);
+  Fr* partial = ctx->scratch_as<Fr>("sc_partial", (size_t)SC_MAX_BLOCKS * NP);
   TablePtrs cur{};
-  for (uint32_t i = 0; i < 8; i++) cur.src[i] = i < nslots ? src[i] : nullptr;
+  for (uint32_t i = 0; i < 8; i++) cur.src[i] = i < src.size() ? src[i] : nullptr;
   auto bufs = [&](Fr* base, size_t per) {
     TablePtrs t{};
     for (uint32_t i = 0; i < 8; i++) t.dst[i] = i < nslots ? base + per * i : nullptr;
     return t;
   };
   TablePtrs tX = bufs(X, N / 2), tY = bufs(Y, std::max<size_t>(1, N / 4));
-  int fold = 0;
+  int fold = 0, pending = 0;
   uint32_t j = 0;
   int parity = 0;  // next destination: 0 -> X, 1 -> Y
   {
     QgTimed tm(ctx, "sumcheck_round");
     for (; j < nvars; j++) {
-      const size_t table = N >> j;  // logical size before this round's fold... after fold
-      // size of the tables this round evaluates: N >> j
-      if (table <= ((size_t)1 << TAIL_LOG)) break;
+      const size_t table = N >> j;  // entries per table evaluated in round j
+      if (table <= ((size_t)1 << PERS_LOG)) break;
       const size_t npairs = table / 2;
-      unsigned blocks = (unsigned)std::min<size_t>(SC_MAX_BLOCKS, div_up(npairs, SC_BLOCK));
+      const unsigned blocks = (unsigned)std::min<size_t>(SC_MAX_BLOCKS, div_up(npairs, SC_BLOCK));
       TablePtrs tp = cur;
       if (fold) {
         const TablePtrs& d = parity ? tY : tX;
         for (int i = 0; i < 8; i++) tp.dst[i] = d.dst[i];
       }
-      hipLaunchKernelGGL((k_sc_round<K, NPMAX>), dim3(blocks), dim3(SC_BLOCK), 0, ctx->stream, tp,
-                         d_sp, npairs, fold, fold ? ro.chal + (j - 1) : ro.chal, partial);
-      QG_LAUNCH_CHECK();
-      hipLaunchKernelGGL((k_sc_finish<NPMAX>), dim3(1), dim3(SC_BLOCK), 0, ctx->stream, d_sp,
-                         partial, blocks, ro, j);
+      hipLaunchKernelGGL((k_sc_round<K, NP>), dim3(blocks), dim3(SC_BLOCK), 0, ctx->stream, tp,
+                         d_sp, h, npairs, fold, ro, j, pending, partial, (Fr*)nullptr);
       QG_LAUNCH_CHECK();
       if (fold) {
         for (int i = 0; i < 8; i++) cur.src[i] = tp.dst[i];
         parity ^= 1;
       }
       fold = 1;
+      pending = 1;
     }
   }
   {
@@ -675,8 +926,16 @@ static void run_rounds(qg_ctx* ctx, uint32_t nvars, const std::vector<const Fr*>
       bufA = b;
       bufB = a;
     }
-    hipLaunchKernelGGL((k_sc_tail<K, NPMAX>), dim3(1), dim3(SC_BLOCK), 0, ctx->stream, t0, bufA,
-                       bufB, d_sp, nvars, j, fold, ro, d_final, d_eval);
+    // persistent launch: one block per CU at most (co-residency for the grid
+    // barrier), fewer when the first persistent round has fewer pair groups
+    constexpr size_t PB = TAIL_BLOCK / NP;
+    const size_t pairs0 = (N >> j) / 2;
+    const unsigned grid = (unsigned)std::max<size_t>(
+        1, std::min<size_t>((size_t)ctx->num_cus(), (pairs0 + PB - 1) / PB));
+    Fr* ppart = ctx->scratch_as<Fr>("sc_ppartial", (size_t)2 * grid * NP);
+    hipLaunchKernelGGL((k_sc_persist<K, NP>), dim3(grid), dim3(TAIL_BLOCK), 0, ctx->stream, t0,
+                       bufA, bufB, d_sp, h, nvars, j, fold, pending, ro, ppart, bar, d_final,
+                       d_eval);
     QG_LAUNCH_CHECK();
   }
 }
@@ -686,10 +945,11 @@ static void run_rounds(qg_ctx* ctx, uint32_t nvars, const std::vector<const Fr*>
 // pair local entries only: one allgather of the (d+1) round sums per round, then
 // every rank runs the identical device transcript.  The last log2(world) rounds
 // run redundantly on the allgathered single values.
-template <int K, int NPMAX>
+template <int K, int NP>
 static void run_rounds_dist(qg_ctx* ctx, uint32_t nvars, const std::vector<const Fr*>& src,
-                            const SopDev* d_sp, uint32_t nslots, RoundOut ro, Fr* d_final,
+                            const SopDev* d_sp, SopHdr h, RoundOut ro, uint32_t* bar, Fr* d_final,
                             Fr* d_eval) {
+  const uint32_t nslots = h.nslots;
   const uint32_t world = (uint32_t)ctx->world;
   uint32_t lw = 0;
   while ((1u << lw) < world) lw++;
@@ -699,16 +959,16 @@ static void run_rounds_dist(qg_ctx* ctx, uint32_t nvars, const std::vector<const
   const size_t NL = (size_t)1 << m;
   Fr* X = ctx->scratch_as<Fr>("sc_x", std::max<size_t>(1, (NL / 2) * std::max(nslots, 1u)));
   Fr* Y = ctx->scratch_as<Fr>("sc_y", std::max<size_t>(1, (NL / 4) * std::max(nslots, 1u)));
-  Fr* partial = ctx->scratch_as<Fr>("sc_partial", (size_t)SC_MAX_BLOCKS * NPMAX);
-  Fr* loc = ctx->scratch_as<Fr>("sc_loc", NPMAX);
-  Fr* all = ctx->scratch_as<Fr>("sc_all", (size_t)world * NPMAX);
+  Fr* partial = ctx->scratch_as<Fr>("sc_partial", (size_t)SC_MAX_BLOCKS * NP);
+  Fr* loc = ctx->scratch_as<Fr>("sc_loc", NP);
+  Fr* all = ctx->scratch_as<Fr>("sc_all", (size_t)world * NP);
   Fr* last = ctx->scratch_as<Fr>("sc_last", 8);
   Fr* graw = ctx->scratch_as<Fr>("sc_graw", (size_t)world * 8);
   Fr* gt = ctx->scratch_as<Fr>("sc_gt", (size_t)world * 8);
   Fr* gA = ctx->scratch_as<Fr>("sc_gA", (size_t)world * 8);
   Fr* gB = ctx->scratch_as<Fr>("sc_gB", (size_t)world * 8);
   TablePtrs cur{};
-  for (uint32_t i = 0; i < 8; i++) cur.src[i] = i < nslots ? src[i] : nullptr;
+  for (uint32_t i = 0; i < 8; i++) cur.src[i] = i < src.size() ? src[i] : nullptr;
   auto bufs = [&](Fr* base, size_t per) {
     TablePtrs t{};
     for (uint32_t i = 0; i < 8; i++) t.dst[i] = i < nslots ? base + per * i : nullptr;
@@ -726,14 +986,11 @@ static void run_rounds_dist(qg_ctx* ctx, uint32_t nvars, const std::vector<const
         const TablePtrs& d = parity ? tY : tX;
         for (int i = 0; i < 8; i++) tp.dst[i] = d.dst[i];
       }
-      hipLaunchKernelGGL((k_sc_round<K, NPMAX>), dim3(blocks), dim3(SC_BLOCK), 0, ctx->stream, tp,
-                         d_sp, npairs, fold, fold ? ro.chal + (j - 1) : ro.chal, partial);
+      hipLaunchKernelGGL((k_sc_round<K, NP>), dim3(blocks), dim3(SC_BLOCK), 0, ctx->stream, tp,
+                         d_sp, h, npairs, fold, ro, j, 0, partial, loc);
       QG_LAUNCH_CHECK();
-      hipLaunchKernelGGL((k_sc_local_sum<NPMAX>), dim3(1), dim3(SC_BLOCK), 0, ctx->stream, d_sp,
-                         partial, blocks, loc);
-      QG_LAUNCH_CHECK();
-      comm_allgather_bytes(ctx, loc, all, sizeof(Fr) * NPMAX);
-      hipLaunchKernelGGL((k_sc_finish<NPMAX>), dim3(1), dim3(SC_BLOCK), 0, ctx->stream, d_sp, all,
+      comm_allgather_bytes(ctx, loc, all, sizeof(Fr) * NP);
+      hipLaunchKernelGGL((k_sc_finish<NP>), dim3(1), dim3(SC_BLOCK), 0, ctx->stream, d_sp, h, all,
                          world, ro, j);
       QG_LAUNCH_CHECK();
       if (fold) {
@@ -763,18 +1020,18 @@ static void run_rounds_dist(qg_ctx* ctx, uint32_t nvars, const std::vector<const
       bufA.dst[i] = i < nslots ? gA + (size_t)world * i : nullptr;
       bufB.dst[i] = i < nslots ? gB + (size_t)world * i : nullptr;
     }
-    hipLaunchKernelGGL((k_sc_tail<K, NPMAX>), dim3(1), dim3(SC_BLOCK), 0, ctx->stream, t0, bufA,
-                       bufB, d_sp, nvars, m, 0, ro, d_final, d_eval);
+    hipLaunchKernelGGL((k_sc_persist<K, NP>), dim3(1), dim3(TAIL_BLOCK), 0, ctx->stream, t0,
+                       bufA, bufB, d_sp, h, nvars, m, 0, 0, ro, partial, bar, d_final, d_eval);
     QG_LAUNCH_CHECK();
   }
 }
 
-template <int K, int NPMAX>
+template <int K, int NP>
 static void run_rounds_any(qg_ctx* ctx, uint32_t nvars, const std::vector<const Fr*>& src,
-                           const SopDev* d_sp, uint32_t nslots, RoundOut ro, Fr* d_final,
+                           const SopDev* d_sp, SopHdr h, RoundOut ro, uint32_t* bar, Fr* d_final,
                            Fr* d_eval) {
-  if (ctx->world > 1) run_rounds_dist<K, NPMAX>(ctx, nvars, src, d_sp, nslots, ro, d_final, d_eval);
-  else run_rounds<K, NPMAX>(ctx, nvars, src, d_sp, nslots, ro, d_final, d_eval);
+  if (ctx->world > 1) run_rounds_dist<K, NP>(ctx, nvars, src, d_sp, h, ro, bar, d_final, d_eval);
+  else run_rounds<K, NP>(ctx, nvars, src, d_sp, h, ro, bar, d_final, d_eval);
 }
 
 static void sumcheck_run(qg_ctx* ctx, uint32_t nvars, uint32_t ntables,
@@ -783,82 +1040,74 @@ static void sumcheck_run(qg_ctx* ctx, uint32_t nvars, uint32_t ntables,
                          const uint64_t claimed_sum[4], uint8_t state[32], uint64_t* round_coeffs,
                          uint32_t* round_lens, uint64_t* point, uint64_t evaluation[4]) {
   QG_CHECK(nvars >= 1 && nvars <= 40, QG_ERR_INVALID, "nvars out of range");
-  const uint32_t width = expr_degree(prog, prog_len) + 1;
-  SopProgram sp = compile_program(prog, prog_len, consts, nconsts, ntables);
-  QG_CHECK(sp.mono_len.size() <= 256 && sp.fac.size() <= 1024, QG_ERR_UNSUPPORTED,
-           "expression too large");
-  QG_CHECK(sp.used.size() <= 8, QG_ERR_UNSUPPORTED, "expression uses more than 8 tables");
-  QG_CHECK(sp.degree <= 15, QG_ERR_UNSUPPORTED, "expression degree above 15");
-  const uint32_t np = sp.degree + 1;
-  QG_CHECK(np <= width, QG_ERR_ASSERT, "degree bookkeeping");
+  auto P = get_program(prog, prog_len, consts, nconsts, ntables);
+  const uint32_t width = P->width;
 
   // transcript: append num_vars (usize) and claimed_sum (sumcheck.rs:35-36)
-  uint8_t st[32];
-  memcpy(st, state, 32);
-  uint8_t b8[8], b32[32];
-  u64_to_bytes(nvars, b8);
-  transcript_append(st, b8, 8);
-  fr_to_bytes(fr_import(claimed_sum), b32);
-  transcript_append(st, b32, 32);
-
-  SopDev* h_sp = new SopDev();
-  memset(h_sp, 0, sizeof(SopDev));
-  h_sp->nmono = (uint32_t)sp.mono_len.size();
-  h_sp->nslots = (uint32_t)sp.used.size();
-  h_sp->np = np;
-  for (size_t m = 0; m < sp.mono_len.size(); m++) {
-    h_sp->mono_len[m] = sp.mono_len[m];
-    h_sp->is_one[m] = sp.is_one[m];
-    h_sp->coeff[m] = sp.coeff[m];
+  ScState hs;
+  memset(&hs, 0, sizeof hs);
+  {
+    uint8_t st[32], b8[8], b32[32];
+    memcpy(st, state, 32);
+    u64_to_bytes(nvars, b8);
+    transcript_append(st, b8, 8);
+    fr_to_bytes(fr_import(claimed_sum), b32);
+    transcript_append(st, b32, 32);
+    memcpy(hs.state, st, 32);
   }
-  for (size_t f = 0; f < sp.fac.size(); f++) h_sp->fac[f] = (uint8_t)sp.fac[f];
-  build_vinv(np, h_sp->vinv);
 
+  // one device region: ScState | barrier counters | chal | coeffs | final (8 slots +
+  // evaluation) | lens.  ScState and the counters are (re)initialised per call.
+  const size_t o_bar = sizeof(ScState);
+  const size_t o_chal = o_bar + sizeof(uint32_t) * ((nvars + 7) & ~7u);
+  const size_t o_coeffs = o_chal + sizeof(Fr) * nvars;
+  const size_t o_final = o_coeffs + sizeof(Fr) * (size_t)nvars * width;
+  const size_t o_lens = o_final + sizeof(Fr) * 9;
+  const size_t io_bytes = o_lens + sizeof(uint32_t) * nvars;
+  uint8_t* io = ctx->scratch_as<uint8_t>("sc_io", io_bytes);
   SopDev* d_sp = ctx->scratch_as<SopDev>("sc_prog", 1);
-  uint32_t* d_state = ctx->scratch_as<uint32_t>("sc_state", 8);
-  Fr* d_chal = ctx->scratch_as<Fr>("sc_chal", nvars);
-  Fr* d_coeffs = ctx->scratch_as<Fr>("sc_coeffs", (size_t)nvars * width);
-  uint32_t* d_lens = ctx->scratch_as<uint32_t>("sc_lens", nvars);
-  Fr* d_final = ctx->scratch_as<Fr>("sc_final", 9);
-  QG_HIP(hipMemcpyAsync(d_sp, h_sp, sizeof(SopDev), hipMemcpyHostToDevice, ctx->stream));
-  QG_HIP(hipMemcpyAsync(d_state, st, 32, hipMemcpyHostToDevice, ctx->stream));
+  const std::string memo = std::to_string(P->id) + "@" + std::to_string((uintptr_t)d_sp);
+  if (ctx->memo["sc_prog"] != memo) {
+    QG_HIP(hipMemcpyAsync(d_sp, &P->img, sizeof(SopDev), hipMemcpyHostToDevice, ctx->stream));
+    ctx->memo["sc_prog"] = memo;
+  }
+  std::vector<uint8_t> hin(o_chal, 0);
+  memcpy(hin.data(), &hs, sizeof hs);
+  QG_HIP(hipMemcpyAsync(io, hin.data(), o_chal, hipMemcpyHostToDevice, ctx->stream));
+  uint32_t* bar = reinterpret_cast<uint32_t*>(io + o_bar);
 
   std::vector<const Fr*> src;
-  for (uint32_t u : sp.used) src.push_back(d_tables[u]);
-  RoundOut ro{d_state, d_chal, d_coeffs, d_lens, width};
+  for (uint32_t u : P->used) src.push_back(d_tables[u]);
+  RoundOut ro{reinterpret_cast<ScState*>(io), reinterpret_cast<Fr*>(io + o_chal),
+              reinterpret_cast<Fr*>(io + o_coeffs), reinterpret_cast<uint32_t*>(io + o_lens),
+              width};
+  Fr* d_final = reinterpret_cast<Fr*>(io + o_final);
   Fr* d_eval = d_final + 8;
-
-  if (sp.used.empty()) {
-    // constant expression: every table slot unused; evaluate with K = 1 and a dummy slot
-    src.push_back(d_tables.empty() ? d_chal : d_tables[0]);
-  }
-  const uint32_t nslots_launch = (uint32_t)sp.used.size();
+  const uint32_t np = P->hdr.np;
+  const size_t nsrc = src.size();
   // (with no used slots, nslots = 0 and loads are skipped)
   if (np <= 4) {
-    if (src.size() <= 4) run_rounds_any<4, 4>(ctx, nvars, src, d_sp, nslots_launch, ro, d_final, d_eval);
-    else run_rounds_any<8, 4>(ctx, nvars, src, d_sp, nslots_launch, ro, d_final, d_eval);
+    if (nsrc <= 4) run_rounds_any<4, 4>(ctx, nvars, src, d_sp, P->hdr, ro, bar, d_final, d_eval);
+    else run_rounds_any<8, 4>(ctx, nvars, src, d_sp, P->hdr, ro, bar, d_final, d_eval);
   } else if (np <= 8) {
-    if (src.size() <= 4) run_rounds_any<4, 8>(ctx, nvars, src, d_sp, nslots_launch, ro, d_final, d_eval);
-    else run_rounds_any<8, 8>(ctx, nvars, src, d_sp, nslots_launch, ro, d_final, d_eval);
+    if (nsrc <= 4) run_rounds_any<4, 8>(ctx, nvars, src, d_sp, P->hdr, ro, bar, d_final, d_eval);
+    else run_rounds_any<8, 8>(ctx, nvars, src, d_sp, P->hdr, ro, bar, d_final, d_eval);
   } else {
-    run_rounds_any<8, 16>(ctx, nvars, src, d_sp, nslots_launch, ro, d_final, d_eval);
+    run_rounds_any<8, 16>(ctx, nvars, src, d_sp, P->hdr, ro, bar, d_final, d_eval);
   }
 
-  std::vector<Fr> h_coeffs((size_t)nvars * width), h_chal(nvars);
-  Fr h_eval;
-  QG_HIP(hipMemcpyAsync(h_coeffs.data(), d_coeffs, sizeof(Fr) * h_coeffs.size(),
-                        hipMemcpyDeviceToHost, ctx->stream));
-  QG_HIP(hipMemcpyAsync(round_lens, d_lens, sizeof(uint32_t) * nvars, hipMemcpyDeviceToHost,
-                        ctx->stream));
-  QG_HIP(hipMemcpyAsync(h_chal.data(), d_chal, sizeof(Fr) * nvars, hipMemcpyDeviceToHost,
-                        ctx->stream));
-  QG_HIP(hipMemcpyAsync(&h_eval, d_eval, sizeof(Fr), hipMemcpyDeviceToHost, ctx->stream));
-  QG_HIP(hipMemcpyAsync(state, d_state, 32, hipMemcpyDeviceToHost, ctx->stream));
+  std::vector<uint8_t> h(io_bytes);
+  QG_HIP(hipMemcpyAsync(h.data(), io, io_bytes, hipMemcpyDeviceToHost, ctx->stream));
   ctx->sync();
-  delete h_sp;
-  for (size_t i = 0; i < h_coeffs.size(); i++) fr_export(h_coeffs[i], round_coeffs + 4 * i);
-  for (uint32_t i = 0; i < nvars; i++) fr_export(h_chal[i], point + 4 * i);
-  fr_export(h_eval, evaluation);
+  QG_CHECK(reinterpret_cast<const ScState*>(h.data())->pad[0] == 0, QG_ERR_DEVICE,
+           "sumcheck: grid barrier timed out (persistent blocks not co-resident)");
+  memcpy(state, h.data(), 32);
+  memcpy(round_lens, h.data() + o_lens, sizeof(uint32_t) * nvars);
+  const Fr* hc = reinterpret_cast<const Fr*>(h.data() + o_coeffs);
+  for (size_t i = 0; i < (size_t)nvars * width; i++) fr_export(hc[i], round_coeffs + 4 * i);
+  const Fr* hp = reinterpret_cast<const Fr*>(h.data() + o_chal);
+  for (uint32_t i = 0; i < nvars; i++) fr_export(hp[i], point + 4 * i);
+  fr_export(reinterpret_cast<const Fr*>(h.data() + o_final)[8], evaluation);
 }
 
 // entries per table held by this rank: 2^nvars, or 2^(nvars - log2(world)) when
@@ -932,6 +1181,13 @@ static void zerocheck_run(qg_ctx* ctx, uint32_t nvars, uint32_t ntables,
 }  // namespace qg
 
 extern "C" {
+
+#ifdef QG_SC_TRACE
+int qg_debug_sc_trace(uint64_t* out, size_t n) {
+  if (n > 2048) n = 2048;
+  return hipMemcpyFromSymbol(out, HIP_SYMBOL(g_sc_trace), n * 8) == hipSuccess ? QG_OK : QG_ERR_DEVICE;
+}
+#endif
 
 int qg_expr_degree(const qg_expr_op* prog, size_t prog_len, uint32_t* out_degree) {
   if (!prog || !out_degree) return QG_ERR_INVALID;

@@ -1,0 +1,44 @@
+"""Phase timeline of one 2^n sumcheck prove (micro benchmark, not a test):
+loads micro/libquill_gpu_trace.so (make -C quill-zkvm_amd trace) and prints
+per-round phase durations from the device timestamps (100 MHz clock)."""
+import ctypes as C
+import os
+import sys
+
+HERE = os.path.dirname(os.path.abspath(__file__))
+sys.path.insert(0, os.path.dirname(HERE))
+import quill_amd._lib as L  # noqa: E402
+
+L.LIB_PATH = os.path.join(HERE, "libquill_gpu_trace.so")
+import quill_amd as q  # noqa: E402
+from quill_amd.hyperplonk import VirtualPolyExpr as E, sumcheck_prove_device  # noqa: E402
+
+nv = int(sys.argv[1]) if len(sys.argv) > 1 else 20
+dev = q.Device(0)
+tabs = [q.DeviceVec(dev, 1 << nv).fill_random(11 + i) for i in range(3)]
+expr = E.Input(0) * E.Input(1) * E.Input(2)
+for _ in range(3):
+    sumcheck_prove_device(dev, nv, tabs, expr, 0, q.Transcript(b"t"))
+lib = L.lib()
+fn = lib.qg_debug_sc_trace
+fn.argtypes = [C.POINTER(C.c_uint64), C.c_size_t]
+buf = (C.c_uint64 * 2048)()
+fn(buf, 2048)
+tick = 0.01  # us per 100 MHz tick
+names_r = ["start", "evaluated(b0)", "last-block", "interp", "hash1", "hash2", "chal", "end"]
+print("round kernels (block 0 / last block), us relative to kernel start")
+for j in range(nv):
+    b = 1024 + 16 * j
+    if buf[b] == 0 or buf[b + 7] == 0:
+        continue
+    t0 = buf[b]
+    print(j, " ".join(f"{names_r[k]}={(buf[b + k] - t0) * tick:.2f}" for k in range(1, 8)
+                      if buf[b + k]))
+names_t = ["start", "evaluated", "reduced", "interp", "hash1", "hash2", "chal"]
+print("tail rounds, us relative to round start")
+for j in range(nv):
+    b = 16 * j
+    if buf[b] == 0 or buf[b + 6] == 0:
+        continue
+    t0 = buf[b]
+    print(j, " ".join(f"{names_t[k]}={(buf[b + k] - t0) * tick:.2f}" for k in range(1, 7)))

@@ -72,6 +72,7 @@ PROTOTYPES = {
     "qg_srs_generate_range": (C.c_int, [P, U64P, U64P, C.c_uint64, SZ, C.POINTER(P)]),
     "qg_srs_destroy": (C.c_int, [P]),
     "qg_srs_len": (SZ, [P]),
+    "qg_srs_window_info": (C.c_int, [P, C.POINTER(C.c_int), C.POINTER(C.c_int)]),
     "qg_srs_download": (C.c_int, [P, SZ, SZ, U64P, U8P]),
     "qg_buf_create": (C.c_int, [P, SZ, C.POINTER(P)]),
     "qg_buf_destroy": (C.c_int, [P]),

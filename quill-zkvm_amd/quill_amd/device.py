@@ -104,11 +104,15 @@ class DeviceVec:
         check(lib().qg_buf_fill_random(self.h, seed), self.dev.h)
         return self
 
-    def to_list(self, n=None):
+    def to_numpy(self, n=None):
+        """raw Montgomery limbs, shape (n, 4) uint64"""
         n = self.n if n is None else n
         out = np.zeros((max(n, 1), 4), dtype=np.uint64)
         check(lib().qg_buf_download(self.h, u64p(out), n), self.dev.h)
-        return fr_list(out[:n])
+        return out[:n]
+
+    def to_list(self, n=None):
+        return fr_list(self.to_numpy(n))
 
     def close(self):
         if self.h:
@@ -156,13 +160,24 @@ class Srs:
     def __len__(self):
         return lib().qg_srs_len(self.h)
 
-    def download(self, offset=0, n=None):
+    def window_info(self):
+        """(c, W): signed-digit window bits and window count"""
+        c, w = C.c_int(), C.c_int()
+        check(lib().qg_srs_window_info(self.h, C.byref(c), C.byref(w)), self.dev.h)
+        return c.value, w.value
+
+    def download_raw(self, offset=0, n=None):
+        """affine Montgomery limbs (n, 8) uint64 + infinity flags (n,) uint8"""
         n = len(self) - offset if n is None else n
         xy = np.zeros((max(n, 1), 8), dtype=np.uint64)
         inf = np.zeros(max(n, 1), dtype=np.uint8)
         check(lib().qg_srs_download(self.h, offset, n, u64p(xy),
                                     inf.ctypes.data_as(C.POINTER(C.c_uint8))), self.dev.h)
-        return [g1_from_abi(xy[i], inf[i]) for i in range(n)]
+        return xy[:n], inf[:n]
+
+    def download(self, offset=0, n=None):
+        xy, inf = self.download_raw(offset, n)
+        return [g1_from_abi(xy[i], inf[i]) for i in range(len(inf))]
 
     def msm(self, scalars):
         arr = fr_array(scalars) if len(scalars) else np.zeros((1, 4), dtype=np.uint64)
