@@ -16,8 +16,8 @@
 #define QG_HD __host__ __device__ __forceinline__
 #define QG_DEV __device__ __forceinline__
 #else
-#define QG_HD static inline
-#define QG_DEV static inline
+#define QG_HD inline
+#define QG_DEV inline
 #endif
 
 namespace qg {

@@ -36,6 +36,7 @@
 
 #include "blake3.h"
 #include "common.h"
+#include "field29.h"
 
 using namespace qg;
 
@@ -175,79 +176,72 @@ static SopProgram compile_program(const qg_expr_op* prog, size_t len, const uint
   return sp;
 }
 
-// device-side program image.  The byte arrays and the header are copied into
-// LDS by every block (one parallel load, no dependent scalar-cache misses on the
-// evaluation path); coefficients and the inverse Vandermonde rows follow.
+// device-side program image.  The header and byte arrays are copied into LDS
+// by every block (one parallel load, no dependent scalar-cache misses on the
+// evaluation path), followed by the 29-bit-limb constants.
+//
+// Arithmetic scale (field29.h): table entries are arkworks Montgomery values
+// (x * 2^256) re-limbed to 9 x 29 bits; mul29 multiplies by 2^-261.  A product
+// of d entries therefore carries 2^(256 - 5(d-1)).  The round sums are kept at
+// S = 2^(256 - 5(dmax-1)): a degree-dmax monomial with coefficient 1 is added
+// as is; any other monomial is multiplied by c * 2^(261 - 5(dmax-d)); a
+// constant term is stored as c * S.  The interpolation constants undo S.
 static constexpr int SOP_MAXM = 256, SOP_MAXF = 1024;
 static constexpr uint32_t SOP_HDR_WORDS = (16 + 2 * SOP_MAXM + SOP_MAXF) / 4;
 
 struct SopDev {
   uint32_t nmono, nslots, np, nfac;
   uint8_t mono_len[SOP_MAXM];
-  uint8_t is_one[SOP_MAXM];
+  uint8_t skip29[SOP_MAXM];  // 1: product already at scale S (no multiply)
   uint8_t fac[SOP_MAXF];
-  Fr coeff[SOP_MAXM];
-  // inverse Vandermonde on nodes 0..np-1: coefficient t = sum_u V[t][u] ev[u].
-  Fr vinv_m[16 * 16];  // Montgomery form
-  Fr vinv_c[16 * 16];  // plain integers: mont_mul(vinv_c, ev) is the canonical product
+  L9 c29[SOP_MAXM];          // per-monomial multiplier (or constant term), plain integer
+  L9 vm29[16 * 16];          // interpolation -> Montgomery coefficients (R = 2^256)
+  L9 vc29[16 * 16];          // interpolation -> canonical coefficients (transcript bytes)
+  L9 t29[16];                // t * 2^261 mod p (evaluation-point offsets, NP > 4)
+  L9 cr29[4];                // 2^522, 2^778 (-> r * 2^261); 2^517, 2^773 (-> r * 2^256)
+  Fr coeff[SOP_MAXM];        // Montgomery coefficients (final claim on the 32-bit path)
+  uint8_t is_one[SOP_MAXM];  // (final claim)
 };
-static_assert(offsetof(SopDev, coeff) == SOP_HDR_WORDS * 4, "SopDev layout");
+static_assert(offsetof(SopDev, c29) == SOP_HDR_WORDS * 4, "SopDev layout");
 
 // program header passed by value (no dependent loads before the LDS copy)
 struct SopHdr {
   uint32_t nmono, nslots, np, pad;
 };
 
-static void build_vinv(uint32_t np, Fr* out_m, Fr* out_c) {
-  // coefficients of L_j(X) = prod_{m != j} (X - m) / (j - m), out[i*16 + j] = coeff_i(L_j)
-  for (uint32_t i = 0; i < 16 * 16; i++) out_m[i] = out_c[i] = Fr::zero();
-  for (uint32_t j = 0; j < np; j++) {
-    std::vector<Fr> poly(1, Fr::one());
-    Fr den = Fr::one();
-    for (uint32_t m = 0; m < np; m++) {
-      if (m == j) continue;
-      std::vector<Fr> np2(poly.size() + 1, Fr::zero());
-      Fr negm = fneg(from_u64<FrP>(m));
-      for (size_t k = 0; k < poly.size(); k++) {
-        np2[k] = np2[k] + poly[k] * negm;
-        np2[k + 1] = np2[k + 1] + poly[k];
-      }
-      poly = np2;
-      Fr diff = (j >= m) ? from_u64<FrP>(j - m) : fneg(from_u64<FrP>(m - j));
-      den = den * diff;
-    }
-    Fr dinv = finv(den);
-    for (uint32_t i = 0; i < np; i++) {
-      out_m[i * 16 + j] = poly[i] * dinv;
-      out_c[i * 16 + j] = from_mont(out_m[i * 16 + j]);
-    }
-  }
-}
+using R29 = F29<FrP>;
 
 template <int NP>
 struct SopLds {
   uint32_t w[SOP_HDR_WORDS];
-  Fr coeff[SOP_MAXM];
-  Fr vm[NP * NP];
-  Fr vc[NP * NP];
+  R29 c29[SOP_MAXM];
+  R29 vm[NP * NP];
+  R29 vc[NP * NP];
+  R29 t29[NP];
+  R29 cr[4];
   QG_DEV uint32_t nmono() const { return w[0]; }
   QG_DEV uint32_t mono_len(uint32_t m) const { return ((const uint8_t*)w)[16 + m]; }
-  QG_DEV uint32_t is_one(uint32_t m) const { return ((const uint8_t*)w)[16 + SOP_MAXM + m]; }
+  QG_DEV uint32_t skip(uint32_t m) const { return ((const uint8_t*)w)[16 + SOP_MAXM + m]; }
   QG_DEV uint32_t fac(uint32_t f) const { return ((const uint8_t*)w)[16 + 2 * SOP_MAXM + f]; }
 };
 
 template <int NP>
 QG_DEV void sop_load(SopLds<NP>& s, const SopDev* __restrict__ g, const SopHdr& h, bool vinv) {
+  const uint32_t tid = threadIdx.x, nt = blockDim.x;
   const uint32_t* gw = reinterpret_cast<const uint32_t*>(g);
-  for (uint32_t i = threadIdx.x; i < SOP_HDR_WORDS; i += blockDim.x) s.w[i] = gw[i];
-  const uint32_t* gc = reinterpret_cast<const uint32_t*>(g->coeff);
-  uint32_t* lc = reinterpret_cast<uint32_t*>(s.coeff);
-  for (uint32_t i = threadIdx.x; i < h.nmono * 8; i += blockDim.x) lc[i] = gc[i];
+  for (uint32_t i = tid; i < SOP_HDR_WORDS; i += nt) s.w[i] = gw[i];
+  const uint32_t* gc = reinterpret_cast<const uint32_t*>(g->c29);
+  uint32_t* lc = reinterpret_cast<uint32_t*>(s.c29);
+  for (uint32_t i = tid; i < h.nmono * 9; i += nt) lc[i] = gc[i];
+  for (uint32_t i = tid; i < NP * 9; i += nt)
+    reinterpret_cast<uint32_t*>(s.t29)[i] = reinterpret_cast<const uint32_t*>(g->t29)[i];
+  for (uint32_t i = tid; i < 4 * 9; i += nt)
+    reinterpret_cast<uint32_t*>(s.cr)[i] = reinterpret_cast<const uint32_t*>(g->cr29)[i];
   if (vinv) {
-    for (uint32_t i = threadIdx.x; i < h.np * h.np * 8; i += blockDim.x) {
-      const uint32_t e = i >> 3, k = i & 7, t = e / h.np, u = e % h.np;
-      s.vm[t * NP + u].v[k] = g->vinv_m[t * 16 + u].v[k];
-      s.vc[t * NP + u].v[k] = g->vinv_c[t * 16 + u].v[k];
+    for (uint32_t i = tid; i < h.np * h.np * 9; i += nt) {
+      const uint32_t e = i / 9, k = i % 9, t = e / h.np, u = e % h.np;
+      s.vm[t * NP + u].l[k] = g->vm29[t * 16 + u].v[k];
+      s.vc[t * NP + u].l[k] = g->vc29[t * 16 + u].v[k];
     }
   }
 }
@@ -271,21 +265,20 @@ QG_DEV Fr sel(const Fr (&v)[K], uint32_t i) {
   }
 }
 
-// h(values) via the monomial program (single point)
-template <int K, int NP>
-QG_DEV Fr sop_eval(const SopLds<NP>& sp, const Fr (&val)[K]) {
+// h(values) on the 32-bit path (final claim): Montgomery coefficients from HBM
+template <int K>
+QG_DEV Fr sop_eval_final(const SopDev* __restrict__ g, uint32_t nmono, const Fr (&val)[K]) {
   Fr acc = Fr::zero();
   uint32_t f = 0;
-  const uint32_t nmono = sp.nmono();
   for (uint32_t m = 0; m < nmono; m++) {
-    const uint32_t len = sp.mono_len(m);
+    const uint32_t len = g->mono_len[m];
     Fr prod;
     if (len == 0) {
-      prod = sp.coeff[m];
+      prod = g->coeff[m];
     } else {
-      prod = sel<K>(val, sp.fac(f));
-      for (uint32_t q = 1; q < len; q++) prod = prod * sel<K>(val, sp.fac(f + q));
-      if (!sp.is_one(m)) prod = prod * sp.coeff[m];
+      prod = sel<K>(val, g->fac[f]);
+      for (uint32_t q = 1; q < len; q++) prod = prod * sel<K>(val, g->fac[f + q]);
+      if (!g->is_one[m]) prod = prod * g->coeff[m];
     }
     f += len;
     acc = acc + prod;
@@ -305,17 +298,23 @@ QG_DEV Fr shfl_xor_fr(const Fr& a, int m) {
   return r;
 }
 
-// t * x for a small per-lane integer t < NP (branch-free double-and-add)
-template <int NP>
-QG_DEV Fr mul_small(const Fr& x, uint32_t t) {
-  Fr acc = (t & 1u) ? x : Fr::zero();
-  Fr y = x;
+// lazy value < 6p -> normalized, < 2p
+QG_DEV R29 red6p(const R29& a) {
+  return condsub29<FrP>(condsub29<FrP>(normfull29<FrP>(a), l9_mul_small(F29P<FrP>::P, 4)),
+                        F29P<FrP>::P2);
+}
+
+// x < 2^256 as 8 x 32 words, reduced modulo p below 2p (values here are < 3p)
+QG_DEV Fr lt_p(const Fr& x) {
+  uint32_t t[8];
 #pragma unroll
-  for (int b = 1; (1 << b) < NP; b++) {
-    y = y + y;
-    acc = acc + (((t >> b) & 1u) ? y : Fr::zero());
-  }
-  return acc;
+  for (int i = 0; i < 8; i++) t[i] = x.v[i];
+  reduce_once<FrP>(t);
+  reduce_once<FrP>(t);
+  Fr r;
+#pragma unroll
+  for (int i = 0; i < 8; i++) r.v[i] = t[i];
+  return r;
 }
 
 // ---------------------------------------------------------------------------
@@ -327,18 +326,19 @@ QG_DEV Fr mul_small(const Fr& x, uint32_t t) {
 // Every thread carries one field accumulator, so registers stay low (high
 // occupancy on the large rounds) and the dependent chain per round is one
 // fold multiply plus deg-1 product multiplies (low latency on the small ones).
+// All arithmetic is 29-bit-limb (field29.h); folded tables are stored < 2p.
 // ---------------------------------------------------------------------------
 template <int K, int NP, int BLOCK>
 struct RoundLds {
-  Fr F[K * (BLOCK / NP) * 2];  // [slot][pair][half]
+  R29 F[K * (BLOCK / NP) * 2];  // [slot][pair][half]
   const Fr* src[8];
   Fr* dst[8];
 };
 
 template <int K, int NP, int BLOCK>
 QG_DEV void round_sweep(RoundLds<K, NP, BLOCK>& L, const SopLds<NP>& sp, const SopHdr& h,
-                        size_t npairs, bool fold, const Fr& r, size_t base0, size_t stride,
-                        Fr& acc) {
+                        size_t npairs, bool fold, const R29& r, size_t base0, size_t stride,
+                        R29& acc) {
   constexpr uint32_t PB = BLOCK / NP;
   const uint32_t tid = threadIdx.x, t = tid % NP, pl = tid / NP;
   const uint32_t nitems = h.nslots * PB * 2;
@@ -346,75 +346,91 @@ QG_DEV void round_sweep(RoundLds<K, NP, BLOCK>& L, const SopLds<NP>& sp, const S
     for (uint32_t it = tid; it < nitems; it += BLOCK) {
       const uint32_t s = it / (PB * 2), e = it % (PB * 2);
       const size_t p = base + (e >> 1);
-      Fr v = Fr::zero();
+      R29 v = R29::zero();
       if (p < npairs) {
         if (fold) {
           const Fr* src = L.src[s] + 4 * p + 2 * (e & 1);
-          const Fr x0 = src[0], x1 = src[1];
-          v = x0 + r * (x1 - x0);
-          L.dst[s][2 * p + (e & 1)] = v;
+          const R29 x0 = to29(src[0]), x1 = to29(src[1]);
+          // x0 + r (x1 - x0): x1 - x0 + 4p (lazy) times r (< 2p) -> < 2p; + x0 -> < 4p
+          v = red6p(add29(x0, mul29(sub29(x1, x0), r)));
+          L.dst[s][2 * p + (e & 1)] = from29(v);
         } else {
-          v = L.src[s][2 * p + (e & 1)];
+          v = to29(L.src[s][2 * p + (e & 1)]);
         }
       }
       L.F[s * PB * 2 + e] = v;
     }
     __syncthreads();
     if (t < h.np && base + pl < npairs) {
-      Fr sum = Fr::zero();
+      R29 sum = R29::zero();
       uint32_t f = 0;
       for (uint32_t m = 0; m < h.nmono; m++) {
         const uint32_t len = sp.mono_len(m);
-        Fr prod;
+        R29 prod;
         if (len == 0) {
-          prod = sp.coeff[m];
+          prod = sp.c29[m];
         } else {
           for (uint32_t q = 0; q < len; q++) {
             const uint32_t s = sp.fac(f + q);
-            const Fr lo = L.F[(s * PB + pl) * 2], hi = L.F[(s * PB + pl) * 2 + 1];
-            const Fr v = lo + mul_small<NP>(hi - lo, t);
-            prod = q == 0 ? v : prod * v;
+            const R29 lo = L.F[(s * PB + pl) * 2], hi = L.F[(s * PB + pl) * 2 + 1];
+            R29 v;
+            if constexpr (NP <= 4) {
+              // lo + t (hi - lo + 4p): lazy, < 20p, then one carry pass
+              const R29 d = norm29(sub29(hi, lo));
+              R29 a = lo;
+              if (t & 1u) a = add29(a, d);
+              if (t & 2u) a = add29(a, add29(d, d));
+              v = norm29(a);
+            } else {
+              v = add29(lo, mul29(sub29(hi, lo), sp.t29[t]));  // < 4p, lazy
+              v = norm29(v);
+            }
+            prod = q == 0 ? v : mul29(prod, v);
           }
-          if (!sp.is_one(m)) prod = prod * sp.coeff[m];
+          if (!sp.skip(m) || len == 1) prod = mul29(prod, sp.c29[m]);
         }
         f += len;
-        sum = sum + prod;
+        sum = red6p(add29(sum, prod));
       }
-      acc = acc + sum;
+      acc = red6p(add29(acc, sum));
     }
     __syncthreads();
   }
 }
 
-// Sum of acc over the threads of each point t (t = tid % NP) -> res[t] (LDS),
-// visible to all threads on return.  red: (BLOCK / 64) * NP LDS scratch.
+// Sum of acc over the threads of each point t (t = tid % NP) -> res[t] (LDS,
+// canonical 32-bit words at scale S), visible to all threads on return.
+// red: (BLOCK / 64) * NP LDS scratch.
 template <int NP>
-QG_DEV void block_reduce_pts(Fr acc, uint32_t np, Fr* red, Fr* res) {
+QG_DEV void block_reduce_pts(R29 acc, uint32_t np, R29* red, Fr* res) {
 #pragma unroll
-  for (int m = 32; m >= NP; m >>= 1) acc = acc + shfl_xor_fr(acc, m);
+  for (int m = 32; m >= NP; m >>= 1) acc = red6p(add29(acc, shfl_xor29(acc, m)));
   const uint32_t lane = threadIdx.x & 63, wid = threadIdx.x >> 6, nw = blockDim.x >> 6;
   if (lane < NP) red[wid * NP + lane] = acc;
   __syncthreads();
   if (threadIdx.x < np) {
-    Fr a = red[threadIdx.x];
-    for (uint32_t w = 1; w < nw; w++) a = a + red[w * NP + threadIdx.x];
-    res[threadIdx.x] = a;
+    R29 a = red[threadIdx.x];
+    for (uint32_t w = 1; w < nw; w++) a = red6p(add29(a, red[w * NP + threadIdx.x]));
+    res[threadIdx.x] = from29(canon29(a));
   }
   __syncthreads();
 }
 
-// Round bookkeeping.  The transcript state, the deferred absorb and the
-// last-block election counter live in one small device struct.
+// Round bookkeeping.  The transcript state, the deferred absorb, the current
+// challenge in 29-bit form and the last-block election counter live in one
+// small device struct.
 struct ScState {
   uint32_t state[8];  // absorbed transcript state
   uint32_t pend[20];  // state' || 48 challenge bytes of the last round, not yet absorbed
   uint32_t ticket;    // blocks of the current round that have published partials
-  uint32_t pad[3];
+  uint32_t err;       // persistent-kernel barrier timeout flag
+  uint32_t r29[9];    // last challenge * 2^261 mod p (< 2p), the fold multiplier
+  uint32_t pad[1];
 };
 
 struct RoundOut {
   ScState* st;
-  Fr* chal;          // nvars challenges
+  Fr* chal;          // nvars challenges (Montgomery, R = 2^256)
   Fr* coeffs;        // nvars x width (Montgomery)
   uint32_t* lens;    // nvars
   uint32_t width;    // row width (>= np)
@@ -425,15 +441,17 @@ struct FinSmem {
   uint32_t chin[16];  // state' || "challenge" || zero pad
   uint32_t xof[16];   // B3-XOF(state' || "challenge")[0..64)
   uint32_t ab[32];    // state' || challenge bytes || zero pad (absorb)
-  Fr r;               // the round challenge (Montgomery)
+  R29 r;              // the round challenge * 2^261 (fold multiplier)
+  Fr r256;            // the round challenge (Montgomery, R = 2^256)
 };
 
-// Round message, transcript and challenge from the np round sums ev[] (LDS).
-// Whole block calls (barriers); wave 0 works.  Interpolation is lane-parallel
-// over (coefficient t, node u): each lane multiplies by the inverse
-// Vandermonde entry in Montgomery form (proof output) and as a plain integer
-// (the canonical transcript bytes, no separate from_mont), then a shuffle sum
-// over u.  Trim by ballot; BLAKE3 on one DPP quad; r from two lanes.
+// Round message, transcript and challenge from the np round sums ev[] (LDS,
+// canonical words at scale S).  Whole block calls (barriers); wave 0 works.
+// Interpolation is lane-parallel over (coefficient t, node u): each lane
+// multiplies by the inverse-Vandermonde entry scaled to give the Montgomery
+// coefficient (proof output) and the canonical one (transcript bytes), then a
+// shuffle sum over u.  Trim by ballot; BLAKE3 on one DPP quad; r from four
+// lanes (r * 2^261 for the fold and r * 2^256 for the output, each lo + hi).
 // Absorbing the 48 challenge bytes is deferred when pend_out != nullptr.
 template <int NP>
 QG_DEV void finish_core(const SopLds<NP>& sp, uint32_t np, const Fr* ev, const RoundOut& ro,
@@ -443,32 +461,33 @@ QG_DEV void finish_core(const SopLds<NP>& sp, uint32_t np, const Fr* ev, const R
   const uint32_t tid = threadIdx.x;
   const bool w0 = tid < 64;
   const uint32_t ct = tid / U, cu = tid % U;
-  Fr cm = Fr::zero(), cc = Fr::zero();
+  R29 cm = R29::zero(), cc = R29::zero();
   if (w0 && ct < np) {
     for (uint32_t u = cu; u < np; u += U) {
-      const Fr e = ev[u];
-      cm = cm + sp.vm[ct * NP + u] * e;
-      cc = cc + sp.vc[ct * NP + u] * e;
+      const R29 e = to29(ev[u]);
+      cm = red6p(add29(cm, mul29(sp.vm[ct * NP + u], e)));
+      cc = red6p(add29(cc, mul29(sp.vc[ct * NP + u], e)));
     }
   }
 #pragma unroll
   for (uint32_t m = 1; m < U; m <<= 1) {
-    cm = cm + shfl_xor_fr(cm, m);
-    cc = cc + shfl_xor_fr(cc, m);
+    cm = red6p(add29(cm, shfl_xor29(cm, m)));
+    cc = red6p(add29(cc, shfl_xor29(cc, m)));
   }
+  const Fr cmw = from29(canon29(cm)), ccw = from29(canon29(cc));
   const bool lead = w0 && cu == 0 && ct < np;
   if (writer) {
-    if (lead) ro.coeffs[(size_t)j * ro.width + ct] = cm;
+    if (lead) ro.coeffs[(size_t)j * ro.width + ct] = cmw;
     for (uint32_t i = np + tid; i < ro.width; i += blockDim.x)
       ro.coeffs[(size_t)j * ro.width + i] = Fr::zero();
   }
-  const uint64_t nz = __ballot(lead && !cc.is_zero());
+  const uint64_t nz = __ballot(lead && !ccw.is_zero());
   // highest nonzero coefficient: lane index / U + 1 (wave 0's ballot)
   const uint32_t len = nz ? (63u - (uint32_t)__clzll(nz)) / U + 1u : 0u;
   if (tid < 8) fs.msg[tid] = state_in[tid];
   if (lead) {
 #pragma unroll
-    for (int i = 0; i < 8; i++) fs.msg[10 + 8 * ct + i] = cc.v[i];
+    for (int i = 0; i < 8; i++) fs.msg[10 + 8 * ct + i] = ccw.v[i];
   }
   for (uint32_t i = 10 + 8 * np + tid; i < 144; i += blockDim.x) fs.msg[i] = 0;
   if (tid == 0) {
@@ -490,21 +509,21 @@ QG_DEV void finish_core(const SopLds<NP>& sp, uint32_t np, const Fr* ev, const R
   __syncthreads();
   SC_TR(tr + 5);
   if (w0) {
-    // r = LE(48 B) mod r: lo * R^2 + hi * R^3 (Montgomery), lanes 0 and 1
-    Fr x, c;
+    // r = lo + hi * 2^256 mod p (lo: bytes 0..31, hi: bytes 32..47)
+    // lanes 0/1: lo * 2^522, hi * 2^778 -> r * 2^261; lanes 2/3: ... -> r * 2^256
+    Fr x;
 #pragma unroll
-    for (int i = 0; i < 8; i++) {
-      x.v[i] = (tid & 1) ? (i < 4 ? fs.xof[8 + i] : 0u) : fs.xof[i];
-      c.v[i] = (tid & 1) ? FrP::R3[i] : FrP::R2[i];
-    }
-    const Fr p = x * c;
-    const Fr rr = p + shfl_xor_fr(p, 1);
-    if (tid == 0) {
+    for (int i = 0; i < 8; i++) x.v[i] = (tid & 1) ? (i < 4 ? fs.xof[8 + i] : 0u) : fs.xof[i];
+    const R29 p = mul29(to29(x), sp.cr[tid & 3]);
+    const R29 q = red6p(add29(p, shfl_xor29(p, 1)));
+    if (tid == 0) fs.r = q;
+    if (tid == 2) {
+      const Fr rr = from29(canon29(q));
+      fs.r256 = rr;
       if (writer) {
         ro.chal[j] = rr;
         ro.lens[j] = len;
       }
-      fs.r = rr;
     }
   }
   if (pend_out) {
@@ -527,7 +546,7 @@ __global__ void __launch_bounds__(SC_BLOCK)
                RoundOut ro, uint32_t j, int pending, Fr* __restrict__ partial, Fr* __restrict__ loc) {
   __shared__ SopLds<NP> sp;
   __shared__ RoundLds<K, NP, SC_BLOCK> L;
-  __shared__ Fr red[(SC_BLOCK / 64) * NP];
+  __shared__ R29 red[(SC_BLOCK / 64) * NP];
   __shared__ Fr res[NP];
   __shared__ FinSmem fs;
   __shared__ uint32_t last;
@@ -542,7 +561,11 @@ __global__ void __launch_bounds__(SC_BLOCK)
       L.dst[i] = tp.dst[i];
     }
   }
-  const Fr r = fold ? ro.chal[j - 1] : Fr::zero();
+  R29 r = R29::zero();
+  if (fold) {
+#pragma unroll
+    for (int i = 0; i < 9; i++) r.l[i] = ro.st->r29[i];
+  }
   if (pending && blockIdx.x == 0 && tid >= 64 && tid < 128) {
     // deferred absorb of round j-1's challenge bytes (wave 1 of block 0)
     if (tid - 64 < 32) fs.ab[tid - 64] = tid - 64 < 20 ? ro.st->pend[tid - 64] : 0u;
@@ -553,7 +576,7 @@ __global__ void __launch_bounds__(SC_BLOCK)
   }
   __syncthreads();
   constexpr uint32_t PB = SC_BLOCK / NP;
-  Fr acc = Fr::zero();
+  R29 acc = R29::zero();
   round_sweep<K, NP, SC_BLOCK>(L, sp, h, npairs, fold != 0, r, (size_t)blockIdx.x * PB,
                                (size_t)gridDim.x * PB, acc);
   if (blockIdx.x == 0) SC_TR(tr + 1);
@@ -570,12 +593,12 @@ __global__ void __launch_bounds__(SC_BLOCK)
   __syncthreads();
   if (!last) return;
   SC_TR(tr + 2);
-  acc = Fr::zero();
+  acc = R29::zero();
   {
     const uint32_t t = tid % NP;
     if (t < h.np)
       for (uint32_t b = tid / NP; b < gridDim.x; b += SC_BLOCK / NP)
-        acc = acc + partial[(size_t)b * NP + t];
+        acc = red6p(add29(acc, to29(partial[(size_t)b * NP + t])));
   }
   block_reduce_pts<NP>(acc, h.np, red, res);
   if (tid == 0) ro.st->ticket = 0;
@@ -584,6 +607,7 @@ __global__ void __launch_bounds__(SC_BLOCK)
     return;
   }
   finish_core<NP>(sp, h.np, res, ro, j, fs, ro.st->state, ro.st->pend, nullptr, tr);
+  if (tid < 9) ro.st->r29[tid] = fs.r.l[tid];
   SC_TR(tr + 7);
 }
 
@@ -593,23 +617,24 @@ __global__ void __launch_bounds__(SC_BLOCK)
     k_sc_finish(const SopDev* __restrict__ spg, SopHdr h, const Fr* __restrict__ rows,
                 uint32_t nrows, RoundOut ro, uint32_t j) {
   __shared__ SopLds<NP> sp;
-  __shared__ Fr red[(SC_BLOCK / 64) * NP];
+  __shared__ R29 red[(SC_BLOCK / 64) * NP];
   __shared__ Fr res[NP];
   __shared__ FinSmem fs;
   __shared__ uint32_t st[8];
   const uint32_t tid = threadIdx.x;
   sop_load<NP>(sp, spg, h, true);
   if (tid < 8) st[tid] = ro.st->state[tid];
-  Fr acc = Fr::zero();
+  R29 acc = R29::zero();
   {
     const uint32_t t = tid % NP;
     if (t < h.np)
       for (uint32_t b = tid / NP; b < nrows; b += SC_BLOCK / NP)
-        acc = acc + rows[(size_t)b * NP + t];
+        acc = red6p(add29(acc, to29(rows[(size_t)b * NP + t])));
   }
   __syncthreads();
   block_reduce_pts<NP>(acc, h.np, red, res);
   finish_core<NP>(sp, h.np, res, ro, j, fs, st, nullptr, ro.st->state);
+  if (tid < 9) ro.st->r29[tid] = fs.r.l[tid];
 }
 
 // Grid barrier among the first n blocks (monotonic per-round counter).  Every
@@ -655,7 +680,7 @@ __global__ void __launch_bounds__(TAIL_BLOCK)
   constexpr uint32_t PB = TAIL_BLOCK / NP;
   __shared__ SopLds<NP> sp;
   __shared__ RoundLds<K, NP, TAIL_BLOCK> L;
-  __shared__ Fr red[(TAIL_BLOCK / 64) * NP];
+  __shared__ R29 red[(TAIL_BLOCK / 64) * NP];
   __shared__ Fr res[NP];
   __shared__ FinSmem fs;
   __shared__ uint32_t st[8];
@@ -666,7 +691,11 @@ __global__ void __launch_bounds__(TAIL_BLOCK)
   sop_load<NP>(sp, spg, h, true);
   if (tid < 8) st[tid] = ro.st->state[tid];
   if (tid < 32) pend[tid] = (pending0 && tid < 20) ? ro.st->pend[tid] : 0u;
-  Fr r = fold0 ? ro.chal[j0 - 1] : Fr::zero();
+  R29 r = R29::zero();
+  if (fold0) {
+#pragma unroll
+    for (int i = 0; i < 9; i++) r.l[i] = ro.st->r29[i];
+  }
   TablePtrs cur = tp0;
   int fold = fold0, pending = pending0;
   for (uint32_t j = j0; j < nvars; j++) {
@@ -683,7 +712,7 @@ __global__ void __launch_bounds__(TAIL_BLOCK)
     __syncthreads();
     if (writer) SC_TR(16 * j + 0);
     if (pending && tid >= 64 && tid < 128) b3_hash_quad(pend, 80, st, 8);  // wave 1
-    Fr acc = Fr::zero();
+    R29 acc = R29::zero();
     round_sweep<K, NP, TAIL_BLOCK>(L, sp, h, npairs, fold != 0, r, (size_t)blk * PB,
                                    (size_t)nb * PB, acc);
     if (writer) SC_TR(16 * j + 1);
@@ -691,11 +720,12 @@ __global__ void __launch_bounds__(TAIL_BLOCK)
     if (nb > 1) {
       Fr* part = partial + (size_t)(j & 1) * gridDim.x * NP;
       if (tid < np) part[(size_t)blk * NP + tid] = res[tid];
-      grid_barrier(bar + j, nb, &ro.st->pad[0]);
-      acc = Fr::zero();
+      grid_barrier(bar + j, nb, &ro.st->err);
+      acc = R29::zero();
       const uint32_t t = tid % NP;
       if (t < np)
-        for (uint32_t b = tid / NP; b < nb; b += PB) acc = acc + part[(size_t)b * NP + t];
+        for (uint32_t b = tid / NP; b < nb; b += PB)
+          acc = red6p(add29(acc, to29(part[(size_t)b * NP + t])));
       block_reduce_pts<NP>(acc, np, red, res);
     }
     if (writer) SC_TR(16 * j + 2);
@@ -714,20 +744,21 @@ __global__ void __launch_bounds__(TAIL_BLOCK)
     cur = nxt;
     fold = 1;
   }
-  // final fold with r_{n-1}: cur.src has 2 entries per slot (block 0 only here)
+  // final fold with r_{n-1} on the 32-bit path: cur.src has 2 entries per slot
   if (tid == 0) {
+    const Fr rr = fs.r256;
     Fr val[K];
 #pragma unroll
     for (int i = 0; i < K; i++) {
       if ((uint32_t)i < nslots) {
-        Fr a = cur.src[i][0], b = cur.src[i][1];
-        val[i] = a + r * (b - a);
+        const Fr a = lt_p(cur.src[i][0]), b = lt_p(cur.src[i][1]);
+        val[i] = a + rr * (b - a);
         final_vals[i] = val[i];
       } else {
         val[i] = Fr::zero();
       }
     }
-    *evaluation = sop_eval<K, NP>(sp, val);
+    *evaluation = sop_eval_final<K>(spg, h.nmono, val);
   }
   // absorb the last challenge bytes
   if (pending && tid >= 64 && tid < 128) b3_hash_quad(pend, 80, ro.st->state, 8);
@@ -759,7 +790,7 @@ __global__ void k_sc_fold_last(TablePtrs cur, uint32_t nslots, const Fr* __restr
   const uint32_t i = threadIdx.x;
   if (i >= nslots) return;
   const Fr r = *chal;
-  const Fr a = cur.src[i][0], b = cur.src[i][1];
+  const Fr a = lt_p(cur.src[i][0]), b = lt_p(cur.src[i][1]);
   out[i] = a + r * (b - a);
 }
 
@@ -805,6 +836,48 @@ void eq_table_device(qg_ctx* ctx, const Fr* d_z, uint32_t nvars, Fr* d_out) {
   QG_LAUNCH_CHECK();
 }
 
+// host helpers on plain integers (< p)
+static Fr plain_mul(const Fr& x, const Fr& y) { return from_mont(to_mont(x) * to_mont(y)); }
+static Fr from_u64_plain(uint64_t v) {
+  Fr r = Fr::zero();
+  r.v[0] = (uint32_t)v;
+  r.v[1] = (uint32_t)(v >> 32);
+  return r;
+}
+static L9 l9_of(const Fr& x) {
+  const R29 t = to29(x);
+  L9 r{};
+  for (int i = 0; i < 9; i++) r.v[i] = t.l[i];
+  return r;
+}
+
+// inverse Vandermonde on nodes 0..np-1: coefficient t of sum_u L_u(X) ev[u] is
+// sum_u V[t][u] ev[u]; out_m[t*16+u] = V (Montgomery), out_c = V (plain)
+static void build_vinv(uint32_t np, Fr* out_m, Fr* out_c) {
+  for (uint32_t i = 0; i < 16 * 16; i++) out_m[i] = out_c[i] = Fr::zero();
+  for (uint32_t j = 0; j < np; j++) {
+    std::vector<Fr> poly(1, Fr::one());
+    Fr den = Fr::one();
+    for (uint32_t m = 0; m < np; m++) {
+      if (m == j) continue;
+      std::vector<Fr> np2(poly.size() + 1, Fr::zero());
+      Fr negm = fneg(from_u64<FrP>(m));
+      for (size_t k = 0; k < poly.size(); k++) {
+        np2[k] = np2[k] + poly[k] * negm;
+        np2[k + 1] = np2[k + 1] + poly[k];
+      }
+      poly = np2;
+      Fr diff = (j >= m) ? from_u64<FrP>(j - m) : fneg(from_u64<FrP>(m - j));
+      den = den * diff;
+    }
+    Fr dinv = finv(den);
+    for (uint32_t i = 0; i < np; i++) {
+      out_m[i * 16 + j] = poly[i] * dinv;
+      out_c[i * 16 + j] = from_mont(out_m[i * 16 + j]);
+    }
+  }
+}
+
 // Compiled programs are cached by their exact bytes (the device image carries
 // the inverse Vandermonde, whose host construction costs field inversions).
 struct ScProgram {
@@ -848,13 +921,34 @@ static std::shared_ptr<const ScProgram> get_program(const qg_expr_op* prog, size
   d.nslots = (uint32_t)sp.used.size();
   d.np = np;
   d.nfac = (uint32_t)sp.fac.size();
+  // scale bookkeeping of the 29-bit evaluation (see SopDev): e = 5 (dmax - 1)
+  const int dmax = (int)sp.degree, e = 5 * (dmax - 1);
   for (size_t m = 0; m < sp.mono_len.size(); m++) {
-    d.mono_len[m] = (uint8_t)sp.mono_len[m];
+    const int dm = (int)sp.mono_len[m];
+    d.mono_len[m] = (uint8_t)dm;
     d.is_one[m] = sp.is_one[m];
     d.coeff[m] = sp.coeff[m];
+    const Fr c = from_mont(sp.coeff[m]);
+    const uint32_t k = dm == 0 ? (uint32_t)(256 - e) : (uint32_t)(261 - 5 * (dmax - dm));
+    d.c29[m] = l9_of(plain_mul(c, pow2_mod_plain<FrP>(k)));
+    d.skip29[m] = (dm == dmax && dm >= 2 && sp.is_one[m]) ? 1 : 0;
   }
   for (size_t f = 0; f < sp.fac.size(); f++) d.fac[f] = (uint8_t)sp.fac[f];
-  build_vinv(np, d.vinv_m, d.vinv_c);
+  {
+    Fr vm[16 * 16], vc[16 * 16];
+    build_vinv(np, vm, vc);  // vc: plain inverse-Vandermonde entries
+    const Fr sm = pow2_mod_plain<FrP>((uint32_t)(261 + e)), sc = pow2_mod_plain<FrP>((uint32_t)(5 + e));
+    for (uint32_t i = 0; i < 16 * 16; i++) {
+      d.vm29[i] = l9_of(plain_mul(vc[i], sm));
+      d.vc29[i] = l9_of(plain_mul(vc[i], sc));
+    }
+  }
+  for (uint32_t t = 0; t < 16; t++)
+    d.t29[t] = l9_of(plain_mul(from_u64_plain(t), pow2_mod_plain<FrP>(261)));
+  d.cr29[0] = l9_of(pow2_mod_plain<FrP>(522));
+  d.cr29[1] = l9_of(pow2_mod_plain<FrP>(778));
+  d.cr29[2] = l9_of(pow2_mod_plain<FrP>(517));
+  d.cr29[3] = l9_of(pow2_mod_plain<FrP>(773));
   p->hdr = {d.nmono, d.nslots, np, 0};
   p->used = sp.used;
   p->nused = (uint32_t)sp.used.size();
@@ -1099,7 +1193,7 @@ static void sumcheck_run(qg_ctx* ctx, uint32_t nvars, uint32_t ntables,
   std::vector<uint8_t> h(io_bytes);
   QG_HIP(hipMemcpyAsync(h.data(), io, io_bytes, hipMemcpyDeviceToHost, ctx->stream));
   ctx->sync();
-  QG_CHECK(reinterpret_cast<const ScState*>(h.data())->pad[0] == 0, QG_ERR_DEVICE,
+  QG_CHECK(reinterpret_cast<const ScState*>(h.data())->err == 0, QG_ERR_DEVICE,
            "sumcheck: grid barrier timed out (persistent blocks not co-resident)");
   memcpy(state, h.data(), 32);
   memcpy(round_lens, h.data() + o_lens, sizeof(uint32_t) * nvars);

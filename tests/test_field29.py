@@ -1,0 +1,53 @@
+"""CPU check of the 29-bit-limb Montgomery layer (csrc/field29.h, host build):
+mul29 = a*b*2^-261 mod p with output < 2p, lazy add/sub + normalisation, the
+2p / p conditional subtractions.  Python integers are the reference."""
+import os
+import shutil
+import subprocess
+import tempfile
+
+import pytest
+
+ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+P = 21888242871839275222246405745257275088696311157297823662689037894645226208583
+RINV = pow(2, -261, P)
+
+
+@pytest.fixture(scope="module")
+def rows():
+    gxx = shutil.which("g++")
+    if gxx is None:
+        pytest.skip("g++ not available")
+    d = tempfile.mkdtemp()
+    exe = os.path.join(d, "f29")
+    subprocess.run([gxx, "-O2", "-std=c++17", "-o", exe,
+                    os.path.join(ROOT, "tests", "cpp", "field29_check.cpp")], check=True)
+    out = subprocess.run([exe], check=True, stdout=subprocess.PIPE).stdout.decode()
+    shutil.rmtree(d, ignore_errors=True)
+    res = []
+    for line in out.strip().splitlines():
+        res.append({k: int(v, 16) for k, v in (kv.split("=") for kv in line.split())})
+    return res
+
+
+def test_mul29(rows):
+    for r in rows:
+        assert r["m"] % P == r["a"] * r["b"] * RINV % P
+        assert r["m"] < 2 * P
+
+
+def test_sub_then_mul(rows):
+    for r in rows:
+        assert r["md"] % P == (r["a"] - r["b"]) * r["c"] * RINV % P
+        assert r["md"] < 2 * P
+
+
+def test_reduce_and_canon(rows):
+    for r in rows:
+        assert r["r"] < 2 * P and r["r"] % P == (r["m"] + r["c"]) % P
+        assert r["cm"] == r["m"] % P
+
+
+def test_lazy_operand(rows):
+    for r in rows:
+        assert r["lz"] % P == (r["a"] + r["b"]) * r["c"] * RINV % P
