@@ -67,12 +67,56 @@ constexpr uint32_t l9_inv29(uint32_t p0) {
   return (0u - x) & M29;  // -p^-1 mod 2^29
 }
 
+constexpr bool l9_geq(const L9& a, const L9& b) {
+  for (int i = 8; i >= 0; i--)
+    if (a.v[i] != b.v[i]) return a.v[i] > b.v[i];
+  return true;
+}
+
+constexpr L9 l9_sub(const L9& a, const L9& b) {
+  L9 r{};
+  uint32_t br = 0;
+  for (int i = 0; i < 9; i++) {
+    const uint32_t t = a.v[i] - b.v[i] - br;
+    br = t >> 31;
+    r.v[i] = i < 8 ? (t & M29) : t;
+  }
+  return r;
+}
+
+// 2^k mod p (plain integer), normalized limbs
+constexpr L9 l9_pow2_mod(const L9& p, uint32_t k) {
+  L9 x{};
+  x.v[0] = 1;
+  for (uint32_t j = 0; j < k; j++) {
+    x = l9_mul_small(x, 2);
+    if (l9_geq(x, p)) x = l9_sub(x, p);
+  }
+  return x;
+}
+
+struct L9x8 {
+  L9 k[8];
+};
+
+constexpr L9x8 l9_multiples(const L9& p) {
+  L9x8 r{};
+  for (uint32_t k = 0; k < 8; k++) r.k[k] = l9_mul_small(p, k);
+  return r;
+}
+
 template <class C>
 struct F29P {
   static constexpr L9 P = l9_from_words(C::P);
   static constexpr L9 P2 = l9_mul_small(P, 2);
+  static constexpr L9 P4 = l9_mul_small(P, 4);
+  static constexpr L9 P8 = l9_mul_small(P, 8);
   static constexpr L9 K4 = l9_redundant(l9_mul_small(P, 4));
   static constexpr uint32_t INV = l9_inv29(C::P[0]);
+  static constexpr L9 ONE = l9_pow2_mod(P, 261);     // 1 in the R = 2^261 domain
+  static constexpr L9 TO261 = l9_pow2_mod(P, 266);   // mul29(x 2^256, .) = x 2^261
+  static constexpr L9 TO256 = l9_pow2_mod(P, 256);   // mul29(x 2^261, .) = x 2^256
+  static constexpr L9x8 KP = l9_multiples(P);        // 0, p, ..., 7p
 };
 
 template <class C>
@@ -220,6 +264,53 @@ QG_HD F29<C> condsub29(const F29<C>& a, const L9& k) {
 template <class C>
 QG_HD F29<C> red2p29(const F29<C>& a) {
   return condsub29<C>(normfull29<C>(a), F29P<C>::P2);
+}
+
+// lazy value < 16p -> normalized, < 2p
+template <class C>
+QG_HD F29<C> red16p29(const F29<C>& a) {
+  F29<C> x = condsub29<C>(normfull29<C>(a), F29P<C>::P8);
+  x = condsub29<C>(x, F29P<C>::P4);
+  return condsub29<C>(x, F29P<C>::P2);
+}
+
+// lazy value < 6p -> normalized, < 2p
+template <class C>
+QG_HD F29<C> red6p29(const F29<C>& a) {
+  return condsub29<C>(condsub29<C>(normfull29<C>(a), F29P<C>::P4), F29P<C>::P2);
+}
+
+// normalized value < 8p: is it 0 mod p?  (low-limb filter, then exact check)
+template <class C>
+QG_HD bool is_zero_mod29(const F29<C>& a) {
+  bool z = false;
+#pragma unroll
+  for (int k = 0; k < 8; k++) {
+    if (a.l[0] == F29P<C>::KP.k[k].v[0]) {
+      bool eq = true;
+#pragma unroll
+      for (int i = 1; i < 9; i++) eq = eq && a.l[i] == F29P<C>::KP.k[k].v[i];
+      z = z || eq;
+    }
+  }
+  return z;
+}
+
+// a^(p-2) in the R = 2^261 domain (a in that domain, normalized < 2p)
+template <class C>
+QG_HD F29<C> inv29(const F29<C>& a) {
+  uint32_t e[8];
+  uint32_t br = 0;
+  e[0] = subb32(C::P[0], 2u, 0, &br);
+  for (int i = 1; i < 8; i++) e[i] = subb32(C::P[i], 0u, br, &br);
+  F29<C> r = F29<C>::from_l9(F29P<C>::ONE);
+  for (int i = 7; i >= 0; i--) {
+    for (int bit = 31; bit >= 0; bit--) {
+      r = mul29(r, r);
+      if ((e[i] >> bit) & 1u) r = mul29(r, a);
+    }
+  }
+  return r;
 }
 
 // normalized value < 2p -> canonical (< p)

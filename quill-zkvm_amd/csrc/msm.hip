@@ -20,6 +20,7 @@
 //    segments of L buckets; segment s contributes acc_s + lo_s * run_s; blocks
 //    tree-reduce in LDS; one final block sums block results.
 #include "common.h"
+#include "curve29.h"
 
 using namespace qg;
 
@@ -457,14 +458,17 @@ __global__ void __launch_bounds__(MSM_BLOCK)
   uint32_t e1 = e0 + (1u << elog);
   const uint32_t bend = bstart[b + 1];
   if (e1 > bend) e1 = bend;
-  G1Xyzz acc = G1Xyzz::infinity();
+  // 29-bit-limb XYZZ accumulator; table points are in the R = 2^261 domain
+  X29 acc = x29_inf();
   for (uint32_t e = e0; e < e1; e++) {
     const uint32_t ent = entries[e];
-    G1Affine p = table[ent & 0x7fffffffu];
-    if (ent >> 31) p.y = fneg(p.y);
-    acc = xyzz_add_affine(acc, p);
+    const G1Affine w = table[ent & 0x7fffffffu];
+    if (w.is_inf()) continue;
+    A29 a = a29_load(w);
+    if (ent >> 31) a.y = red2p29(sub29(Q29::zero(), a.y));
+    acc = x29_add_affine(acc, a);
   }
-  partial[t] = acc;
+  partial[t] = x29_store(acc);
   owner[t] = b;
 }
 
@@ -477,15 +481,16 @@ __global__ void k_msm_tree_step(G1Xyzz* __restrict__ partial, const uint32_t* __
   const uint32_t b = owner[t];
   const uint32_t off = t - tstart[b];
   if ((off & (2 * s - 1)) == 0 && t + s < tstart[b + 1])
-    partial[t] = xyzz_add(partial[t], partial[t + s]);
+    partial[t] = x29_store(x29_add(x29_load(partial[t]), x29_load(partial[t + s])));
 }
 
 // ---- reduction ------------------------------------------------------------
-__device__ void block_reduce_xyzz(G1Xyzz v, G1Xyzz* sh, G1Xyzz* out) {
-  sh[threadIdx.x] = v;
+__device__ void block_reduce_x29(X29 v, G1Xyzz* sh, G1Xyzz* out) {
+  sh[threadIdx.x] = x29_store(v);
   __syncthreads();
   for (unsigned s = blockDim.x / 2; s > 0; s >>= 1) {
-    if (threadIdx.x < s) sh[threadIdx.x] = xyzz_add(sh[threadIdx.x], sh[threadIdx.x + s]);
+    if (threadIdx.x < s)
+      sh[threadIdx.x] = x29_store(x29_add(x29_load(sh[threadIdx.x]), x29_load(sh[threadIdx.x + s])));
     __syncthreads();
   }
   if (threadIdx.x == 0) *out = sh[0];
@@ -497,7 +502,7 @@ __global__ void k_msm_combine(const G1Xyzz* __restrict__ partial, const uint32_t
   const uint32_t j = blockIdx.x * blockDim.x + threadIdx.x;
   if (j >= nb) return;
   const uint32_t t0 = tstart[j];
-  buckets[j] = t0 < tstart[j + 1] ? partial[t0] : G1Xyzz::infinity();
+  buckets[j] = t0 < tstart[j + 1] ? partial[t0] : x29_store(x29_inf());
 }
 
 // Segment s of MSM_SEG buckets: V_s = sum_i (lo+i+1) B_{lo+i}
@@ -508,39 +513,62 @@ __global__ void __launch_bounds__(MSM_BLOCK)
   __shared__ G1Xyzz sh[MSM_BLOCK];
   const uint32_t seg = blockIdx.x * blockDim.x + threadIdx.x;
   const uint32_t lo = seg * MSM_SEG;
-  G1Xyzz v = G1Xyzz::infinity();
+  X29 v = x29_inf();
   if (lo < nb) {
     const uint32_t hi = lo + MSM_SEG < nb ? lo + MSM_SEG : nb;
-    G1Xyzz run = buckets[hi - 1], acc = run;
+    X29 run = x29_load(buckets[hi - 1]), acc = run;
     for (uint32_t j = hi - 1; j-- > lo;) {
-      run = xyzz_add(run, buckets[j]);
-      acc = xyzz_add(acc, run);
+      run = x29_add(run, x29_load(buckets[j]));
+      acc = x29_add(acc, run);
     }
-    v = xyzz_add(acc, xyzz_mul_small(run, lo));
+    v = x29_add(acc, x29_mul_small(run, lo));
   }
-  block_reduce_xyzz(v, sh, &block_out[blockIdx.x]);
+  block_reduce_x29(v, sh, &block_out[blockIdx.x]);
 }
 
 __global__ void __launch_bounds__(MSM_BLOCK)
     k_msm_final(const G1Xyzz* __restrict__ in, uint32_t m, G1Xyzz* __restrict__ out) {
   __shared__ G1Xyzz sh[MSM_BLOCK];
-  G1Xyzz v = G1Xyzz::infinity();
-  for (uint32_t i = threadIdx.x; i < m; i += blockDim.x) v = xyzz_add(v, in[i]);
-  block_reduce_xyzz(v, sh, out);
+  X29 v = x29_inf();
+  for (uint32_t i = threadIdx.x; i < m; i += blockDim.x) v = x29_add(v, x29_load(in[i]));
+  block_reduce_x29(v, sh, out);
 }
 
-// ---- SRS construction -----------------------------------------------------
-// table[w*N + i] = 2^c * table[(w-1)*N + i]
+// R = 2^261 XYZZ words -> R = 2^256 Montgomery XYZZ (canonical) for the host
+__global__ void k_msm_export(const G1Xyzz* __restrict__ in, G1Xyzz* __restrict__ out) {
+  const X29 p = x29_load(*in);
+  if (x29_is_inf(p)) {
+    *out = G1Xyzz::infinity();
+    return;
+  }
+  *out = {q29_export(p.X), q29_export(p.Y), q29_export(p.ZZ), q29_export(p.ZZZ)};
+}
+
+// table points R = 2^256 -> R = 2^261 domain (canonical), in place
+__global__ void k_srs_to261(G1Affine* __restrict__ pts, size_t n) {
+  const size_t i = (size_t)blockIdx.x * blockDim.x + threadIdx.x;
+  if (i >= n) return;
+  const G1Affine w = pts[i];
+  if (w.is_inf()) return;
+  pts[i] = {from29(q29_import(w.x)), from29(q29_import(w.y))};
+}
+
 __global__ void k_srs_shift(G1Affine* table, size_t N, int w, int c) {
-  size_t i = (size_t)blockIdx.x * blockDim.x + threadIdx.x;
+  const size_t i = (size_t)blockIdx.x * blockDim.x + threadIdx.x;
   if (i >= N) return;
-  G1Affine a = table[(size_t)(w - 1) * N + i];
-  G1Xyzz p = G1Xyzz::from_affine(a);
-  for (int k = 0; k < c; k++) p = xyzz_dbl(p);
-  table[(size_t)w * N + i] = xyzz_to_affine(p);
+  const G1Affine a = table[(size_t)(w - 1) * N + i];
+  if (a.is_inf()) {
+    table[(size_t)w * N + i] = a;
+    return;
+  }
+  X29 p = x29_from_affine(a29_load(a));
+  for (int k = 0; k < c; k++) p = x29_dbl(p);
+  // affine: x = X / ZZ, y = Y / ZZZ with one inversion
+  const Q29 t = inv29(mul29(p.ZZ, p.ZZZ));
+  const Q29 zzinv = mul29(t, p.ZZZ), zzzinv = mul29(t, p.ZZ);
+  table[(size_t)w * N + i] = {from29(canon29(mul29(p.X, zzinv))), from29(canon29(mul29(p.Y, zzzinv)))};
 }
 
-// tau^(offset+i) for i < n, K consecutive powers per thread
 __global__ void k_powers(Fr tau, uint64_t offset, size_t n, int K, Fr* out) {
   size_t t = (size_t)blockIdx.x * blockDim.x + threadIdx.x;
   size_t i0 = t * (size_t)K;
@@ -599,8 +627,13 @@ __global__ void k_import_bases(const uint64_t* __restrict__ xy, const uint8_t* _
   out[i] = a;
 }
 
+// table 0 arrives in the arkworks R = 2^256 form; every table is kept in the
+// R = 2^261 domain of the 29-bit-limb accumulation (curve29.h)
 static void srs_build_shifts(qg_ctx* ctx, qg_srs* srs) {
   QgTimed tm(ctx, "srs_shift");
+  hipLaunchKernelGGL(k_srs_to261, dim3(div_up(srs->n, 256)), dim3(256), 0, ctx->stream,
+                     srs->d_table, srs->n);
+  QG_LAUNCH_CHECK();
   for (int w = 1; w < srs->W; w++) {
     hipLaunchKernelGGL(k_srs_shift, dim3(div_up(srs->n, 256)), dim3(256), 0, ctx->stream,
                        srs->d_table, srs->n, w, srs->c);
@@ -669,7 +702,7 @@ G1Affine msm_device(qg_ctx* ctx, const qg_srs* srs, const Fr* d_scalars, size_t 
     G1Xyzz* buckets = ctx->scratch_as<G1Xyzz>("msm_buckets", nb);
     const uint32_t nseg = div_up(nb, MSM_SEG);
     const uint32_t nred = div_up(nseg, MSM_BLOCK);
-    G1Xyzz* red = ctx->scratch_as<G1Xyzz>("msm_red", nred + 1);
+    G1Xyzz* red = ctx->scratch_as<G1Xyzz>("msm_red", nred + 2);
     QG_CHECK(ntiles <= 1024 * 64 && H <= 1024 && NL <= 4096, QG_ERR_UNSUPPORTED,
              "bucket count too large");
     QG_CHECK(max_threads < 0xffffffffull && max_chunks < 0xffffffffull, QG_ERR_UNSUPPORTED,
@@ -761,7 +794,10 @@ G1Affine msm_device(qg_ctx* ctx, const qg_srs* srs, const Fr* d_scalars, size_t 
                          red + nred);
       QG_LAUNCH_CHECK();
     }
-    QG_HIP(hipMemcpyAsync(&local, red + nred, sizeof(G1Xyzz), hipMemcpyDeviceToHost, ctx->stream));
+    hipLaunchKernelGGL(k_msm_export, dim3(1), dim3(1), 0, ctx->stream, red + nred, red + nred + 1);
+    QG_LAUNCH_CHECK();
+    QG_HIP(hipMemcpyAsync(&local, red + nred + 1, sizeof(G1Xyzz), hipMemcpyDeviceToHost,
+                          ctx->stream));
     ctx->sync();
   }
   if (ctx->world > 1) {
@@ -781,16 +817,19 @@ G1Affine msm_device(qg_ctx* ctx, const qg_srs* srs, const Fr* d_scalars, size_t 
 }
 
 // dependent Fq multiply chains: 8 independent chains per thread, ITER steps
+// Fq multiply throughput of the arithmetic the MSM runs (29-bit limbs)
 __global__ void __launch_bounds__(256) k_fq_mul_bench(Fq* io, int iters) {
   size_t i = (size_t)blockIdx.x * blockDim.x + threadIdx.x;
-  Fq a[4], b = io[i & 1023];
-  for (int k = 0; k < 4; k++) a[k] = io[(i + k + 1) & 1023];
+  Q29 a[4], b = to29(io[i & 1023]);
+  for (int k = 0; k < 4; k++) a[k] = to29(io[(i + k + 1) & 1023]);
   for (int it = 0; it < iters; it++) {
 #pragma unroll
-    for (int k = 0; k < 4; k++) a[k] = a[k] * b;
+    for (int k = 0; k < 4; k++) a[k] = mul29(a[k], b);
   }
-  Fq s = a[0] + a[1] + a[2] + a[3];
-  if (s.v[0] == 0x12345678u) io[i & 1023] = s;  // keep live
+  uint32_t s = 0;
+  for (int k = 0; k < 4; k++)
+    for (int l = 0; l < 9; l++) s ^= a[k].l[l];
+  if (s == 0x12345678u) io[i & 1023].v[0] = s;  // keep live
 }
 
 }  // namespace qg
@@ -934,7 +973,14 @@ int qg_srs_download(const qg_srs* srs, size_t offset, size_t n, uint64_t* affine
     QG_HIP(hipMemcpyAsync(h.data(), srs->d_table + offset, n * sizeof(G1Affine),
                           hipMemcpyDeviceToHost, ctx->stream));
     ctx->sync();
-    for (size_t i = 0; i < n; i++) g1_export(h[i], affine_xy + 8 * i, infinity ? infinity + i : nullptr);
+    // R = 2^261 -> arkworks R = 2^256: Montgomery multiply by 2^251 (plain)
+    Fq c = Fq::zero();
+    c.v[7] = 0x08000000u;
+    for (size_t i = 0; i < n; i++) {
+      G1Affine a = h[i];
+      if (!a.is_inf()) a = {a.x * c, a.y * c};
+      g1_export(a, affine_xy + 8 * i, infinity ? infinity + i : nullptr);
+    }
   });
 }
 
