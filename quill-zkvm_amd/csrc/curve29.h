@@ -33,13 +33,13 @@ QG_HD X29 x29_from_affine(const A29& a) {
 // mdbl-2008-s-1: 2a for an affine point
 QG_HD X29 x29_dbl_affine(const A29& a) {
   const Q29 U = normfull29(add29(a.y, a.y));  // < 4p
-  const Q29 V = mul29(U, U);
+  const Q29 V = sqr29(U);
   const Q29 W = mul29(U, V);
   const Q29 S = mul29(a.x, V);
-  const Q29 X2 = mul29(a.x, a.x);
+  const Q29 X2 = sqr29(a.x);
   const Q29 M = normfull29(add29(add29(X2, X2), X2));  // < 6p
-  const Q29 X3 = red16p29(sub29(sub29(mul29(M, M), S), S));
-  const Q29 Y3 = red6p29(sub29(mul29(M, sub29(S, X3)), mul29(W, a.y)));
+  const Q29 X3 = red16p29(sub29(sub29(sqr29(M), S), S));
+  const Q29 Y3 = red6p29(mulsub29(M, norm29(sub29(S, X3)), W, a.y));
   return {X3, Y3, V, W};
 }
 
@@ -47,13 +47,13 @@ QG_HD X29 x29_dbl_affine(const A29& a) {
 QG_HD X29 x29_dbl(const X29& p) {
   if (x29_is_inf(p)) return p;
   const Q29 U = normfull29(add29(p.Y, p.Y));
-  const Q29 V = mul29(U, U);
+  const Q29 V = sqr29(U);
   const Q29 W = mul29(U, V);
   const Q29 S = mul29(p.X, V);
-  const Q29 X2 = mul29(p.X, p.X);
+  const Q29 X2 = sqr29(p.X);
   const Q29 M = normfull29(add29(add29(X2, X2), X2));
-  const Q29 X3 = red16p29(sub29(sub29(mul29(M, M), S), S));
-  const Q29 Y3 = red6p29(sub29(mul29(M, sub29(S, X3)), mul29(W, p.Y)));
+  const Q29 X3 = red16p29(sub29(sub29(sqr29(M), S), S));
+  const Q29 Y3 = red6p29(mulsub29(M, norm29(sub29(S, X3)), W, p.Y));
   return {X3, Y3, mul29(V, p.ZZ), mul29(W, p.ZZZ)};
 }
 
@@ -68,11 +68,11 @@ QG_HD X29 x29_add_affine(const X29& p, const A29& a) {
     if (is_zero_mod29(R)) return x29_dbl_affine(a);
     return x29_inf();
   }
-  const Q29 PP = mul29(P, P);
+  const Q29 PP = sqr29(P);
   const Q29 PPP = mul29(P, PP);
   const Q29 Q = mul29(p.X, PP);
-  const Q29 X3 = red16p29(sub29(sub29(sub29(mul29(R, R), PPP), Q), Q));
-  const Q29 Y3 = red6p29(sub29(mul29(R, sub29(Q, X3)), mul29(p.Y, PPP)));
+  const Q29 X3 = red16p29(sub29(sub29(sub29(sqr29(R), PPP), Q), Q));
+  const Q29 Y3 = red6p29(mulsub29(R, norm29(sub29(Q, X3)), p.Y, PPP));
   return {X3, Y3, mul29(p.ZZ, PP), mul29(p.ZZZ, PPP)};
 }
 
@@ -90,11 +90,11 @@ QG_HD X29 x29_add(const X29& p, const X29& q) {
     if (is_zero_mod29(R)) return x29_dbl(p);
     return x29_inf();
   }
-  const Q29 PP = mul29(P, P);
+  const Q29 PP = sqr29(P);
   const Q29 PPP = mul29(P, PP);
   const Q29 Q = mul29(U1, PP);
-  const Q29 X3 = red16p29(sub29(sub29(sub29(mul29(R, R), PPP), Q), Q));
-  const Q29 Y3 = red6p29(sub29(mul29(R, sub29(Q, X3)), mul29(S1, PPP)));
+  const Q29 X3 = red16p29(sub29(sub29(sub29(sqr29(R), PPP), Q), Q));
+  const Q29 Y3 = red6p29(mulsub29(R, norm29(sub29(Q, X3)), S1, PPP));
   return {X3, Y3, mul29(mul29(p.ZZ, q.ZZ), PP), mul29(mul29(p.ZZZ, q.ZZZ), PPP)};
 }
 

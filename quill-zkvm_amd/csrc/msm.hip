@@ -74,7 +74,7 @@ QG_DEV void for_each_digit(const Fr& mont_scalar, int c, int W, Emit&& emit) {
 // group (skewed scalars, the short top window) spreads over many blocks.
 static constexpr int SORT_BLOCK = 256;
 static constexpr int SORT_TILE_MAX = 1024;                  // scalars per block (pass A)
-static constexpr size_t SORT_LDS_A = 120 * 1024;            // LDS budget for staged entries
+static constexpr size_t SORT_LDS_A = 72 * 1024;             // LDS budget for staged entries (2 blocks/CU)
 static constexpr int SORT_CHUNK = 8192;                     // entries per block (pass B)
 
 __global__ void __launch_bounds__(SORT_BLOCK)
@@ -128,23 +128,28 @@ __device__ __forceinline__ int lds_upper(const uint32_t* off, int n, uint32_t p)
   return lo;
 }
 
-// Pass A scatter: digits of the block's tile are bucketed by group in LDS,
-// then written out as contiguous per-group runs (coalesced stores).
+// Pass A scatter: digits of the block's tile are bucketed by group in LDS
+// (entry + its group id), then written out as contiguous per-group runs
+// (coalesced stores) through a per-block base table, no per-element search.
 __global__ void __launch_bounds__(SORT_BLOCK)
     k_sortA_scatter(const Fr* __restrict__ scalars, size_t n, size_t N, int c, int W, int LO, int H,
                     uint32_t nblk, uint32_t tile, const uint32_t* __restrict__ ghist,
                     const uint32_t* __restrict__ goff, unsigned long long* __restrict__ tmp) {
   extern __shared__ __attribute__((aligned(16))) unsigned char smem[];
   unsigned long long* ent = reinterpret_cast<unsigned long long*>(smem);
-  uint32_t* loff = reinterpret_cast<uint32_t*>(ent + (size_t)tile * W);
+  uint16_t* grp = reinterpret_cast<uint16_t*>(ent + (size_t)tile * W);
+  uint32_t* loff = reinterpret_cast<uint32_t*>(grp + (((size_t)tile * W + 1) & ~(size_t)1));
   uint32_t* cur = loff + H;
-  uint32_t* scr = cur + H;
+  uint32_t* gb = cur + H;
+  uint32_t* scr = gb + H;
   for (int g = threadIdx.x; g < H; g += blockDim.x) {
     loff[g] = ghist[(size_t)g * nblk + blockIdx.x];
     cur[g] = 0;
   }
   __syncthreads();
   lds_exscan(loff, H, scr);
+  for (int g = threadIdx.x; g < H; g += blockDim.x)
+    gb[g] = goff[(size_t)g * nblk + blockIdx.x] - loff[g];
   const size_t base = (size_t)blockIdx.x * tile;
   const size_t end = base + tile < n ? base + tile : n;
   for (size_t i = base + threadIdx.x; i < end; i += blockDim.x)
@@ -153,13 +158,11 @@ __global__ void __launch_bounds__(SORT_BLOCK)
       const uint32_t slot = loff[g] + atomicAdd(&cur[g], 1u);
       const uint32_t e = (uint32_t)((size_t)w * N + i) | (neg ? 0x80000000u : 0u);
       ent[slot] = ((unsigned long long)b << 32) | e;
+      grp[slot] = (uint16_t)g;
     });
   __syncthreads();
   const uint32_t total = loff[H - 1] + cur[H - 1];
-  for (uint32_t p = threadIdx.x; p < total; p += blockDim.x) {
-    const int g = lds_upper(loff, H, p);
-    tmp[goff[(size_t)g * nblk + blockIdx.x] + (p - loff[g])] = ent[p];
-  }
+  for (uint32_t p = threadIdx.x; p < total; p += blockDim.x) tmp[gb[grp[p]] + p] = ent[p];
 }
 
 // groups -> chunks (single block): gstart[g] = goff[g*nblk], chunk bases, chunk->group map
@@ -226,17 +229,18 @@ __global__ void k_sort_bucket_count(const uint32_t* __restrict__ cbase, const ui
   counts[b] = c;
 }
 
-__global__ void k_sort_chunk_offsets(const uint32_t* __restrict__ cbase, uint32_t* __restrict__ chist,
-                                     int LO, uint32_t nb, const uint32_t* __restrict__ bstart) {
+__global__ void k_sort_chunk_offsets(const uint32_t* __restrict__ cbase,
+                                     const uint32_t* __restrict__ chist, int LO, uint32_t nb,
+                                     const uint32_t* __restrict__ bstart,
+                                     uint32_t* __restrict__ coff) {
   const uint32_t b = blockIdx.x * blockDim.x + threadIdx.x;
   if (b >= nb) return;
   const uint32_t g = b >> LO, l = b & ((1u << LO) - 1);
   uint32_t run = bstart[b];
   for (uint32_t k = cbase[g]; k < cbase[g + 1]; k++) {
     const size_t idx = ((size_t)k << LO) + l;
-    const uint32_t c = chist[idx];
-    chist[idx] = run;  // histogram -> chunk output offset (in place)
-    run += c;
+    coff[idx] = run;  // chunk k's output offset for bucket b
+    run += chist[idx];
   }
 }
 
@@ -245,28 +249,28 @@ __global__ void k_sort_chunk_offsets(const uint32_t* __restrict__ cbase, uint32_
 __global__ void __launch_bounds__(SORT_BLOCK)
     k_sortB_scatter(const unsigned long long* __restrict__ tmp, const uint32_t* __restrict__ gstart,
                     const uint32_t* __restrict__ cbase, const uint32_t* __restrict__ chunk_group,
-                    const uint32_t* __restrict__ nchunks, int NL, const uint32_t* __restrict__ coff,
-                    uint32_t* __restrict__ entries) {
+                    const uint32_t* __restrict__ nchunks, int NL, const uint32_t* __restrict__ chist,
+                    const uint32_t* __restrict__ coff, uint32_t* __restrict__ entries) {
   extern __shared__ __attribute__((aligned(16))) unsigned char smem[];
   uint32_t* e32 = reinterpret_cast<uint32_t*>(smem);
   uint16_t* bins = reinterpret_cast<uint16_t*>(e32 + SORT_CHUNK);
   uint32_t* loff = reinterpret_cast<uint32_t*>(bins + SORT_CHUNK);
   uint32_t* cur = loff + NL;
-  uint32_t* scr = cur + NL;
+  uint32_t* cb = cur + NL;
+  uint32_t* scr = cb + NL;
   const uint32_t k = blockIdx.x;
   if (k >= *nchunks) return;
   const uint32_t g = chunk_group[k];
   const uint32_t s = gstart[g] + (k - cbase[g]) * SORT_CHUNK;
   const uint32_t e = min(s + SORT_CHUNK, gstart[g + 1]);
+  // the chunk's histogram was computed by k_sortB_hist (chist), so tmp is read once here
   for (int l = threadIdx.x; l < NL; l += blockDim.x) {
-    loff[l] = 0;
+    loff[l] = chist[(size_t)k * NL + l];
     cur[l] = 0;
   }
   __syncthreads();
-  for (uint32_t p = s + threadIdx.x; p < e; p += blockDim.x)
-    atomicAdd(&loff[(uint32_t)(tmp[p] >> 32) & (NL - 1)], 1u);
-  __syncthreads();
   lds_exscan(loff, NL, scr);
+  for (int l = threadIdx.x; l < NL; l += blockDim.x) cb[l] = coff[(size_t)k * NL + l] - loff[l];
   for (uint32_t p = s + threadIdx.x; p < e; p += blockDim.x) {
     const unsigned long long v = tmp[p];
     const uint32_t l = (uint32_t)(v >> 32) & (NL - 1);
@@ -275,10 +279,7 @@ __global__ void __launch_bounds__(SORT_BLOCK)
     bins[slot] = (uint16_t)l;
   }
   __syncthreads();
-  for (uint32_t q = threadIdx.x; q < e - s; q += blockDim.x) {
-    const uint32_t l = bins[q];
-    entries[coff[(size_t)k * NL + l] + (q - loff[l])] = e32[q];
-  }
+  for (uint32_t q = threadIdx.x; q < e - s; q += blockDim.x) entries[cb[bins[q]] + q] = e32[q];
 }
 
 // ---- generic exclusive scan of uint32 (out[n] = total) -------------------
@@ -458,11 +459,21 @@ __global__ void __launch_bounds__(MSM_BLOCK)
   uint32_t e1 = e0 + (1u << elog);
   const uint32_t bend = bstart[b + 1];
   if (e1 > bend) e1 = bend;
-  // 29-bit-limb XYZZ accumulator; table points are in the R = 2^261 domain
+  // 29-bit-limb XYZZ accumulator; table points are in the R = 2^261 domain.
+  // Software pipeline: the next point's random 64-B load (and the entry
+  // after it) are in flight while the current mixed addition computes.
   X29 acc = x29_inf();
+  uint32_t ent_next = entries[e0];
+  uint32_t ent_after = e0 + 1 < e1 ? entries[e0 + 1] : 0u;
+  G1Affine pt_next = table[ent_next & 0x7fffffffu];
   for (uint32_t e = e0; e < e1; e++) {
-    const uint32_t ent = entries[e];
-    const G1Affine w = table[ent & 0x7fffffffu];
+    const uint32_t ent = ent_next;
+    const G1Affine w = pt_next;
+    if (e + 1 < e1) {
+      ent_next = ent_after;
+      pt_next = table[ent_next & 0x7fffffffu];
+      if (e + 2 < e1) ent_after = entries[e + 2];
+    }
     if (w.is_inf()) continue;
     A29 a = a29_load(w);
     if (ent >> 31) a.y = red2p29(sub29(Q29::zero(), a.y));
@@ -672,7 +683,7 @@ G1Affine msm_device(qg_ctx* ctx, const qg_srs* srs, const Fr* d_scalars, size_t 
     const int H = 1 << HI, NL = 1 << LO;
     // pass-A tile: as many scalars as fit their W digits (8 B each) in LDS
     uint32_t tile = SORT_TILE_MAX;
-    while (tile > 64 && (size_t)tile * W * 8 > SORT_LDS_A) tile >>= 1;
+    while (tile > 64 && (size_t)tile * W * 10 > SORT_LDS_A) tile >>= 1;
     const uint32_t nblk = div_up(n, tile);
     const size_t nghist = (size_t)H * nblk;
     const size_t max_chunks = max_entries / SORT_CHUNK + H + 1;
@@ -684,6 +695,7 @@ G1Affine msm_device(qg_ctx* ctx, const qg_srs* srs, const Fr* d_scalars, size_t 
     uint32_t* cgroup = ctx->scratch_as<uint32_t>("msm_cgroup", max_chunks);
     uint32_t* misc = ctx->scratch_as<uint32_t>("msm_misc", 4);  // [0] nchunks, [1] max tpb
     uint32_t* chist = ctx->scratch_as<uint32_t>("msm_chist", max_chunks * NL);
+    uint32_t* coff = ctx->scratch_as<uint32_t>("msm_coff", max_chunks * NL);
     unsigned long long* tmp = ctx->scratch_as<unsigned long long>("msm_tmp", max_entries + 1);
     uint32_t* counts = ctx->scratch_as<uint32_t>("msm_counts", nb);
     uint32_t* bstart = ctx->scratch_as<uint32_t>("msm_bstart", nb + 1);
@@ -725,7 +737,8 @@ G1Affine msm_device(qg_ctx* ctx, const qg_srs* srs, const Fr* d_scalars, size_t 
       hipLaunchKernelGGL(k_scan32_add, dim3(div_up(nghist, 256)), dim3(256), 0, ctx->stream, gtiles,
                          nghist, goff);
       QG_LAUNCH_CHECK();
-      const size_t smemA = (size_t)tile * W * 8 + (2 * (size_t)H + SORT_BLOCK) * 4;
+      const size_t smemA = (size_t)tile * W * 8 + (((size_t)tile * W + 1) & ~(size_t)1) * 2 +
+                           (3 * (size_t)H + SORT_BLOCK) * 4;
       QG_CHECK(smemA <= 160 * 1024, QG_ERR_UNSUPPORTED, "pass-A tile exceeds LDS");
       static bool attr_set = false;
       if (!attr_set) {
@@ -760,11 +773,11 @@ G1Affine msm_device(qg_ctx* ctx, const qg_srs* srs, const Fr* d_scalars, size_t 
                          (size_t)nb, bstart, tstart, cursor);
       QG_LAUNCH_CHECK();
       hipLaunchKernelGGL(k_sort_chunk_offsets, dim3(div_up(nb, 256)), dim3(256), 0, ctx->stream,
-                         cbase, chist, LO, nb, bstart);
+                         cbase, chist, LO, nb, bstart, coff);
       QG_LAUNCH_CHECK();
-      const size_t smemB = (size_t)SORT_CHUNK * 6 + (2 * (size_t)NL + SORT_BLOCK) * 4;
+      const size_t smemB = (size_t)SORT_CHUNK * 6 + (3 * (size_t)NL + SORT_BLOCK) * 4;
       hipLaunchKernelGGL(k_sortB_scatter, dim3((unsigned)max_chunks), dim3(SORT_BLOCK), smemB,
-                         ctx->stream, tmp, gstart, cbase, cgroup, misc, NL, chist, entries);
+                         ctx->stream, tmp, gstart, cbase, cgroup, misc, NL, chist, coff, entries);
       QG_LAUNCH_CHECK();
     }
     {

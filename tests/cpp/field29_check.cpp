@@ -39,6 +39,8 @@ int main() {
     F29<FqP> md = mul29(norm29(d), Cc);             // (a - b) c 2^-261
     F29<FqP> r = red2p29(add29(m, Cc));             // (m + c) < 2p
     F29<FqP> lz = mul29(add29(A, B), Cc);           // lazy operand
+    F29<FqP> sq = sqr29(norm29(sub29(A, B)));       // (a - b)^2 2^-261
+    F29<FqP> ms = mulsub29(A, norm29(sub29(B, Cc)), Cc, m);  // a (b - c) - c m
     pr("a", a);
     pr("b", b);
     pr("c", c);
@@ -47,6 +49,8 @@ int main() {
     pr("r", from29(r));
     pr("cm", from29(canon29(red2p29(m))));
     pr("lz", from29(lz));
+    pr("sq", from29(sq));
+    pr("ms", from29(ms));
     printf("\n");
   }
   return 0;

@@ -51,3 +51,15 @@ def test_reduce_and_canon(rows):
 def test_lazy_operand(rows):
     for r in rows:
         assert r["lz"] % P == (r["a"] + r["b"]) * r["c"] * RINV % P
+
+
+def test_square(rows):
+    for r in rows:
+        assert r["sq"] % P == (r["a"] - r["b"]) ** 2 * RINV % P
+        assert r["sq"] < 2 * P
+
+
+def test_mulsub(rows):
+    for r in rows:
+        assert r["ms"] % P == (r["a"] * (r["b"] - r["c"]) - r["c"] * r["m"]) * RINV % P
+        assert r["ms"] < 6 * P
