@@ -39,6 +39,8 @@ def parse():
     ap.add_argument("--log-msm", type=int, default=24)
     ap.add_argument("--log-sumcheck", type=int, default=20)
     ap.add_argument("--no-sumcheck", action="store_true")
+    ap.add_argument("--log-mle", type=int, default=22,
+                    help="config C4: ML-PCS commit + open at 2^k evaluations (0: skip)")
     ap.add_argument("--no-cpu-baseline", action="store_true")
     ap.add_argument("--cpu-sample-log", type=int, default=20,
                     help="log2 size of the CPU-baseline MSM sample (a prefix of the workload)")
@@ -199,6 +201,8 @@ def main():
             tot = sum((traffic[k]["read_bytes_per_launch"] + traffic[k]["write_bytes_per_launch"])
                       * traffic[k]["launches"] for k in SC_KERNELS if k in traffic)
             out["sumcheck"]["roofline"]["traffic"] = tot
+    if args.log_mle > 0:
+        out["mle_open"] = bench_mle(q, dev, args, barrier_sync, max_over_ranks, rank, world)
     if rank == 0 and not args.no_cpu_baseline:
         out["cpu_baseline"] = cpu_baseline(args, srs, scalars)
         if not args.no_sumcheck:
@@ -246,6 +250,50 @@ def bench_sumcheck(q, dev, args, barrier_sync, max_over_ranks, rank):
                          "algorithmic_bytes": total_bytes},
             "round_kernels_ms_per_call": rk_ms / max(args.steps, 1),
             "tail_kernel_ms_per_call": tl_ms / max(args.steps, 1)}
+
+
+def bench_mle(q, dev, args, barrier_sync, max_over_ranks, rank=0, world=1):
+    """Config C4: MultilinearPCS commit + open (MLEvalProof::prove) at 2^k
+    evaluations, point drawn from the transcript after absorbing the commitment
+    (the mlpcs.rs:258-267 pattern).  With N ranks the 2^k evaluations and the SRS
+    are sharded (rank r holds [r 2^k/N, (r+1) 2^k/N)): eq/dot/quotients and all
+    six MSMs sharded, S polynomial replicated (strong scaling)."""
+    from quill_amd import KZG, Transcript
+    k = args.log_mle
+    n = 1 << k
+    L = n // world
+    kzg = KZG(dev, q.Srs.generate(dev, TAU, L, offset=rank * L), n - 1)
+    poly = q.DeviceVec(dev, L).fill_random(0x5155494C4C + 4 + 1000 * rank)
+
+    def step():
+        C = kzg.srs.msm_dev(poly)
+        t = Transcript(b"MLPCS bench")
+        t.append_g1(C)
+        point = [t.draw_field_element() for _ in range(k)]
+        return kzg.open_dev(poly, L, point, t)
+
+    for _ in range(max(1, args.warmup)):
+        step()
+    names = ("eq_table", "inner_product", "s_polynomial", "kzg_division", "msm_bucketing",
+             "msm_accumulate", "msm_reduce")
+    steps = max(1, min(args.steps, 3))
+    dev.enable_timing(True)
+    barrier_sync()
+    t0 = time.perf_counter()
+    for _ in range(steps):
+        step()
+    barrier_sync()
+    dt = max_over_ranks(time.perf_counter() - t0)
+    parts = {nm: dev.kernel_time(nm)[0] / steps for nm in names}
+    dev.enable_timing(False)
+    poly.close()
+    kzg.srs.close()
+    return {"metric": f"ML-PCS commit + open (MLEvalProof::prove) ms at 2^{k} evaluations",
+            "ms": dt / steps * 1e3, "higher_is_better": False, "msms_per_step": 6,
+            "parts_ms_rank0": parts, "steps": steps,
+            "sharding": f"2^{k} evaluations over {world} rank(s) (strong scaling); "
+                        "S polynomial replicated",
+            "note": "6 MSMs (commit, S commitment, 4 KZG quotients) dominate"}
 
 
 def _kernel_traffic(traffic, kernel):

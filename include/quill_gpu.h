@@ -165,6 +165,9 @@ typedef struct qg_mle_proof {
  * (append point, evaluation, s_comm; draw r). */
 int qg_mle_open(qg_ctx* ctx, const qg_srs* srs, const uint64_t* poly, size_t n,
                 const uint64_t* point, size_t nvars, uint8_t state[32], qg_mle_proof* out);
+/* Same, on a device-resident evaluation vector (first n entries of `poly`). */
+int qg_mle_open_dev(qg_ctx* ctx, const qg_srs* srs, const qg_buf* poly, size_t n,
+                    const uint64_t* point, size_t nvars, uint8_t state[32], qg_mle_proof* out);
 
 /* Building blocks of the opening, exposed for testing and for callers that
  * batch their own protocol:

@@ -153,9 +153,9 @@ int qg_ctx_destroy(qg_ctx* ctx) {
   if (ctx->stream) (void)hipStreamSynchronize(ctx->stream);
   comm_release(ctx);
   for (auto& kv : ctx->scratch) (void)hipFree(kv.second.first);
-  for (auto& e : ctx->pending) {
-    (void)hipEventDestroy(e.a);
-    (void)hipEventDestroy(e.b);
+  for (auto& kv : ctx->pending) {
+    (void)hipEventDestroy(kv.second.a);
+    (void)hipEventDestroy(kv.second.b);
   }
   for (auto e : ctx->event_pool) (void)hipEventDestroy(e);
   if (ctx->stream) (void)hipStreamDestroy(ctx->stream);

@@ -52,8 +52,10 @@ struct qg_ctx {
   struct Ev {
     std::string name;
     hipEvent_t a, b;
+    bool ended;
   };
-  std::vector<Ev> pending;
+  std::map<int, Ev> pending;  // handle -> region (stable across nested syncs)
+  int next_handle = 0;
   std::map<std::string, std::pair<double, uint32_t>> ktime;
   std::vector<hipEvent_t> event_pool;
   // small per-context memo (e.g. which program image the device copy holds)
@@ -99,27 +101,34 @@ struct qg_ctx {
   // begin/end a timed region on the context stream
   int tbegin(const char* name) {
     if (!timing) return -1;
-    Ev e{name, ev_get(), ev_get()};
+    Ev e{name, ev_get(), ev_get(), false};
     QG_HIP(hipEventRecord(e.a, stream));
-    pending.push_back(e);
-    return (int)pending.size() - 1;
+    const int h = next_handle++;
+    pending[h] = e;
+    return h;
   }
   void tend(int h) noexcept {
-    if (h < 0) return;
-    (void)hipEventRecord(pending[h].b, stream);
+    auto it = pending.find(h);
+    if (h < 0 || it == pending.end()) return;
+    (void)hipEventRecord(it->second.b, stream);
+    it->second.ended = true;
   }
-  // resolve pending events (after a stream sync)
+  // resolve the closed regions (after a stream sync); open ones stay pending
   void tresolve() {
-    for (auto& e : pending) {
+    for (auto it = pending.begin(); it != pending.end();) {
+      if (!it->second.ended) {
+        ++it;
+        continue;
+      }
       float ms = 0.f;
-      QG_HIP(hipEventElapsedTime(&ms, e.a, e.b));
-      auto& slot = ktime[e.name];
+      QG_HIP(hipEventElapsedTime(&ms, it->second.a, it->second.b));
+      auto& slot = ktime[it->second.name];
       slot.first += ms;
       slot.second += 1;
-      event_pool.push_back(e.a);
-      event_pool.push_back(e.b);
+      event_pool.push_back(it->second.a);
+      event_pool.push_back(it->second.b);
+      it = pending.erase(it);
     }
-    pending.clear();
   }
   void sync() {
     QG_HIP(hipStreamSynchronize(stream));

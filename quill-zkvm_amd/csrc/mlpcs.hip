@@ -316,10 +316,20 @@ static void s_poly_device(qg_ctx* ctx, const Fr* f, size_t nf, const Fr* g, size
   QG_LAUNCH_CHECK();
 }
 
-__global__ void k_last_nonzero(const Fr* __restrict__ a, size_t n, unsigned long long* out) {
-  size_t i = (size_t)blockIdx.x * blockDim.x + threadIdx.x;
-  if (i >= n) return;
-  if (!a[i].is_zero()) atomicMax(out, (unsigned long long)(i + 1));
+// highest nonzero index + 1: per-thread max over a grid-stride range, wave max
+// by shuffles, one atomic per wave (a contended atomic per element cost 0.75 ms
+// at 2^22)
+__global__ void __launch_bounds__(256)
+    k_last_nonzero(const Fr* __restrict__ a, size_t n, unsigned long long* out) {
+  unsigned long long m = 0;
+  for (size_t i = (size_t)blockIdx.x * blockDim.x + threadIdx.x; i < n;
+       i += (size_t)gridDim.x * blockDim.x)
+    if (!a[i].is_zero()) m = i + 1;
+  for (int k = 32; k > 0; k >>= 1) {
+    const unsigned long long o = __shfl_xor(m, k, 64);
+    m = o > m ? o : m;
+  }
+  if ((threadIdx.x & 63) == 0 && m) atomicMax(out, m);
 }
 
 // trimmed length of a device vector
@@ -327,7 +337,8 @@ static size_t trimmed_len(qg_ctx* ctx, const Fr* a, size_t n) {
   if (n == 0) return 0;
   unsigned long long* d = ctx->scratch_as<unsigned long long>("trim_len", 1);
   QG_HIP(hipMemsetAsync(d, 0, sizeof(unsigned long long), ctx->stream));
-  hipLaunchKernelGGL(k_last_nonzero, dim3(div_up(n, 256)), dim3(256), 0, ctx->stream, a, n, d);
+  const unsigned blocks = (unsigned)std::min<size_t>(2048, div_up(n, 256));
+  hipLaunchKernelGGL(k_last_nonzero, dim3(blocks), dim3(256), 0, ctx->stream, a, n, d);
   QG_LAUNCH_CHECK();
   unsigned long long h = 0;
   QG_HIP(hipMemcpyAsync(&h, d, sizeof(h), hipMemcpyDeviceToHost, ctx->stream));
@@ -356,6 +367,186 @@ static void kzg_open_device(qg_ctx* ctx, const qg_srs* srs, const Fr* c, size_t 
   }
   fr_export(y, out->y);
   g1_export(pi, out->proof_xy, &out->proof_inf);
+}
+
+// ---------------------------------------------------------------- sharded opening
+// Ranks hold contiguous slices [off, off + L) of a global coefficient vector.
+// Suffix-Horner is linear in its carry: the global s_i on a slice equals the
+// local scan plus x^(le - i) C, C = global s at the slice end.  C comes from
+// one allgather of the per-rank local values T_r = s_local[0].
+
+// s_i += x^(le - i) C for i < le; s_le = C   (pw[k] = x^k)
+__global__ void k_sh_carry(Fr* __restrict__ s, size_t le, const Fr* __restrict__ pw, Fr C) {
+  const size_t i = (size_t)blockIdx.x * blockDim.x + threadIdx.x;
+  if (i < le) s[i] = s[i] + pw[le - i] * C;
+  if (i == le) s[i] = C;
+}
+
+// small host values gathered over the communicator (rank order)
+static void allgather_host(qg_ctx* ctx, const void* src, size_t bytes, void* dst_all) {
+  uint8_t* ds = ctx->scratch_as<uint8_t>("ag_send", bytes);
+  uint8_t* dr = ctx->scratch_as<uint8_t>("ag_recv", bytes * (size_t)ctx->world);
+  QG_HIP(hipMemcpyAsync(ds, src, bytes, hipMemcpyHostToDevice, ctx->stream));
+  comm_allgather_bytes(ctx, ds, dr, bytes);
+  QG_HIP(hipMemcpyAsync(dst_all, dr, bytes * (size_t)ctx->world, hipMemcpyDeviceToHost,
+                        ctx->stream));
+  ctx->sync();
+}
+
+// global trimmed length of a vector sliced as [rank * L, rank * L + nloc)
+static size_t trimmed_len_global(qg_ctx* ctx, const Fr* a, size_t nloc, size_t L) {
+  const uint64_t loc = nloc ? trimmed_len(ctx, a, nloc) : 0;
+  const uint64_t mine = loc ? (uint64_t)ctx->rank * L + loc : 0;
+  std::vector<uint64_t> all(ctx->world);
+  allgather_host(ctx, &mine, sizeof mine, all.data());
+  uint64_t m = 0;
+  for (uint64_t v : all) m = v > m ? v : m;
+  return (size_t)m;
+}
+
+// KZG::open of a sharded polynomial (global trimmed length Lt, slices of L):
+// every rank gets the same opening; the quotient MSM is sharded.
+static void kzg_open_sharded(qg_ctx* ctx, const qg_srs* srs, const Fr* c, size_t L, size_t Lt,
+                             const Fr& x, qg_kzg_opening* out) {
+  const int world = ctx->world, rank = ctx->rank;
+  const size_t off = (size_t)rank * L;
+  const size_t le = Lt > off ? std::min(L, Lt - off) : 0;  // this rank's live coefficients
+  fr_export(x, out->x);
+  Fr* s = ctx->scratch_as<Fr>("open_s", le + 1);
+  Fr T = Fr::zero();
+  if (le > 0) {
+    QgTimed tm(ctx, "kzg_division");
+    suffix_horner(ctx, c, le, x, s);
+    QG_HIP(hipMemcpyAsync(&T, s, sizeof(Fr), hipMemcpyDeviceToHost, ctx->stream));
+    ctx->sync();
+  }
+  std::vector<Fr> Ts(world);
+  allgather_host(ctx, &T, sizeof(Fr), Ts.data());
+  // C_r = sum_{r' > r} T_r' x^((r' - r - 1) L);  y = sum_r T_r x^(r L)
+  const Fr xL = fpow_small(x, L);
+  Fr C = Fr::zero(), y = Fr::zero();
+  for (int r = world - 1; r >= 0; r--) {
+    if (r == rank) C = y;  // y accumulated over r' > rank so far, in powers of x^L
+    y = Ts[r] + xL * y;
+  }
+  if (le > 0) {
+    QgTimed tm(ctx, "kzg_division");
+    Fr* pw = ctx->scratch_as<Fr>("open_pw", le + 1);
+    const int K = 64;
+    hipLaunchKernelGGL(k_powers_ml, dim3(div_up(div_up(le + 1, (size_t)K), ML_BLOCK)), dim3(ML_BLOCK),
+                       0, ctx->stream, x, le + 1, K, pw);
+    QG_LAUNCH_CHECK();
+    hipLaunchKernelGGL(k_sh_carry, dim3(div_up(le + 1, ML_BLOCK)), dim3(ML_BLOCK), 0, ctx->stream,
+                       s, le, pw, C);
+    QG_LAUNCH_CHECK();
+  }
+  // q_i = s_{i+1} for global i < Lt - 1; this rank's part starts at s + 1
+  const size_t qn = (Lt > 0 && Lt - 1 > off) ? std::min(le, Lt - 1 - off) : 0;
+  QG_CHECK(qn <= srs->n, QG_ERR_INVALID, "Polynomial degree exceeds max degree");
+  const G1Affine pi = msm_device(ctx, srs, s + 1, qn);
+  fr_export(y, out->y);
+  g1_export(pi, out->proof_xy, &out->proof_inf);
+}
+
+// MLEvalProof::prove with a communicator: this rank holds poly[rank L, (rank+1) L)
+// of the 2^nvars evaluations (L = 2^nvars / world) and the matching SRS shard.
+// eq table and the dot product per slice; the S polynomial needs whole vectors
+// (a correlation), so the slices are allgathered and S is computed on every
+// rank; its commitment and all four quotient commitments are sharded MSMs.
+static void mle_open_sharded(qg_ctx* ctx, const qg_srs* srs, const Fr* dpoly, size_t L,
+                             const uint64_t* point, size_t nvars, uint8_t state[32],
+                             qg_mle_proof* out) {
+  const size_t N = (size_t)1 << nvars;
+  QG_CHECK(L * (size_t)ctx->world == N, QG_ERR_UNSUPPORTED,
+           "sharded opening needs world * local length == 2^nvars");
+  const size_t off = (size_t)ctx->rank * L;
+  Fr* dz = ctx->scratch_as<Fr>("mle_z", nvars ? nvars : 1);
+  Fr* dpr = ctx->scratch_as<Fr>("mle_pr", N);
+  Fr* dfull = ctx->scratch_as<Fr>("mle_full", N);
+  fr_upload(ctx, dz, point, nvars);
+  eq_table_device(ctx, dz, (uint32_t)nvars, dpr);
+  // evaluation: local dot over the slice, summed over ranks
+  const Fr part = dot_device(ctx, dpoly, dpr + off, L);
+  std::vector<Fr> parts(ctx->world);
+  allgather_host(ctx, &part, sizeof(Fr), parts.data());
+  Fr evaluation = Fr::zero();
+  for (const Fr& v : parts) evaluation = evaluation + v;
+  // S on every rank from the gathered vector
+  comm_allgather_bytes(ctx, dpoly, dfull, L * sizeof(Fr));
+  Fr* dS = ctx->scratch_as<Fr>("mle_S", N > 1 ? N - 1 : 1);
+  size_t Slen = 0;
+  if (N > 1) {
+    s_poly_device(ctx, dfull, N, dpr, N, dS);
+    Slen = trimmed_len(ctx, dS, N - 1);
+  }
+  const size_t sloc = Slen > off ? std::min(L, Slen - off) : 0;
+  QG_CHECK(sloc <= srs->n, QG_ERR_INVALID, "Polynomial degree exceeds max degree");
+  G1Affine s_comm = msm_device(ctx, srs, dS + off, sloc);
+  // transcript: point (Vec<Fr>), evaluation, s_comm; draw r (mlpcs.rs:100-107)
+  std::vector<uint8_t> msg(8 + 32 * nvars);
+  u64_to_bytes(nvars, msg.data());
+  for (size_t i = 0; i < nvars; i++) fr_to_bytes(fr_import(point + 4 * i), msg.data() + 8 + 32 * i);
+  transcript_append(state, msg.data(), msg.size());
+  uint8_t b32[32], b64[64];
+  fr_to_bytes(evaluation, b32);
+  transcript_append(state, b32, 32);
+  g1_serialize(s_comm, b64);
+  transcript_append(state, b64, 64);
+  Fr r = transcript_draw_fr(state);
+  QG_CHECK(!r.is_zero(), QG_ERR_ASSERT, "challenge r = 0");
+  Fr r_inv = finv(r);
+  fr_export(evaluation, out->evaluation);
+  g1_export(s_comm, out->s_comm_xy, &out->s_comm_inf);
+  const size_t Lt = trimmed_len_global(ctx, dpoly, L, L);
+  kzg_open_sharded(ctx, srs, dpoly, L, Lt, r, &out->poly_opening);
+  kzg_open_sharded(ctx, srs, dpoly, L, Lt, r_inv, &out->poly_opening_inv);
+  kzg_open_sharded(ctx, srs, dS + off, L, Slen, r, &out->s_opening);
+  kzg_open_sharded(ctx, srs, dS + off, L, Slen, r_inv, &out->s_opening_inv);
+}
+
+// MLEvalProof::prove (mlpcs.rs:83-124) on a device-resident evaluation vector
+static void mle_open_device(qg_ctx* ctx, const qg_srs* srs, const Fr* dpoly, size_t n,
+                            const uint64_t* point, size_t nvars, uint8_t state[32],
+                            qg_mle_proof* out) {
+  if (ctx->world > 1) return mle_open_sharded(ctx, srs, dpoly, n, point, nvars, state, out);
+  const size_t N = (size_t)1 << nvars;
+  Fr* dz = ctx->scratch_as<Fr>("mle_z", nvars ? nvars : 1);
+  Fr* dpr = ctx->scratch_as<Fr>("mle_pr", N);
+  fr_upload(ctx, dz, point, nvars);
+  // P_r coefficients = eq table (mlpcs.rs:68-78)
+  eq_table_device(ctx, dz, (uint32_t)nvars, dpr);
+  // evaluation = <poly, P_r> over the common prefix (mlpcs.rs:91-94)
+  Fr evaluation = dot_device(ctx, dpoly, dpr, n < N ? n : N);
+  // S polynomial and its commitment (mlpcs.rs:95-97)
+  const size_t M = n > N ? n : N;
+  Fr* dS = ctx->scratch_as<Fr>("mle_S", M > 1 ? M - 1 : 1);
+  size_t Slen = 0;
+  if (M > 1) {
+    s_poly_device(ctx, dpoly, n, dpr, N, dS);
+    Slen = trimmed_len(ctx, dS, M - 1);
+  }
+  QG_CHECK(Slen <= srs->n, QG_ERR_INVALID, "Polynomial degree exceeds max degree");
+  G1Affine s_comm = msm_device(ctx, srs, dS, Slen);
+  // transcript: point (Vec<Fr>), evaluation, s_comm; draw r (mlpcs.rs:100-107)
+  std::vector<uint8_t> msg(8 + 32 * nvars);
+  u64_to_bytes(nvars, msg.data());
+  for (size_t i = 0; i < nvars; i++) fr_to_bytes(fr_import(point + 4 * i), msg.data() + 8 + 32 * i);
+  transcript_append(state, msg.data(), msg.size());
+  uint8_t b32[32], b64[64];
+  fr_to_bytes(evaluation, b32);
+  transcript_append(state, b32, 32);
+  g1_serialize(s_comm, b64);
+  transcript_append(state, b64, 64);
+  Fr r = transcript_draw_fr(state);
+  QG_CHECK(!r.is_zero(), QG_ERR_ASSERT, "challenge r = 0");
+  Fr r_inv = finv(r);
+  fr_export(evaluation, out->evaluation);
+  g1_export(s_comm, out->s_comm_xy, &out->s_comm_inf);
+  // four KZG openings (mlpcs.rs:108-113)
+  kzg_open_device(ctx, srs, dpoly, n, r, &out->poly_opening);
+  kzg_open_device(ctx, srs, dpoly, n, r_inv, &out->poly_opening_inv);
+  kzg_open_device(ctx, srs, dS, Slen, r, &out->s_opening);
+  kzg_open_device(ctx, srs, dS, Slen, r_inv, &out->s_opening_inv);
 }
 
 }  // namespace qg
@@ -411,46 +602,20 @@ int qg_mle_open(qg_ctx* ctx, const qg_srs* srs, const uint64_t* poly, size_t n,
   return qg_guard(ctx, [&] {
     QG_CHECK(nvars <= 30, QG_ERR_INVALID, "too many variables");
     QG_HIP(hipSetDevice(ctx->device));
-    const size_t N = (size_t)1 << nvars;
     Fr* dpoly = ctx->scratch_as<Fr>("mle_poly", n ? n : 1);
-    Fr* dz = ctx->scratch_as<Fr>("mle_z", nvars ? nvars : 1);
-    Fr* dpr = ctx->scratch_as<Fr>("mle_pr", N);
     fr_upload(ctx, dpoly, poly, n);
-    fr_upload(ctx, dz, point, nvars);
-    // P_r coefficients = eq table (mlpcs.rs:68-78)
-    eq_table_device(ctx, dz, (uint32_t)nvars, dpr);
-    // evaluation = <poly, P_r> over the common prefix (mlpcs.rs:91-94)
-    Fr evaluation = dot_device(ctx, dpoly, dpr, n < N ? n : N);
-    // S polynomial and its commitment (mlpcs.rs:95-97)
-    const size_t M = n > N ? n : N;
-    Fr* dS = ctx->scratch_as<Fr>("mle_S", M > 1 ? M - 1 : 1);
-    size_t Slen = 0;
-    if (M > 1) {
-      s_poly_device(ctx, dpoly, n, dpr, N, dS);
-      Slen = trimmed_len(ctx, dS, M - 1);
-    }
-    QG_CHECK(Slen <= srs->n, QG_ERR_INVALID, "Polynomial degree exceeds max degree");
-    G1Affine s_comm = msm_device(ctx, srs, dS, Slen);
-    // transcript: point (Vec<Fr>), evaluation, s_comm; draw r (mlpcs.rs:100-107)
-    std::vector<uint8_t> msg(8 + 32 * nvars);
-    u64_to_bytes(nvars, msg.data());
-    for (size_t i = 0; i < nvars; i++) fr_to_bytes(fr_import(point + 4 * i), msg.data() + 8 + 32 * i);
-    transcript_append(state, msg.data(), msg.size());
-    uint8_t b32[32], b64[64];
-    fr_to_bytes(evaluation, b32);
-    transcript_append(state, b32, 32);
-    g1_serialize(s_comm, b64);
-    transcript_append(state, b64, 64);
-    Fr r = transcript_draw_fr(state);
-    QG_CHECK(!r.is_zero(), QG_ERR_ASSERT, "challenge r = 0");
-    Fr r_inv = finv(r);
-    fr_export(evaluation, out->evaluation);
-    g1_export(s_comm, out->s_comm_xy, &out->s_comm_inf);
-    // four KZG openings (mlpcs.rs:108-113)
-    kzg_open_device(ctx, srs, dpoly, n, r, &out->poly_opening);
-    kzg_open_device(ctx, srs, dpoly, n, r_inv, &out->poly_opening_inv);
-    kzg_open_device(ctx, srs, dS, Slen, r, &out->s_opening);
-    kzg_open_device(ctx, srs, dS, Slen, r_inv, &out->s_opening_inv);
+    mle_open_device(ctx, srs, dpoly, n, point, nvars, state, out);
+  });
+}
+
+int qg_mle_open_dev(qg_ctx* ctx, const qg_srs* srs, const qg_buf* poly, size_t n,
+                    const uint64_t* point, size_t nvars, uint8_t state[32], qg_mle_proof* out) {
+  if (!ctx || !srs || !poly || n > poly->n || (!point && nvars) || !state || !out)
+    return QG_ERR_INVALID;
+  return qg_guard(ctx, [&] {
+    QG_CHECK(nvars <= 30, QG_ERR_INVALID, "too many variables");
+    QG_HIP(hipSetDevice(ctx->device));
+    mle_open_device(ctx, srs, poly->d, n, point, nvars, state, out);
   });
 }
 

@@ -27,6 +27,7 @@ using namespace qg;
 namespace qg {
 
 static constexpr int MSM_SEG = 8;       // buckets per reduction segment
+static constexpr int MSM_COMBINE_SEQ = 8;  // group sums a bucket's combine adds sequentially
 static constexpr int MSM_BLOCK = 256;
 
 // window size for an SRS of n bases (tuned later)
@@ -507,13 +508,24 @@ __device__ void block_reduce_x29(X29 v, G1Xyzz* sh, G1Xyzz* out) {
   if (threadIdx.x == 0) *out = sh[0];
 }
 
-// B_j = bucket j's tree-combined partial (empty bucket -> infinity)
+// B_j = sum of bucket j's group sums at offsets 0, step, 2 step, ... (empty
+// bucket -> infinity); at most MSM_COMBINE_SEQ of them
 __global__ void k_msm_combine(const G1Xyzz* __restrict__ partial, const uint32_t* __restrict__ tstart,
-                              uint32_t nb, G1Xyzz* __restrict__ buckets) {
+                              uint32_t nb, uint32_t step, G1Xyzz* __restrict__ buckets) {
   const uint32_t j = blockIdx.x * blockDim.x + threadIdx.x;
   if (j >= nb) return;
-  const uint32_t t0 = tstart[j];
-  buckets[j] = t0 < tstart[j + 1] ? partial[t0] : x29_store(x29_inf());
+  const uint32_t t0 = tstart[j], t1 = tstart[j + 1];
+  if (t0 == t1) {
+    buckets[j] = x29_store(x29_inf());
+    return;
+  }
+  if (t1 - t0 <= step) {
+    buckets[j] = partial[t0];
+    return;
+  }
+  X29 acc = x29_load(partial[t0]);
+  for (uint32_t t = t0 + step; t < t1; t += step) acc = x29_add(acc, x29_load(partial[t]));
+  buckets[j] = x29_store(acc);
 }
 
 // Segment s of MSM_SEG buckets: V_s = sum_i (lo+i+1) B_{lo+i}
@@ -792,13 +804,18 @@ G1Affine msm_device(qg_ctx* ctx, const qg_srs* srs, const Fr* d_scalars, size_t 
     QG_HIP(hipStreamSynchronize(ctx->stream));
     {
       QgTimed tm(ctx, "msm_reduce");
-      for (uint32_t st = 1; st < max_tpb; st <<= 1) {
+      // tree steps only until every bucket has <= MSM_COMBINE_SEQ group sums
+      // left; the combine kernel adds those sequentially (one launch instead
+      // of log2(max partials) full-grid steps for typical, unskewed scalars)
+      uint32_t st = 1;
+      while ((size_t)st * MSM_COMBINE_SEQ < max_tpb) {
         hipLaunchKernelGGL(k_msm_tree_step, dim3(div_up(max_threads, MSM_BLOCK)), dim3(MSM_BLOCK),
                            0, ctx->stream, partial, owner, tstart, nb, st);
         QG_LAUNCH_CHECK();
+        st <<= 1;
       }
       hipLaunchKernelGGL(k_msm_combine, dim3(div_up(nb, MSM_BLOCK)), dim3(MSM_BLOCK), 0,
-                         ctx->stream, partial, tstart, nb, buckets);
+                         ctx->stream, partial, tstart, nb, st, buckets);
       QG_LAUNCH_CHECK();
       hipLaunchKernelGGL(k_msm_reduce, dim3(nred), dim3(MSM_BLOCK), 0, ctx->stream, buckets, nb,
                          red);

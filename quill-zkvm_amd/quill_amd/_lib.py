@@ -85,6 +85,7 @@ PROTOTYPES = {
     "qg_kzg_commit": (C.c_int, [P, P, U64P, SZ, U64P, U8P]),
     "qg_kzg_open": (C.c_int, [P, P, U64P, SZ, U64P, C.POINTER(KzgOpening)]),
     "qg_mle_open": (C.c_int, [P, P, U64P, SZ, U64P, SZ, U8P, C.POINTER(MleProof)]),
+    "qg_mle_open_dev": (C.c_int, [P, P, P, SZ, U64P, SZ, U8P, C.POINTER(MleProof)]),
     "qg_eq_table": (C.c_int, [P, U64P, SZ, U64P]),
     "qg_s_polynomial": (C.c_int, [P, U64P, SZ, U64P, SZ, U64P]),
     "qg_inner_product": (C.c_int, [P, U64P, SZ, U64P, SZ, U64P]),

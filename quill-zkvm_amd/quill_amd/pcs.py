@@ -100,6 +100,17 @@ class KZG:
         return _opening(out)
 
     # MultilinearPCS::open == MLEvalProof::prove (mlpcs.rs:83-124, 191-198)
+    def open_dev(self, vec, n, eval_point, transcript: Transcript) -> MLEvalProof:
+        """open() on the first n entries of a device-resident DeviceVec"""
+        pt = fr_array(eval_point) if len(eval_point) else np.zeros((1, 4), dtype=np.uint64)
+        out = MleProof()
+        check(lib().qg_mle_open_dev(self.dev.h, self.srs.h, vec.h, n, u64p(pt), len(eval_point),
+                                    transcript.c_state(), C.byref(out)), self.dev.h)
+        return MLEvalProof(list(eval_point), fr_from_mont_limbs(list(out.evaluation)),
+                           g1_from_abi(out.s_comm_xy, out.s_comm_inf),
+                           _opening(out.poly_opening), _opening(out.poly_opening_inv),
+                           _opening(out.s_opening), _opening(out.s_opening_inv))
+
     def open(self, poly, eval_point, transcript: Transcript) -> MLEvalProof:
         arr = fr_array(poly) if len(poly) else np.zeros((1, 4), dtype=np.uint64)
         pt = fr_array(eval_point) if len(eval_point) else np.zeros((1, 4), dtype=np.uint64)

@@ -110,3 +110,37 @@ def test_sharded_zerocheck(world):
         return rp, pt, ev, t.state
     for rp, pt, ev, s in run_ranks(world, fn):
         assert rp == zp.sumcheck_proof.r_polys and pt == opt and ev == oev and s == ot.state
+
+
+@pytest.mark.parametrize("world,tail_zeros", [(2, 0), (4, 0), (4, 131), (2, 1)])
+def test_sharded_mle_open(world, tail_zeros):
+    """MLEvalProof::prove with the evaluations and the SRS sharded over ranks
+    equals the single-context proof (and transcript state)."""
+    import quill_amd as q
+    from quill_amd import KZG, Transcript
+    rnd = random.Random(40 + world)
+    nv = 9
+    N = 1 << nv
+    L = N // world
+    tau = rnd.randrange(R)
+    poly = [rnd.randrange(R) for _ in range(N)]
+    for i in range(tail_zeros):  # trimmed length ends inside a lower rank's slice
+        poly[N - 1 - i] = 0
+    point = [rnd.randrange(R) for _ in range(nv)]
+    dev0 = q.Device(0)
+    ref_kzg = KZG.trusted_setup(N, tau, dev0)
+    t_ref = Transcript(b"shard-open")
+    ref = ref_kzg.open(poly, point, t_ref)
+    ref_kzg.srs.close()
+    dev0.close()
+
+    def fn(dev, rank, world):
+        kzg = KZG(dev, q.Srs.generate(dev, tau, L, offset=rank * L), N - 1)
+        vec = q.DeviceVec.from_list(dev, poly[rank * L:(rank + 1) * L])
+        t = Transcript(b"shard-open")
+        pr = kzg.open_dev(vec, L, point, t)
+        vec.close()
+        kzg.srs.close()
+        return pr, t.state
+    for pr, st in run_ranks(world, fn):
+        assert pr == ref and st == t_ref.state

@@ -333,3 +333,19 @@ def test_sumcheck_2p16_property(dev):
     assert vpt == claim.point and vev == claim.evaluation and vt.state == t.state
     g_at = [o.mle_evaluate(tb, vpt) for tb in tabs]
     assert g_at[0] * g_at[1] % R * g_at[2] % R == vev
+
+
+def test_mle_open_dev_matches_host_entry(dev):
+    """qg_mle_open_dev on a device vector == qg_mle_open on the same host values."""
+    from quill_amd import KZG, DeviceVec, Transcript
+    rnd = random.Random(33)
+    nv = 10
+    n = (1 << nv) - 3  # a prefix shorter than the hypercube
+    kzg = KZG.trusted_setup(1 << nv, rnd.randrange(R), dev)
+    vec = DeviceVec(dev, 1 << nv).fill_random(99)
+    poly = vec.to_list(n)
+    point = [rnd.randrange(R) for _ in range(nv)]
+    t1, t2 = Transcript(b"dev"), Transcript(b"dev")
+    p1 = kzg.open(poly, point, t1)
+    p2 = kzg.open_dev(vec, n, point, t2)
+    assert p1 == p2 and t1.state == t2.state
