@@ -76,6 +76,35 @@ QG_HD X29 x29_add_affine(const X29& p, const A29& a) {
   return {X3, Y3, mul29(p.ZZ, PP), mul29(p.ZZZ, PPP)};
 }
 
+// madd-2008-s for a bucket accumulator kept lazily reduced between additions:
+// X normalized < 16p, Y normalized < 8p, ZZ/ZZZ < 2p (x29_acc_finish brings
+// it back to < 2p before it is stored).  Saves the X3/Y3 conditional
+// subtractions of every addition.
+QG_HD X29 x29_acc_madd(const X29& p, const A29& a) {
+  if (x29_is_inf(p)) return x29_from_affine(a);
+  const Q29 U2 = mul29(a.x, p.ZZ);
+  const Q29 S2 = mul29(a.y, p.ZZZ);
+  const Q29 P = normfull29(subk29(U2, p.X, F29P<FqP>::K17));  // (p, 19p)
+  const Q29 R = normfull29(subk29(S2, p.Y, F29P<FqP>::K9));   // (p, 11p)
+  if (is_zero_mod29_20(P)) {
+    if (is_zero_mod29_20(R)) return x29_dbl_affine(a);
+    return x29_inf();
+  }
+  const Q29 PP = sqr29(P);                 // < 3p
+  const Q29 PPP = mul29(P, PP);            // < 2p
+  const Q29 Q = mul29(p.X, PP);            // < 2p
+  const Q29 X3 = normfull29(sub29(sub29(sub29(sqr29(R), PPP), Q), Q));  // < 16p
+  const Q29 Y3 = normfull29(mulsub29(R, norm29(subk29(Q, X3, F29P<FqP>::K17)), p.Y, PPP));  // < 8p
+  return {X3, Y3, mul29(p.ZZ, PP), mul29(p.ZZZ, PPP)};
+}
+
+// lazily reduced accumulator -> every coordinate < 2p
+QG_HD X29 x29_acc_finish(const X29& p) {
+  if (x29_is_inf(p)) return p;
+  return {red16p29(p.X), condsub29<FqP>(condsub29<FqP>(p.Y, F29P<FqP>::P4), F29P<FqP>::P2), p.ZZ,
+          p.ZZZ};
+}
+
 // add-2008-s: p + q
 QG_HD X29 x29_add(const X29& p, const X29& q) {
   if (x29_is_inf(p)) return q;

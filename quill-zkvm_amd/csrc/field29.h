@@ -105,6 +105,16 @@ constexpr L9x8 l9_multiples(const L9& p) {
   return r;
 }
 
+struct L9x20 {
+  L9 k[20];
+};
+
+constexpr L9x20 l9_multiples20(const L9& p) {
+  L9x20 r{};
+  for (uint32_t k = 0; k < 20; k++) r.k[k] = l9_mul_small(p, k);
+  return r;
+}
+
 template <class C>
 struct F29P {
   static constexpr L9 P = l9_from_words(C::P);
@@ -117,6 +127,9 @@ struct F29P {
   static constexpr L9 TO261 = l9_pow2_mod(P, 266);   // mul29(x 2^256, .) = x 2^261
   static constexpr L9 TO256 = l9_pow2_mod(P, 256);   // mul29(x 2^261, .) = x 2^256
   static constexpr L9x8 KP = l9_multiples(P);        // 0, p, ..., 7p
+  static constexpr L9x20 KP20 = l9_multiples20(P);   // 0, p, ..., 19p
+  static constexpr L9 K9 = l9_redundant(l9_mul_small(P, 9));    // subtrahends < 8p
+  static constexpr L9 K17 = l9_redundant(l9_mul_small(P, 17));  // subtrahends < 16p
 };
 
 template <class C>
@@ -281,6 +294,15 @@ QG_HD F29<C> sub29(const F29<C>& a, const F29<C>& b) {
   return r;
 }
 
+// a + k - b with a redundant multiple k of p (subtrahend value below k - p)
+template <class C>
+QG_HD F29<C> subk29(const F29<C>& a, const F29<C>& b, const L9& k) {
+  F29<C> r;
+#pragma unroll
+  for (int i = 0; i < 9; i++) r.l[i] = a.l[i] + (k.v[i] - b.l[i]);
+  return r;
+}
+
 // one parallel carry pass: limbs < 2^32 -> almost-normalized (< 2^29 + 8)
 template <class C>
 QG_HD F29<C> norm29(const F29<C>& a) {
@@ -355,6 +377,22 @@ QG_HD bool is_zero_mod29(const F29<C>& a) {
       bool eq = true;
 #pragma unroll
       for (int i = 1; i < 9; i++) eq = eq && a.l[i] == F29P<C>::KP.k[k].v[i];
+      z = z || eq;
+    }
+  }
+  return z;
+}
+
+// normalized value < 20p: is it 0 mod p?
+template <class C>
+QG_HD bool is_zero_mod29_20(const F29<C>& a) {
+  bool z = false;
+#pragma unroll
+  for (int k = 0; k < 20; k++) {
+    if (a.l[0] == F29P<C>::KP20.k[k].v[0]) {
+      bool eq = true;
+#pragma unroll
+      for (int i = 1; i < 9; i++) eq = eq && a.l[i] == F29P<C>::KP20.k[k].v[i];
       z = z || eq;
     }
   }

@@ -460,27 +460,18 @@ __global__ void __launch_bounds__(MSM_BLOCK)
   uint32_t e1 = e0 + (1u << elog);
   const uint32_t bend = bstart[b + 1];
   if (e1 > bend) e1 = bend;
-  // 29-bit-limb XYZZ accumulator; table points are in the R = 2^261 domain.
-  // Software pipeline: the next point's random 64-B load (and the entry
-  // after it) are in flight while the current mixed addition computes.
+  // 29-bit-limb XYZZ accumulator (lazily reduced); table points are in the
+  // R = 2^261 domain
   X29 acc = x29_inf();
-  uint32_t ent_next = entries[e0];
-  uint32_t ent_after = e0 + 1 < e1 ? entries[e0 + 1] : 0u;
-  G1Affine pt_next = table[ent_next & 0x7fffffffu];
   for (uint32_t e = e0; e < e1; e++) {
-    const uint32_t ent = ent_next;
-    const G1Affine w = pt_next;
-    if (e + 1 < e1) {
-      ent_next = ent_after;
-      pt_next = table[ent_next & 0x7fffffffu];
-      if (e + 2 < e1) ent_after = entries[e + 2];
-    }
+    const uint32_t ent = entries[e];
+    const G1Affine w = table[ent & 0x7fffffffu];
     if (w.is_inf()) continue;
     A29 a = a29_load(w);
     if (ent >> 31) a.y = red2p29(sub29(Q29::zero(), a.y));
-    acc = x29_add_affine(acc, a);
+    acc = x29_acc_madd(acc, a);
   }
-  partial[t] = x29_store(acc);
+  partial[t] = x29_store(x29_acc_finish(acc));
   owner[t] = b;
 }
 
