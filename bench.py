@@ -27,6 +27,7 @@ ROOT = os.path.dirname(os.path.abspath(__file__))
 sys.path.insert(0, os.path.join(ROOT, "quill-zkvm_amd"))
 
 HBM_PEAK_GBPS = 8000.0  # MI355X_MICROARCH.md: HBM3E 8.0 TB/s spec
+LOGUP_BYTES_PER_ROW = 128  # 3 x 32 B table reads + 32 B column write
 MSM_BYTES_PER_SCALAR = 96  # 32 B scalar + 64 B affine base
 MSM_FQMUL_PER_SCALAR = 176  # 16 signed windows x 11 Fq mults
 
@@ -41,6 +42,8 @@ def parse():
     ap.add_argument("--no-sumcheck", action="store_true")
     ap.add_argument("--log-mle", type=int, default=22,
                     help="config C4: ML-PCS commit + open at 2^k evaluations (0: skip)")
+    ap.add_argument("--log-logup", type=int, default=22,
+                    help="Logup column rows per GPU (log2); 0 disables")
     ap.add_argument("--no-cpu-baseline", action="store_true")
     ap.add_argument("--cpu-sample-log", type=int, default=20,
                     help="log2 size of the CPU-baseline MSM sample (a prefix of the workload)")
@@ -72,12 +75,22 @@ def traffic_probe(args):
                               0, q.Transcript(b"sumcheck_bench"))
         for t in tabs:
             t.close()
+    if args.log_logup > 0:
+        from quill_amd.logup import logup_column_device
+        n = 1 << args.log_logup
+        tabs = [q.DeviceVec(dev, n).fill_random(0x5155494C4C + 5 + 11 * i) for i in range(3)]
+        out = q.DeviceVec(dev, n)
+        logup_column_device(dev, args.log_logup, tabs, E.Input(0) + E.Const(LOGUP_A) * E.Input(1),
+                            LOGUP_BETA, out, E.Input(2))
+        for t in tabs + [out]:
+            t.close()
     dev.close()
 
 
 def measure_traffic(args):
     import pmc_traffic
-    probe = ["--log-msm", str(args.log_msm), "--log-sumcheck", str(args.log_sumcheck)]
+    probe = ["--log-msm", str(args.log_msm), "--log-sumcheck", str(args.log_sumcheck),
+             "--log-logup", str(args.log_logup)]
     if args.no_sumcheck:
         probe.append("--no-sumcheck")
     try:
@@ -203,6 +216,9 @@ def main():
             out["sumcheck"]["roofline"]["traffic"] = tot
     if args.log_mle > 0:
         out["mle_open"] = bench_mle(q, dev, args, barrier_sync, max_over_ranks, rank, world)
+    if args.log_logup > 0:
+        out["logup"] = bench_logup(q, dev, args, barrier_sync, max_over_ranks, rank, world,
+                                   traffic)
     if rank == 0 and not args.no_cpu_baseline:
         out["cpu_baseline"] = cpu_baseline(args, srs, scalars)
         if not args.no_sumcheck:
@@ -294,6 +310,75 @@ def bench_mle(q, dev, args, barrier_sync, max_over_ranks, rank=0, world=1):
             "sharding": f"2^{k} evaluations over {world} rank(s) (strong scaling); "
                         "S polynomial replicated",
             "note": "6 MSMs (commit, S commitment, 4 KZG quotients) dominate"}
+
+
+LOGUP_A, LOGUP_BETA = 0xA1FA, 0xBE7A5EED
+
+
+def bench_logup(q, dev, args, barrier_sync, max_over_ranks, rank=0, world=1, traffic=None):
+    """Logup log-derivative column (multiset_check.rs:43-95 / set_inclusion.rs:
+    93-131, subset mode): out = m / (beta + h) with h = t0 + a t1 (two batched
+    columns, lookup.rs:46-56) and m = t2, 2^k rows per GPU (weak scaling)."""
+    from quill_amd import VirtualPolyExpr as E
+    from quill_amd.logup import logup_column_device
+    k = args.log_logup
+    n = 1 << k
+    lw = max(world.bit_length() - 1, 0)
+    tabs = [q.DeviceVec(dev, n).fill_random(0x5155494C4C + 5 + 11 * i + 100 * rank)
+            for i in range(3)]
+    out = q.DeviceVec(dev, n)
+    h = E.Input(0) + E.Const(LOGUP_A) * E.Input(1)
+    m = E.Input(2)
+    for _ in range(max(1, args.warmup)):
+        logup_column_device(dev, k + lw, tabs, h, LOGUP_BETA, out, m)
+    dev.enable_timing(True)
+    barrier_sync()
+    t0 = time.perf_counter()
+    for _ in range(args.steps):
+        s = logup_column_device(dev, k + lw, tabs, h, LOGUP_BETA, out, m)
+    barrier_sync()
+    dt = max_over_ranks(time.perf_counter() - t0)
+    kms, kn = dev.kernel_time("logup_column")
+    dev.enable_timing(False)
+    kern_ms = max_over_ranks(kms / max(kn, 1))
+    nbytes = LOGUP_BYTES_PER_ROW * n
+    res = {"metric": f"Logup column rows/s at 2^{k} rows per GPU (m / (beta + t0 + a t1))",
+           "value": world * n * args.steps / dt, "unit": "rows/s", "higher_is_better": True,
+           "ms": dt / args.steps * 1e3, "kernel_ms": kern_ms,
+           "roofline": {"bound": "hbm", "kernel": "logup_column", "achieved":
+                        nbytes / (kern_ms * 1e-3) / 1e9, "peak": HBM_PEAK_GBPS, "unit": "GB/s",
+                        "frac": nbytes / (kern_ms * 1e-3) / 1e9 / HBM_PEAK_GBPS,
+                        "traffic": _kernel_traffic(traffic, "k_logup"),
+                        "algorithmic_bytes": nbytes,
+                        "note": "3 table reads + 1 column write of 32 B per row"},
+           "column_sum_low64": hex(s & ((1 << 64) - 1))}
+    if rank == 0 and not args.no_cpu_baseline:
+        res["cpu_baseline"] = cpu_baseline_logup(args, tabs, out)
+    for t in tabs + [out]:
+        t.close()
+    return res
+
+
+def cpu_baseline_logup(args, tabs, out):
+    """The reference's per-row loop (evaluate h, .inverse(), * m) restated in C
+    (oracle/oracle_c.c: oc_logup_column, ark-ff binary-Euclid inverse), single
+    thread, on the first 2^18 rows of the timed workload; must equal the GPU
+    column on those rows."""
+    try:
+        oc = _oracle_c()
+        sys.path.insert(0, os.path.join(ROOT, "oracle"))
+        import quill_oracle as qo
+    except Exception as e:
+        return {"value": None, "unit": "rows/s", "error": f"oracle C library unavailable: {e}"}
+    ns = min(1 << 18, len(out))
+    cols = [t.to_numpy(ns) for t in tabs]
+    ref, sec = oc.logup_column_arrays(cols[0], cols[1], cols[2], qo.fr_to_limbs_mont(LOGUP_A),
+                                      qo.fr_to_limbs_mont(LOGUP_BETA))
+    import numpy as np
+    return {"value": ns / sec, "unit": "rows/s", "cores": 1, "kind": "port",
+            "sample": f"first {ns} rows of the timed workload, per-row inverse like the "
+                      f"reference ({sec:.2f} s)", "seconds": sec,
+            "matches_gpu_column_of_sample": bool(np.array_equal(ref, out.to_numpy(ns)))}
 
 
 def _kernel_traffic(traffic, kernel):

@@ -240,6 +240,31 @@ int qg_zerocheck_prove_dev(qg_ctx* ctx, uint32_t nvars, uint32_t ntables,
                            uint64_t* round_coeffs, uint32_t* round_lens, uint64_t* point,
                            uint64_t evaluation[4]);
 
+/* ---------------------------------------------------------------- Logup */
+/* Log-derivative column of the Logup PIOPs: the per-row loops of
+ * MultisetEqualityProof::prove (hyperplonk/src/piops/multiset_check.rs:43-95)
+ * and SetInclusionProof::prove (hyperplonk/src/piops/set_inclusion.rs:93-131):
+ *     out[x] = m(x) / (beta + h(x))        for every row x of the hypercube,
+ * h and m given as postfix expressions over `tables` (same encoding as the
+ * sumcheck above; m = 1 when m_prog is NULL, LookupMode::Equality).  Rows are
+ * 2^nvars (with a communicator attached: nvars is global and each rank passes
+ * and receives its 2^(nvars - log2(world)) block).  `out_sum` (nullable)
+ * receives sum_x out[x] over all ranks — the claimed sums of
+ * set_inclusion.rs:162-166,193-197.  Returns QG_ERR_ASSERT when some
+ * beta + h(x) == 0 (the reference panics in inverse().unwrap(), :51/:63).
+ * Limits: <= 128 monomials per expression, <= 64 distinct tables. */
+int qg_logup_column(qg_ctx* ctx, uint32_t nvars, uint32_t ntables, const uint64_t* const* tables,
+                    const qg_expr_op* h_prog, size_t h_len, const uint64_t* h_consts,
+                    size_t h_nconsts, const qg_expr_op* m_prog, size_t m_len,
+                    const uint64_t* m_consts, size_t m_nconsts, const uint64_t beta[4],
+                    uint64_t* out, uint64_t out_sum[4]);
+/* Same with device-resident tables and output (out must not alias a table). */
+int qg_logup_column_dev(qg_ctx* ctx, uint32_t nvars, uint32_t ntables, const qg_buf* const* tables,
+                        const qg_expr_op* h_prog, size_t h_len, const uint64_t* h_consts,
+                        size_t h_nconsts, const qg_expr_op* m_prog, size_t m_len,
+                        const uint64_t* m_consts, size_t m_nconsts, const uint64_t beta[4],
+                        qg_buf* out, uint64_t out_sum[4]);
+
 /* ---------------------------------------------------------------- profiling */
 /* Per-kernel device time (ms) of the last call on this context, measured with
  * HIP events on the stream the kernels run on.  `name` is one of the kernel

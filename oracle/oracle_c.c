@@ -669,3 +669,79 @@ int oc_bench_sumcheck(int log_n, uint64_t seed, double* seconds) {
   free(pt);
   return 0;
 }
+
+/* ---------------------------------------------------------------- Logup */
+static inline int u4_is_one(const uint64_t a[4]) { return a[0] == 1 && !(a[1] | a[2] | a[3]); }
+static inline void u4_shr1(uint64_t a[4]) {
+  for (int i = 0; i < 3; i++) a[i] = (a[i] >> 1) | (a[i + 1] << 63);
+  a[3] >>= 1;
+}
+/* (x + p) / 2 for odd x < p (x + p < 2^255: no carry out of 256 bits) */
+static inline void u4_add_p_shr1(const modulus* m, uint64_t x[4]) {
+  u128 c = 0;
+  for (int i = 0; i < 4; i++) {
+    c += (u128)x[i] + m->p[i];
+    x[i] = (uint64_t)c;
+    c >>= 64;
+  }
+  u4_shr1(x);
+}
+
+/* ark-ff 0.5.0 Fp::inverse for Montgomery backends: binary extended Euclid
+ * (Guide to ECC, Alg. 2.22) started at b = R^2, so aR -> a^{-1}R.  This is the
+ * per-row `.inverse()` of multiset_check.rs:51,63 (zero has no inverse). */
+static int f_inv_bea(const modulus* m, fp a, fp* out) {
+  if (f_is_zero(a)) return -1;
+  uint64_t u[4], v[4];
+  fp b, c;
+  memcpy(u, a.v, 32);
+  memcpy(v, m->p, 32);
+  memcpy(b.v, m->r2, 32);
+  memset(c.v, 0, 32);
+  while (!u4_is_one(u) && !u4_is_one(v)) {
+    while (!(u[0] & 1)) {
+      u4_shr1(u);
+      if (b.v[0] & 1) u4_add_p_shr1(m, b.v);
+      else u4_shr1(b.v);
+    }
+    while (!(v[0] & 1)) {
+      u4_shr1(v);
+      if (c.v[0] & 1) u4_add_p_shr1(m, c.v);
+      else u4_shr1(c.v);
+    }
+    if (geq(u, v)) {
+      sub4(u, u, v);
+      b = f_sub(m, b, c);
+    } else {
+      sub4(v, v, u);
+      c = f_sub(m, c, b);
+    }
+  }
+  *out = u4_is_one(u) ? b : c;
+  return 0;
+}
+
+/* Logup column as the reference computes it (multiset_check.rs:43-95 /
+ * set_inclusion.rs:93-131) for h = t0 + a*t1 and multiplicities m = t2:
+ * per row evaluate h, (beta + h).inverse(), then multiply by m.  Montgomery
+ * limbs in and out; returns -1 at the first zero denominator (the panic),
+ * else 0 and the single-thread wall time in *seconds. */
+int oc_logup_column(const uint64_t* t0, const uint64_t* t1, const uint64_t* t2, size_t n,
+                    const uint64_t a[4], const uint64_t beta[4], uint64_t* out, double* seconds) {
+  fp A, B;
+  memcpy(A.v, a, 32);
+  memcpy(B.v, beta, 32);
+  double s = now_s();
+  for (size_t i = 0; i < n; i++) {
+    fp x0, x1, x2, d, r;
+    memcpy(x0.v, t0 + 4 * i, 32);
+    memcpy(x1.v, t1 + 4 * i, 32);
+    memcpy(x2.v, t2 + 4 * i, 32);
+    d = f_add(&FR, B, f_add(&FR, x0, f_mul(&FR, A, x1)));
+    if (f_inv_bea(&FR, d, &r)) return -1;
+    r = f_mul(&FR, r, x2);
+    memcpy(out + 4 * i, r.v, 32);
+  }
+  if (seconds) *seconds = now_s() - s;
+  return 0;
+}

@@ -6,6 +6,8 @@ import ctypes as C
 import os
 import platform
 
+import numpy as np
+
 HERE = os.path.dirname(os.path.abspath(__file__))
 LIB = os.path.join(HERE, "_build", "liboracle_c.so")
 _lib = None
@@ -13,6 +15,7 @@ _lib = None
 R_MOD = 21888242871839275222246405745257275088548364400416034343698204186575808495617
 P_MOD = 21888242871839275222246405745257275088696311157297823662689037894645226208583
 _M64 = (1 << 64) - 1
+U64P = C.POINTER(C.c_uint64)
 
 
 def lib():
@@ -32,6 +35,8 @@ def lib():
                                           C.POINTER(C.c_double), C.POINTER(C.c_double), U64P,
                                           C.POINTER(C.c_uint8)]
         L.oc_bench_sumcheck.argtypes = [C.c_int, C.c_uint64, C.POINTER(C.c_double)]
+        L.oc_logup_column.argtypes = [U64P, U64P, U64P, C.c_size_t, U64P, U64P, U64P,
+                                      C.POINTER(C.c_double)]
         _lib = L
     return _lib
 
@@ -142,3 +147,21 @@ def bench_sumcheck_baseline(log_n: int = 16, seed: int = 0x5155494C4C):
     return {"ms": s.value * 1e3, "cores": 1, "kind": "port",
             "sample": f"evaluation-form sumcheck prover, h = g1*g2*g3 at 2^{log_n} vars "
                       f"(lower bound on the reference's per-pair DensePolynomial structure)"}
+
+
+def logup_column_arrays(t0, t1, t2, a_mont, beta_mont):
+    """C restatement of the reference's per-row Logup loop on Montgomery-limb
+    arrays (n x 4 uint64): out = t2 / (beta + t0 + a t1).  Returns (out, seconds);
+    raises ZeroDivisionError on a zero denominator."""
+    n = t0.shape[0]
+    out = np.zeros((n, 4), dtype=np.uint64)
+    s = C.c_double()
+    arrs = [np.ascontiguousarray(x, dtype=np.uint64) for x in (t0, t1, t2)]
+    av = np.array(a_mont, dtype=np.uint64)
+    bv = np.array(beta_mont, dtype=np.uint64)
+    p = [x.ctypes.data_as(U64P) for x in arrs]
+    rc = lib().oc_logup_column(p[0], p[1], p[2], n, av.ctypes.data_as(U64P),
+                               bv.ctypes.data_as(U64P), out.ctypes.data_as(U64P), C.byref(s))
+    if rc:
+        raise ZeroDivisionError("logup denominator is zero")
+    return out, s.value

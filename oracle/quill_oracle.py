@@ -779,6 +779,263 @@ class ZeroCheckProof:
 
 
 # ---------------------------------------------------------------------------
+# Logup PIOPs (hyperplonk/src/piops/{multiset_check,set_inclusion,
+# permutation_check,lookup}.rs)
+# ---------------------------------------------------------------------------
+LOOKUP_SUBSET, LOOKUP_EQUALITY = "subset", "equality"
+
+
+def logup_column(store: VirtualPolynomialStore, h, beta, m=None):
+    """multiset_check.rs:43-95 / set_inclusion.rs:93-131: per row
+    m(x) / (beta + h(x)) (h, m: virtual-polynomial indices; m = 1 when None).  The reference calls
+    `.inverse().unwrap()`, i.e. panics on a zero denominator: ZeroDivisionError."""
+    n = 1 << store.num_vars
+    den = []
+    for i in range(n):
+        g = [p[i] for p in store.polynomials]
+        d = (beta + store.evaluate_point(g, h)) % R_MOD
+        if d == 0:
+            raise ZeroDivisionError("logup denominator is zero (inverse().unwrap())")
+        den.append(d)
+    # Montgomery batch inversion (same values as n separate inversions)
+    pre, acc = [], 1
+    for d in den:
+        acc = acc * d % R_MOD
+        pre.append(acc)
+    inv = fr_inv(acc)
+    out = [0] * n
+    for i in reversed(range(n)):
+        out[i] = inv * (pre[i - 1] if i else 1) % R_MOD
+        inv = inv * den[i] % R_MOD
+    if m is not None:
+        for i in range(n):
+            g = [p[i] for p in store.polynomials]
+            out[i] = out[i] * store.evaluate_point(g, m) % R_MOD
+    return out
+
+
+class MultisetEqualityProof:
+    """multiset_check.rs:18-24."""
+
+    def __init__(self, cl, cr, sumcheck_proof, open_left, open_right):
+        self.denom_left_commitment, self.denom_right_commitment = cl, cr
+        self.sumcheck_proof = sumcheck_proof
+        self.opening_proof_denom_left, self.opening_proof_denom_right = open_left, open_right
+
+    @staticmethod
+    def prove(store: VirtualPolynomialStore, h_left, h_right, t: Transcript, kzg: KZG,
+              mode=LOOKUP_EQUALITY, multiplicities=None):
+        """multiset_check.rs:28-181 (mutates `store`: +3 tables, +1 virtual poly)."""
+        n = store.num_vars
+        beta = t.draw_field_element()
+        left = logup_column(store, h_left, beta)
+        if mode == LOOKUP_SUBSET:
+            assert multiplicities is not None, "Multiplicities polynomial must be provided"
+            right = logup_column(store, h_right, beta, multiplicities)
+        else:
+            assert multiplicities is None, "Multiplicities polynomial must not be provided"
+            right = logup_column(store, h_right, beta)
+        cl, cr = kzg.commit(left), kzg.commit(right)
+        t.append_g1(cl)
+        t.append_g1(cr)
+        lam = t.draw_field_element()
+        alpha = t.draw_field_element()
+        dl = store.allocate_polynomial(left)
+        dr = store.allocate_polynomial(right)
+        m = store.virtual_polys[multiplicities] if mode == LOOKUP_SUBSET else Expr.const(1)
+        zc = (Expr.input(dl) * (Expr.const(beta) + store.virtual_polys[h_left]) - Expr.const(1)
+              + Expr.const(lam) * (Expr.input(dr) * (Expr.const(beta)
+                                                     + store.virtual_polys[h_right]) - m))
+        z = [t.draw_field_element() for _ in range(n)]
+        eq_idx = store.allocate_polynomial(fast_eq_eval_hypercube(n, z))
+        h_hat = store.new_virtual_from_expr(zc)
+        store.mul_in_place(h_hat, eq_idx)
+        store.mul_const_in_place(h_hat, alpha)
+        store.add_in_place(h_hat, dl)
+        store.sub_in_place(h_hat, dr)
+        sc, (point, _ev) = SumcheckProof.prove_fast(n, store, h_hat, 0, t)
+        ol = MLEvalProof.prove(left, point, kzg, t)
+        orr = MLEvalProof.prove(right, point, kzg, t)
+        return MultisetEqualityProof(cl, cr, sc, ol, orr), point
+
+    def verify(self, t: Transcript, kzg: KZG, left_claim, right_claim,
+               mode=LOOKUP_EQUALITY, mult_claim=None):
+        """multiset_check.rs:183-283.  Claims are (point, evaluation); raises
+        ValueError with the reference's message on rejection."""
+        beta = t.draw_field_element()
+        t.append_g1(self.denom_left_commitment)
+        t.append_g1(self.denom_right_commitment)
+        lam = t.draw_field_element()
+        alpha = t.draw_field_element()
+        z = [t.draw_field_element() for _ in range(len(left_claim[0]))]
+        if self.sumcheck_proof.claimed_sum % R_MOD != 0:
+            raise ValueError("Multiset equality sumcheck claimed sum is not zero")
+        point, ev = self.sumcheck_proof.verify(t)
+        okl = self.opening_proof_denom_left.verify(self.denom_left_commitment, kzg, t)
+        okr = self.opening_proof_denom_right.verify(self.denom_right_commitment, kzg, t)
+        if not okl or not okr:
+            raise ValueError("Multiset equality opening proof verification failed")
+        if (self.opening_proof_denom_left.evaluation_point != point
+                or self.opening_proof_denom_right.evaluation_point != point):
+            raise ValueError("Multiset equality opening proof evaluation point does not match")
+        if list(left_claim[0]) != point or list(right_claim[0]) != point:
+            raise ValueError("Multiset equality h evaluation point does not match sumcheck")
+        m = 1
+        if mode == LOOKUP_SUBSET:
+            if mult_claim is None:
+                raise AssertionError("Multiplicities evaluation must be provided in subset mode")
+            if list(mult_claim[0]) != point:
+                raise ValueError("Multiset equality multiplicities evaluation point mismatch")
+            m = mult_claim[1]
+        dl = self.opening_proof_denom_left.evaluation
+        dr = self.opening_proof_denom_right.evaluation
+        zc = dl * (beta + left_claim[1]) - 1 + lam * (dr * (beta + right_claim[1]) - m)
+        final = (zc * eq_eval(z, left_claim[0]) * alpha + dl - dr) % R_MOD
+        if final != ev % R_MOD:
+            raise ValueError("Multiset equality final evaluation does not match sumcheck")
+
+
+class SetInclusionProof:
+    """set_inclusion.rs:52-61."""
+
+    def __init__(self, cl, cr, scl, scr, ol, orr):
+        self.denom_left_commitment, self.denom_right_commitment = cl, cr
+        self.sumcheck_proof_left, self.sumcheck_proof_right = scl, scr
+        self.opening_proof_denom_left, self.opening_proof_denom_right = ol, orr
+
+    @staticmethod
+    def prove(store_left: VirtualPolynomialStore, h_left, store_right: VirtualPolynomialStore,
+              h_right, multiplicities, t: Transcript, kzg: KZG):
+        """set_inclusion.rs:74-235 -> (proof, (left point, right point))."""
+        nl, nr = store_left.num_vars, store_right.num_vars
+        gamma = t.draw_field_element()  # logup_eval_point
+        left = logup_column(store_left, h_left, gamma)
+        right = logup_column(store_right, h_right, gamma, multiplicities)
+        cl, cr = kzg.commit(left), kzg.commit(right)
+        t.append_g1(cl)
+        t.append_g1(cr)
+        z1 = [t.draw_field_element() for _ in range(nl)]
+        alpha = t.draw_field_element()
+        dl = store_left.allocate_polynomial(left)
+        dr = store_right.allocate_polynomial(right)
+        m_expr = store_right.virtual_polys[multiplicities]
+        hl = store_left.virtual_polys[h_left]
+        hr = store_right.virtual_polys[h_right]
+        eq1 = store_left.allocate_polynomial(fast_eq_eval_hypercube(nl, z1))
+        el = (Expr.input(dl) * (Expr.const(gamma) + hl) - Expr.const(1))
+        el = el * Expr.input(eq1) + Expr.input(dl) * Expr.const(alpha)
+        vl = store_left.new_virtual_from_expr(el)
+        sum_l = sum(left) % R_MOD * alpha % R_MOD
+        scl, (pl, _) = SumcheckProof.prove_fast(nl, store_left, vl, sum_l, t)
+        z2 = [t.draw_field_element() for _ in range(nr)]
+        beta = t.draw_field_element()
+        eq2 = store_right.allocate_polynomial(fast_eq_eval_hypercube(nr, z2))
+        er = Expr.input(dr) * (Expr.const(gamma) + hr) - m_expr
+        er = er * Expr.input(eq2) + Expr.input(dr) * Expr.const(beta)
+        vr = store_right.new_virtual_from_expr(er)
+        sum_r = sum(right) % R_MOD * beta % R_MOD
+        scr, (pr, _) = SumcheckProof.prove_fast(nr, store_right, vr, sum_r, t)
+        ol = MLEvalProof.prove(left, pl, kzg, t)
+        orr = MLEvalProof.prove(right, pr, kzg, t)
+        return SetInclusionProof(cl, cr, scl, scr, ol, orr), (pl, pr)
+
+    def verify(self, t: Transcript, kzg: KZG, h_left_claim, h_right_claim, mult_claim):
+        """set_inclusion.rs:237-349 (claims are (point, evaluation))."""
+        nl, nr = len(h_left_claim[0]), len(h_right_claim[0])
+        gamma = t.draw_field_element()
+        t.append_g1(self.denom_left_commitment)
+        t.append_g1(self.denom_right_commitment)
+        z1 = [t.draw_field_element() for _ in range(nl)]
+        alpha = t.draw_field_element()
+        pl, evl = self.sumcheck_proof_left.verify(t)
+        z2 = [t.draw_field_element() for _ in range(nr)]
+        beta = t.draw_field_element()
+        pr, evr = self.sumcheck_proof_right.verify(t)
+        if not self.opening_proof_denom_left.verify(self.denom_left_commitment, kzg, t):
+            raise ValueError("Left denominator opening proof failed")
+        if not self.opening_proof_denom_right.verify(self.denom_right_commitment, kzg, t):
+            raise ValueError("Right denominator opening proof failed")
+        dl = self.opening_proof_denom_left.evaluation
+        dr = self.opening_proof_denom_right.evaluation
+        if pl != self.opening_proof_denom_left.evaluation_point:
+            raise ValueError("Left sumcheck point does not match PCS opening point")
+        if (list(h_left_claim[0]) != pl or list(h_right_claim[0]) != pr
+                or list(mult_claim[0]) != pr):
+            raise ValueError("Mismatched evaluation points for set inclusion")
+        if pr != self.opening_proof_denom_right.evaluation_point:
+            raise ValueError("Right sumcheck point does not match PCS opening point")
+        lz = dl * (gamma + h_left_claim[1]) - 1
+        if (lz * eq_eval(pl, z1) + alpha * dl - evl) % R_MOD != 0:
+            raise ValueError("Left sumcheck evaluation mismatch")
+        rz = dr * (gamma + h_right_claim[1]) - mult_claim[1]
+        if (rz * eq_eval(pr, z2) + beta * dr - evr) % R_MOD != 0:
+            raise ValueError("Right sumcheck evaluation mismatch")
+        v1 = self.sumcheck_proof_left.claimed_sum * fr_inv(alpha) % R_MOD
+        v2 = self.sumcheck_proof_right.claimed_sum * fr_inv(beta) % R_MOD
+        if v1 != v2:
+            raise ValueError("Log-derivative sums do not match")
+
+
+def permutation_check_prove(store, h_left, h_right, id_indices, perm_indices, t, kzg):
+    """permutation_check.rs:13-59 -> (MultisetEqualityProof, point)."""
+    n = store.num_vars
+    assert len(id_indices) == 1 << n and len(perm_indices) == 1 << n
+    id_ref = store.allocate_polynomial(id_indices)
+    perm_ref = store.allocate_polynomial(perm_indices)
+    alpha = t.draw_field_element()
+    lh = store.new_virtual_from_virtual(h_left)
+    store.mul_const_in_place(lh, alpha)
+    store.add_in_place(lh, id_ref)
+    rh = store.new_virtual_from_virtual(h_right)
+    store.mul_const_in_place(rh, alpha)
+    store.add_in_place(rh, perm_ref)
+    return MultisetEqualityProof.prove(store, lh, rh, t, kzg, LOOKUP_EQUALITY, None)
+
+
+def permutation_check_verify(proof, t, kzg, left_claim, right_claim, id_claim, perm_claim):
+    """permutation_check.rs:61-93."""
+    alpha = t.draw_field_element()
+    lh = (left_claim[0], (id_claim[1] + alpha * left_claim[1]) % R_MOD)
+    rh = (right_claim[0], (perm_claim[1] + alpha * right_claim[1]) % R_MOD)
+    proof.verify(t, kzg, lh, rh, LOOKUP_EQUALITY, None)
+
+
+def lookup_prove(source_store, source_cols, dest_store, dest_cols, multiplicities, t, kzg):
+    """lookup.rs:28-84 -> (SetInclusionProof, (left point, right point))."""
+    assert len(source_cols) == len(dest_cols)
+    n = len(source_cols)
+    t.append_u64(n)
+    assert n > 0
+    alpha = t.draw_field_element()
+    ap = [pow(alpha, i, R_MOD) for i in range(n)]
+    bl = source_store.virtual_polys[source_cols[0]]
+    br = dest_store.virtual_polys[dest_cols[0]]
+    for i in range(1, n):
+        bl = bl + Expr.const(ap[i]) * source_store.virtual_polys[source_cols[i]]
+        br = br + Expr.const(ap[i]) * dest_store.virtual_polys[dest_cols[i]]
+    vl = source_store.new_virtual_from_expr(bl)
+    vr = dest_store.new_virtual_from_expr(br)
+    return SetInclusionProof.prove(source_store, vl, dest_store, vr, multiplicities, t, kzg)
+
+
+def lookup_verify(proof, t, kzg, source_claims, dest_claims, mult_claim):
+    """lookup.rs:87-141 (claims are (point, evaluation))."""
+    n = len(source_claims)
+    if len(dest_claims) != n:
+        raise ValueError("Mismatched lookup evaluation vector lengths")
+    t.append_u64(n)
+    alpha = t.draw_field_element()
+    ap = [pow(alpha, i, R_MOD) for i in range(n)]
+    sp, dp = list(source_claims[0][0]), list(dest_claims[0][0])
+    for c in source_claims:
+        if list(c[0]) != sp:
+            raise ValueError("Lookup evaluation points for columns are inconsistent")
+    se = sum(c[1] * a for c, a in zip(source_claims, ap)) % R_MOD
+    de = sum(c[1] * a for c, a in zip(dest_claims, ap)) % R_MOD
+    proof.verify(t, kzg, (sp, se), (dp, de), mult_claim)
+
+
+# ---------------------------------------------------------------------------
 # Deterministic synthetic inputs (SURVEY §8(d)): splitmix64 -> xoshiro256**
 # ---------------------------------------------------------------------------
 class Xoshiro256ss:

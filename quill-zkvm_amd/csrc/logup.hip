@@ -1,0 +1,441 @@
+// Logup log-derivative columns for gfx950 — replaces the per-row loops of
+//   MultisetEqualityProof::prove  hyperplonk/src/piops/multiset_check.rs:43-95
+//   SetInclusionProof::prove      hyperplonk/src/piops/set_inclusion.rs:93-131
+// which evaluate h(x) through the expression tree for every row x, call
+// (beta + h(x)).inverse().unwrap() 2^n times, and multiply by m(x) in subset
+// mode.  Here: out[x] = m(x) / (beta + h(x)) in one HBM pass.
+//
+//  * Both expressions are compiled on the host into sums of monomials
+//    (expr.h).  The coefficient of a monomial with f factors is pre-scaled by
+//    2^(261 + 5f) (denominator) or 2^(256 + 5f) (multiplier), so multiplying
+//    raw arkworks table entries (x 2^256) with mul29 (x 2^-261) lands the
+//    denominator in the R = 2^261 domain and the multiplier in arkworks form
+//    with no conversion multiplies.
+//  * Batch inversion (Montgomery's trick) at three levels: each thread keeps
+//    the running prefix of its LG_K rows in registers (the row values go to
+//    LDS), the wave scans the thread products with shuffles (prefix and
+//    suffix), wave 0 inverts the block product (Fermat, sqr29), and every
+//    thread recovers its own inverse as inv(total) x prefix x suffix.  One
+//    inversion per LG_ROWS rows; ~3 multiplies per row otherwise.
+//  * A zero denominator makes the block product zero: the kernel flags it and
+//    the call returns QG_ERR_ASSERT (the reference panics in unwrap()).
+//  * Per-block sums of the outputs feed SetInclusionProof's claimed sums
+//    (set_inclusion.rs:162-166, 193-197) without a second pass.
+#include <string.h>
+
+#include <vector>
+
+#include "common.h"
+#include "expr.h"
+#include "field29.h"
+
+using namespace qg;
+
+namespace qg {
+
+using R29 = F29<FrP>;
+
+static constexpr int LG_BLOCK = 256;
+static constexpr int LG_K = 8;                     // rows per thread
+static constexpr int LG_ROWS = LG_BLOCK * LG_K;    // rows per block
+static constexpr int LG_MAXM = 128;                // monomials per expression
+static constexpr int LG_MAXF = 512;                // factor slots (both expressions)
+static constexpr int LG_MAXT = 64;                 // distinct tables referenced
+
+// device image of the two compiled expressions: [0] = beta + h, [1] = m
+struct LgDev {
+  uint32_t nm[2];
+  uint32_t mlen[2][LG_MAXM];
+  uint32_t fstart[2][LG_MAXM];
+  L9 coef[2][LG_MAXM];
+  uint32_t fac[LG_MAXF];
+  const Fr* tab[LG_MAXT];
+};
+
+// one expression at one row; < 2p, normalized
+QG_DEV R29 lg_eval(const LgDev* __restrict__ g, int w, size_t row) {
+  R29 acc = R29::zero();
+  const uint32_t nm = g->nm[w];
+  for (uint32_t m = 0; m < nm; m++) {
+    R29 t = R29::from_l9(g->coef[w][m]);
+    const uint32_t len = g->mlen[w][m], fs = g->fstart[w][m];
+    for (uint32_t j = 0; j < len; j++) t = mul29(t, to29(g->tab[g->fac[fs + j]][row]));
+    acc = red2p29(add29(acc, t));
+  }
+  return acc;
+}
+
+QG_DEV R29 shfl_up29(const R29& a, int d) {
+  R29 r;
+#pragma unroll
+  for (int i = 0; i < 9; i++) r.l[i] = __shfl_up(a.l[i], d, 64);
+  return r;
+}
+QG_DEV R29 shfl_down29(const R29& a, int d) {
+  R29 r;
+#pragma unroll
+  for (int i = 0; i < 9; i++) r.l[i] = __shfl_down(a.l[i], d, 64);
+  return r;
+}
+
+// a^(r-2), square-and-multiply (R = 2^261 domain; a < 2p normalized).  The
+// exponent is a compile-time constant, so every branch is uniform.
+QG_DEV R29 inv29_sq(const R29& a) {
+  uint32_t e[8];
+  uint32_t br = 0;
+  e[0] = subb32(FrP::P[0], 2u, 0, &br);
+#pragma unroll
+  for (int i = 1; i < 8; i++) e[i] = subb32(FrP::P[i], 0u, br, &br);
+  R29 r = a;  // top bit of r - 2 (bit 253)
+  for (int bit = 252; bit >= 0; bit--) {
+    r = sqr29(r);
+    if ((e[bit >> 5] >> (bit & 31)) & 1u) r = mul29(r, a);
+  }
+  return r;
+}
+
+QG_DEV R29 lds_row(const uint32_t* vs, int k, int tid) {
+  R29 v;
+#pragma unroll
+  for (int i = 0; i < 9; i++) v.l[i] = vs[(k * 9 + i) * LG_BLOCK + tid];
+  return v;
+}
+QG_DEV void lds_put(uint32_t* vs, int k, int tid, const R29& v) {
+#pragma unroll
+  for (int i = 0; i < 9; i++) vs[(k * 9 + i) * LG_BLOCK + tid] = v.l[i];
+}
+
+__global__ __launch_bounds__(LG_BLOCK) void k_logup(const LgDev* __restrict__ g, size_t n,
+                                                    Fr* __restrict__ out, Fr* __restrict__ bsum,
+                                                    uint32_t* __restrict__ err) {
+  __shared__ uint32_t vs[LG_K * 9 * LG_BLOCK];  // row denominators, [k][limb][thread]
+  __shared__ uint32_t wtot[LG_BLOCK / 64][9];
+  __shared__ uint32_t winv[9];
+  __shared__ uint32_t wsum[LG_BLOCK / 64][9];
+  const int tid = threadIdx.x, lane = tid & 63, wv = tid >> 6;
+  const size_t base = (size_t)blockIdx.x * LG_ROWS + tid;
+  const R29 one = R29::from_l9(F29P<FrP>::ONE);
+
+  // 1. denominators to LDS, then the running prefix of this thread's rows
+  for (int k = 0; k < LG_K; k++) {
+    const size_t row = base + (size_t)k * LG_BLOCK;
+    const R29 v = row < n ? lg_eval(g, 0, row) : one;
+#pragma unroll
+    for (int i = 0; i < 9; i++) vs[(k * 9 + i) * LG_BLOCK + tid] = v.l[i];
+  }
+  // (written out: the unroller declines this loop and would spill pre[] to scratch)
+  static_assert(LG_K == 8, "prefix chain is written out for 8 rows");
+  R29 pre[LG_K];
+  pre[0] = lds_row(vs, 0, tid);
+  pre[1] = mul29(pre[0], lds_row(vs, 1, tid));
+  pre[2] = mul29(pre[1], lds_row(vs, 2, tid));
+  pre[3] = mul29(pre[2], lds_row(vs, 3, tid));
+  pre[4] = mul29(pre[3], lds_row(vs, 4, tid));
+  pre[5] = mul29(pre[4], lds_row(vs, 5, tid));
+  pre[6] = mul29(pre[5], lds_row(vs, 6, tid));
+  pre[7] = mul29(pre[6], lds_row(vs, 7, tid));
+  const R29 T = pre[LG_K - 1];
+
+  // 2. exclusive prefix / suffix products of T across the block
+  R29 ip = T, is = T;  // inclusive in-wave prefix / suffix
+  for (int d = 1; d < 64; d <<= 1) {
+    const R29 a = shfl_up29(ip, d), b = shfl_down29(is, d);
+    if (lane >= d) ip = mul29(a, ip);
+    if (lane + d < 64) is = mul29(is, b);
+  }
+  if (lane == 63)
+#pragma unroll
+    for (int i = 0; i < 9; i++) wtot[wv][i] = ip.l[i];
+  R29 ep = shfl_up29(ip, 1), es = shfl_down29(is, 1);
+  if (lane == 0) ep = one;
+  if (lane == 63) es = one;
+  __syncthreads();
+  R29 tot = one;
+  for (int w = 0; w < LG_BLOCK / 64; w++) {  // wave products straight from LDS (uniform loop)
+    R29 t;
+#pragma unroll
+    for (int i = 0; i < 9; i++) t.l[i] = wtot[w][i];
+    if (w < wv) ep = mul29(ep, t);
+    if (w > wv) es = mul29(es, t);
+    if (wv == 0) tot = mul29(tot, t);
+  }
+  if (wv == 0) {
+    tot = canon29(tot);
+    if (is_zero29(tot)) {
+      if (lane == 0) atomicOr(err, 1u);
+    }
+    const R29 ti = inv29_sq(tot);
+    if (lane == 0)
+#pragma unroll
+      for (int i = 0; i < 9; i++) winv[i] = ti.l[i];
+  }
+  __syncthreads();
+  R29 inv_run;
+#pragma unroll
+  for (int i = 0; i < 9; i++) inv_run.l[i] = winv[i];
+  inv_run = mul29(mul29(inv_run, ep), es);  // 1 / T
+
+  // 3. back-substitution: 1 / v_k overwrites v_k in LDS (own slots only)
+#define LG_BACK(k)                                        \
+  {                                                       \
+    const R29 x = mul29(inv_run, pre[k - 1]);             \
+    inv_run = mul29(inv_run, lds_row(vs, k, tid));        \
+    lds_put(vs, k, tid, x);                               \
+  }
+  LG_BACK(7) LG_BACK(6) LG_BACK(5) LG_BACK(4) LG_BACK(3) LG_BACK(2) LG_BACK(1)
+#undef LG_BACK
+  lds_put(vs, 0, tid, inv_run);
+
+  // 4. multiplier, store, block sum
+  R29 acc = R29::zero();
+  for (int k = 0; k < LG_K; k++) {
+    const size_t row = base + (size_t)k * LG_BLOCK;
+    if (row >= n) break;
+    const R29 x = lds_row(vs, k, tid);
+    const R29 m = lg_eval(g, 1, row);  // M x 2^256
+    const R29 y = canon29(mul29(x, m));
+    out[row] = from29(y);
+    acc = red2p29(add29(acc, y));
+  }
+  // block sum (values < 2p; a wave tree then 4 wave partials)
+  for (int d = 32; d >= 1; d >>= 1) {
+    R29 o;
+#pragma unroll
+    for (int i = 0; i < 9; i++) o.l[i] = __shfl_xor(acc.l[i], d, 64);
+    acc = red2p29(add29(acc, o));
+  }
+  if (lane == 0)
+#pragma unroll
+    for (int i = 0; i < 9; i++) wsum[wv][i] = acc.l[i];
+  __syncthreads();
+  if (tid == 0) {
+    R29 s = R29::zero();
+#pragma unroll
+    for (int w = 0; w < LG_BLOCK / 64; w++) {
+      R29 t;
+#pragma unroll
+      for (int i = 0; i < 9; i++) t.l[i] = wsum[w][i];
+      s = red2p29(add29(s, t));
+    }
+    bsum[blockIdx.x] = from29(canon29(s));
+  }
+}
+
+// sum of the per-block sums (one block)
+__global__ __launch_bounds__(256) void k_logup_sum(const Fr* __restrict__ bsum, uint32_t nb,
+                                                   Fr* __restrict__ res) {
+  __shared__ uint32_t ws[4][9];
+  const int tid = threadIdx.x, lane = tid & 63, wv = tid >> 6;
+  R29 acc = R29::zero();
+  for (uint32_t i = tid; i < nb; i += 256) acc = red2p29(add29(acc, to29(bsum[i])));
+  for (int d = 32; d >= 1; d >>= 1) {
+    R29 o;
+#pragma unroll
+    for (int i = 0; i < 9; i++) o.l[i] = __shfl_xor(acc.l[i], d, 64);
+    acc = red2p29(add29(acc, o));
+  }
+  if (lane == 0)
+#pragma unroll
+    for (int i = 0; i < 9; i++) ws[wv][i] = acc.l[i];
+  __syncthreads();
+  if (tid == 0) {
+    R29 s = R29::zero();
+    for (int w = 0; w < 4; w++) {
+      R29 t;
+#pragma unroll
+      for (int i = 0; i < 9; i++) t.l[i] = ws[w][i];
+      s = red2p29(add29(s, t));
+    }
+    *res = from29(canon29(s));
+  }
+}
+
+// ---------------------------------------------------------------- host
+static Fr lg_plain_mul(const Fr& x, const Fr& y) { return from_mont(to_mont(x) * to_mont(y)); }
+static L9 lg_l9(const Fr& plain) {
+  const R29 t = to29(plain);
+  L9 r{};
+  for (int i = 0; i < 9; i++) r.v[i] = t.l[i];
+  return r;
+}
+
+// compile one expression into slot w of the image; `add_const` (Montgomery)
+// is added to the constant monomial; `base` = 261 or 256 (output scale)
+static void lg_compile(LgDev& d, int w, const SopProgram& sp, const Fr& add_const, bool with_const,
+                       uint32_t base, std::vector<uint32_t>& tables_used, uint32_t& nfac) {
+  std::vector<uint32_t> mlen = sp.mono_len;
+  std::vector<Fr> coeff = sp.coeff;
+  std::vector<std::vector<uint32_t>> facs;
+  size_t off = 0;
+  for (size_t m = 0; m < mlen.size(); m++) {
+    std::vector<uint32_t> f;
+    for (uint32_t j = 0; j < mlen[m]; j++) f.push_back(sp.used[sp.fac[off + j]]);
+    off += mlen[m];
+    facs.push_back(f);
+  }
+  if (with_const) {
+    bool found = false;
+    for (size_t m = 0; m < mlen.size(); m++)
+      if (mlen[m] == 0) {
+        coeff[m] = coeff[m] + add_const;
+        found = true;
+      }
+    if (!found) {
+      mlen.push_back(0);
+      coeff.push_back(add_const);
+      facs.push_back({});
+    }
+  }
+  QG_CHECK(mlen.size() <= (size_t)LG_MAXM, QG_ERR_UNSUPPORTED, "logup expression has too many monomials");
+  d.nm[w] = (uint32_t)mlen.size();
+  for (size_t m = 0; m < mlen.size(); m++) {
+    d.mlen[w][m] = mlen[m];
+    d.fstart[w][m] = nfac;
+    for (uint32_t t : facs[m]) {
+      QG_CHECK(nfac < (uint32_t)LG_MAXF, QG_ERR_UNSUPPORTED, "logup expressions have too many factors");
+      uint32_t slot = 0;
+      while (slot < tables_used.size() && tables_used[slot] != t) slot++;
+      if (slot == tables_used.size()) {
+        QG_CHECK(slot < (uint32_t)LG_MAXT, QG_ERR_UNSUPPORTED, "logup expressions use too many tables");
+        tables_used.push_back(t);
+      }
+      d.fac[nfac++] = slot;
+    }
+    d.coef[w][m] = lg_l9(lg_plain_mul(from_mont(coeff[m]), pow2_mod_plain<FrP>(base + 5 * mlen[m])));
+  }
+}
+
+static size_t lg_local_size(const qg_ctx* ctx, uint32_t nvars) {
+  uint32_t lw = 0;
+  while ((1 << lw) < ctx->world) lw++;
+  QG_CHECK((1 << lw) == ctx->world, QG_ERR_INVALID, "world size must be a power of two");
+  QG_CHECK(nvars >= lw, QG_ERR_INVALID, "nvars must be at least log2(world)");
+  QG_CHECK(nvars < 40, QG_ERR_INVALID, "nvars too large");
+  return (size_t)1 << (nvars - lw);
+}
+
+// out[x] = m(x) / (beta + h(x)) over this rank's rows; returns sum_x out[x]
+// over all ranks (Fr, i.e. arkworks Montgomery words)
+static Fr logup_run(qg_ctx* ctx, uint32_t nvars, uint32_t ntables, const std::vector<const Fr*>& tabs,
+                    const qg_expr_op* hp, size_t hl, const uint64_t* hc, size_t hn,
+                    const qg_expr_op* mp, size_t ml, const uint64_t* mc, size_t mn,
+                    const uint64_t beta[4], Fr* d_out) {
+  QG_CHECK(hp && hl, QG_ERR_INVALID, "missing h expression");
+  const size_t n = lg_local_size(ctx, nvars);
+  LgDev img;
+  memset(&img, 0, sizeof(img));
+  std::vector<uint32_t> used;
+  uint32_t nfac = 0;
+  const SopProgram sh = compile_program(hp, hl, hc, hn, ntables);
+  lg_compile(img, 0, sh, fr_import(beta), true, 261, used, nfac);
+  if (mp && ml) {
+    const SopProgram sm = compile_program(mp, ml, mc, mn, ntables);
+    lg_compile(img, 1, sm, Fr::zero(), false, 256, used, nfac);
+  } else {
+    SopProgram one;
+    lg_compile(img, 1, one, Fr::one(), true, 256, used, nfac);
+  }
+  for (size_t s = 0; s < used.size(); s++) img.tab[s] = tabs[used[s]];
+
+  const uint32_t nb = div_up(n, LG_ROWS);
+  uint8_t* io = ctx->scratch_as<uint8_t>("lg_io", sizeof(LgDev) + 64);
+  LgDev* d_img = reinterpret_cast<LgDev*>(io);
+  Fr* d_res = reinterpret_cast<Fr*>(io + sizeof(LgDev));
+  uint32_t* d_err = reinterpret_cast<uint32_t*>(io + sizeof(LgDev) + 32);
+  Fr* d_bsum = ctx->scratch_as<Fr>("lg_bsum", nb);
+  QG_HIP(hipMemcpyAsync(d_img, &img, sizeof(img), hipMemcpyHostToDevice, ctx->stream));
+  QG_HIP(hipMemsetAsync(d_err, 0, 4, ctx->stream));
+  {
+    QgTimed tm(ctx, "logup_column");
+    hipLaunchKernelGGL(k_logup, dim3(nb), dim3(LG_BLOCK), 0, ctx->stream, d_img, n, d_out, d_bsum,
+                       d_err);
+    QG_LAUNCH_CHECK();
+    hipLaunchKernelGGL(k_logup_sum, dim3(1), dim3(256), 0, ctx->stream, d_bsum, nb, d_res);
+    QG_LAUNCH_CHECK();
+  }
+  struct {
+    Fr res;
+    uint32_t err;
+  } h;
+  QG_HIP(hipMemcpyAsync(&h.res, d_res, sizeof(Fr), hipMemcpyDeviceToHost, ctx->stream));
+  QG_HIP(hipMemcpyAsync(&h.err, d_err, 4, hipMemcpyDeviceToHost, ctx->stream));
+  ctx->sync();
+  // every rank learns whether any rank hit a zero denominator, and the global sum
+  struct {
+    Fr s;
+    uint32_t err, pad[7];
+  } mine{h.res, h.err, {}};
+  Fr total = Fr::zero();
+  uint32_t any_err = 0;
+  if (ctx->world > 1) {
+    uint8_t* d_g = ctx->scratch_as<uint8_t>("lg_gather", sizeof(mine) * (ctx->world + 1));
+    QG_HIP(hipMemcpyAsync(d_g, &mine, sizeof(mine), hipMemcpyHostToDevice, ctx->stream));
+    comm_allgather_bytes(ctx, d_g, d_g + sizeof(mine), sizeof(mine));
+    std::vector<decltype(mine)> all(ctx->world);
+    QG_HIP(hipMemcpyAsync(all.data(), d_g + sizeof(mine), sizeof(mine) * ctx->world,
+                          hipMemcpyDeviceToHost, ctx->stream));
+    ctx->sync();
+    for (auto& a : all) {
+      total = total + a.s;
+      any_err |= a.err;
+    }
+  } else {
+    total = h.res;
+    any_err = h.err;
+  }
+  QG_CHECK(!any_err, QG_ERR_ASSERT, "logup denominator beta + h(x) is zero (reference: inverse().unwrap())");
+  return total;
+}
+
+}  // namespace qg
+
+// ---------------------------------------------------------------- C-ABI
+extern "C" {
+
+int qg_logup_column(qg_ctx* ctx, uint32_t nvars, uint32_t ntables, const uint64_t* const* tables,
+                    const qg_expr_op* h_prog, size_t h_len, const uint64_t* h_consts,
+                    size_t h_nconsts, const qg_expr_op* m_prog, size_t m_len,
+                    const uint64_t* m_consts, size_t m_nconsts, const uint64_t beta[4],
+                    uint64_t* out, uint64_t out_sum[4]) {
+  return qg_guard(ctx, [&] {
+    QG_CHECK(ctx && beta && out, QG_ERR_INVALID, "null argument");
+    QG_CHECK(ntables == 0 || tables, QG_ERR_INVALID, "null tables");
+    const size_t n = lg_local_size(ctx, nvars);
+    Fr* d = ctx->scratch_as<Fr>("lg_in", std::max<size_t>(1, n * (ntables + 1)));
+    std::vector<const Fr*> tabs;
+    for (uint32_t i = 0; i < ntables; i++) {
+      QG_CHECK(tables[i] != nullptr, QG_ERR_INVALID, "null table");
+      fr_upload(ctx, d + n * i, tables[i], n);
+      tabs.push_back(d + n * i);
+    }
+    Fr* d_out = d + n * ntables;
+    const Fr s = logup_run(ctx, nvars, ntables, tabs, h_prog, h_len, h_consts, h_nconsts, m_prog,
+                           m_len, m_consts, m_nconsts, beta, d_out);
+    fr_download(ctx, out, d_out, n);
+    if (out_sum) fr_export(s, out_sum);
+  });
+}
+
+int qg_logup_column_dev(qg_ctx* ctx, uint32_t nvars, uint32_t ntables, const qg_buf* const* tables,
+                        const qg_expr_op* h_prog, size_t h_len, const uint64_t* h_consts,
+                        size_t h_nconsts, const qg_expr_op* m_prog, size_t m_len,
+                        const uint64_t* m_consts, size_t m_nconsts, const uint64_t beta[4],
+                        qg_buf* out, uint64_t out_sum[4]) {
+  return qg_guard(ctx, [&] {
+    QG_CHECK(ctx && beta && out, QG_ERR_INVALID, "null argument");
+    QG_CHECK(ntables == 0 || tables, QG_ERR_INVALID, "null tables");
+    const size_t n = lg_local_size(ctx, nvars);
+    QG_CHECK(out->n >= n, QG_ERR_INVALID, "output buffer too short");
+    std::vector<const Fr*> tabs;
+    for (uint32_t i = 0; i < ntables; i++) {
+      QG_CHECK(tables[i] && tables[i]->n >= n, QG_ERR_INVALID, "table buffer missing or too short");
+      QG_CHECK(tables[i]->d != out->d, QG_ERR_INVALID, "output aliases an input table");
+      tabs.push_back(tables[i]->d);
+    }
+    const Fr s = logup_run(ctx, nvars, ntables, tabs, h_prog, h_len, h_consts, h_nconsts, m_prog,
+                           m_len, m_consts, m_nconsts, beta, out->d);
+    if (out_sum) fr_export(s, out_sum);
+  });
+}
+
+}  // extern "C"

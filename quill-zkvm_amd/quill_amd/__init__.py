@@ -10,3 +10,5 @@ from .hyperplonk import (SumcheckProof, VirtualPolyExpr, VirtualPolynomialStore,
                          ZeroCheckProof)
 from .pcs import KZG, EvaluationClaim, KZGOpeningProof, MLEvalProof  # noqa: F401
 from .transcript import Transcript  # noqa: F401
+from .logup import (LookupMode, LookupProof, MultisetEqualityProof,  # noqa: F401
+                    PermutationCheckProof, SetInclusionProof)

@@ -102,6 +102,12 @@ PROTOTYPES = {
     "qg_zerocheck_prove_dev": (C.c_int, [P, C.c_uint32, C.c_uint32, C.POINTER(P),
                                          C.POINTER(ExprOp), SZ, U64P, SZ, U8P, U64P, U32P,
                                          U64P, U64P]),
+    "qg_logup_column": (C.c_int, [P, C.c_uint32, C.c_uint32, C.POINTER(U64P),
+                                  C.POINTER(ExprOp), SZ, U64P, SZ, C.POINTER(ExprOp), SZ, U64P,
+                                  SZ, U64P, U64P, U64P]),
+    "qg_logup_column_dev": (C.c_int, [P, C.c_uint32, C.c_uint32, C.POINTER(P),
+                                      C.POINTER(ExprOp), SZ, U64P, SZ, C.POINTER(ExprOp), SZ,
+                                      U64P, SZ, U64P, P, U64P]),
     "qg_ctx_enable_timing": (C.c_int, [P, C.c_int]),
     "qg_microbench_fq_mul": (C.c_int, [P, C.POINTER(C.c_double)]),
     "qg_ctx_kernel_time": (C.c_int, [P, C.c_char_p, C.POINTER(C.c_double), U32P]),
