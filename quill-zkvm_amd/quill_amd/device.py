@@ -100,6 +100,9 @@ class DeviceVec:
         check(lib().qg_buf_upload(v.h, u64p(arr), len(xs)), dev.h)
         return v
 
+    def __len__(self):
+        return self.n
+
     def fill_random(self, seed: int):
         check(lib().qg_buf_fill_random(self.h, seed), self.dev.h)
         return self
