@@ -119,6 +119,25 @@ int qg_buf_download(const qg_buf* buf, uint64_t* fr, size_t n);
 /* Fill with uniform Fr from splitmix64->xoshiro256** keyed by (seed, index
  * block); used for synthetic benchmark witnesses. */
 int qg_buf_fill_random(qg_buf* buf, uint64_t seed);
+/* Non-owning view of entries [offset, offset+n) of `base` (destroy it with
+ * qg_buf_destroy; the base must outlive it).  The HyperPlonk full witness is
+ * the concatenation of its columns (hyperplonk/src/proof/proof.rs:270); its
+ * columns are views of it, so nothing is copied. */
+int qg_buf_view(qg_buf* base, size_t offset, size_t n, qg_buf** out);
+/* Upload n Montgomery Fr to entries [offset, offset+n). */
+int qg_buf_upload_at(qg_buf* buf, size_t offset, const uint64_t* fr, size_t n);
+/* Upload n canonical (non-Montgomery) 4 x u64 LE values < r, converted on the
+ * device (QG_ERR_INVALID if some value >= r). */
+int qg_buf_upload_canonical(qg_buf* buf, size_t offset, const uint64_t* canon, size_t n);
+/* F::from(u64) for n values: the id / permutation index columns of
+ * Circuit::permutation (hyperplonk/src/frontend/transition_circuit.rs:120-151). */
+int qg_buf_upload_u64(qg_buf* buf, size_t offset, const uint64_t* v, size_t n);
+/* Device-to-device copy of n entries. */
+int qg_buf_copy(qg_buf* dst, size_t dst_off, const qg_buf* src, size_t src_off, size_t n);
+/* First i < n with a[a_off+i] != b[b_off+i], or -1: the copy-constraint check
+ * of TransitionCircuit::check_constraints (transition_circuit.rs:186-202). */
+int qg_buf_first_mismatch(const qg_buf* a, size_t a_off, const qg_buf* b, size_t b_off, size_t n,
+                          int64_t* first);
 
 /* ---------------------------------------------------------------- MSM / KZG */
 /* E::G1::msm_unchecked(bases, scalars) (pcs/src/kzg.rs:72): sum of
@@ -173,6 +192,9 @@ int qg_mle_open_dev(qg_ctx* ctx, const qg_srs* srs, const qg_buf* poly, size_t n
  * batch their own protocol:
  *  compute_pr (mlpcs.rs:68-78) == eq(bin(i), point) table, untrimmed (2^nvars) */
 int qg_eq_table(qg_ctx* ctx, const uint64_t* point, size_t nvars, uint64_t* out);
+/*  fast_eq_eval_hypercube (hyperplonk/src/utils/eq_eval.rs:6-31) into a device
+ *  vector (first 2^nvars entries of `out`). */
+int qg_eq_table_dev(qg_ctx* ctx, const uint64_t* point, size_t nvars, qg_buf* out);
 /*  InnerProductProof::compute_s_polynomial (pcs/src/ipa.rs:122-157), untrimmed:
  *  out has max(nf, ng) - 1 entries (caller trims trailing zeros). */
 int qg_s_polynomial(qg_ctx* ctx, const uint64_t* f, size_t nf, const uint64_t* g, size_t ng,
@@ -264,6 +286,14 @@ int qg_logup_column_dev(qg_ctx* ctx, uint32_t nvars, uint32_t ntables, const qg_
                         size_t h_nconsts, const qg_expr_op* m_prog, size_t m_len,
                         const uint64_t* m_consts, size_t m_nconsts, const uint64_t beta[4],
                         qg_buf* out, uint64_t out_sum[4]);
+
+/* Circuit::check_constraints for one constraint expression
+ * (hyperplonk/src/frontend/transition_circuit.rs:153-172): `first_row`
+ * receives the first row x of the hypercube (this rank's block) with
+ * h(x) != 0, or -1 when h vanishes on every row. */
+int qg_expr_first_nonzero_dev(qg_ctx* ctx, uint32_t nvars, uint32_t ntables,
+                              const qg_buf* const* tables, const qg_expr_op* prog, size_t len,
+                              const uint64_t* consts, size_t nconsts, int64_t* first_row);
 
 /* ---------------------------------------------------------------- profiling */
 /* Per-kernel device time (ms) of the last call on this context, measured with

@@ -544,6 +544,9 @@ static fp tr_draw_fr(uint8_t st[32]) {
   fp lo, hi = {{0, 0, 0, 0}};
   memcpy(lo.v, ch, 32);
   memcpy(hi.v, ch + 32, 16);
+  /* lo is any 256-bit value: reduce mod r first (the no-carry CIOS needs
+     operands < r; 2^256 < 6r) */
+  while (geq(lo.v, FR.p)) sub4(lo.v, lo.v, FR.p);
   fp r2, r3;
   memcpy(r2.v, FR.r2, 32);
   r3 = f_mul(&FR, r2, r2); /* R^2*R^2/R = R^3 */

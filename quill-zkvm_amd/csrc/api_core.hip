@@ -121,6 +121,39 @@ __global__ void k_fill_random(Fr* out, size_t n, uint64_t seed) {
   }
 }
 
+// F::from(u64) for small integers (index mappings, transition_circuit.rs:120-151)
+__global__ void k_from_u64(Fr* out, const uint64_t* v, size_t n) {
+  const size_t i = (size_t)blockIdx.x * blockDim.x + threadIdx.x;
+  if (i >= n) return;
+  Fr x;
+  for (int l = 0; l < 8; l++) x.v[l] = 0;
+  x.v[0] = (uint32_t)v[i];
+  x.v[1] = (uint32_t)(v[i] >> 32);
+  out[i] = to_mont(x);
+}
+
+// canonical 4 x u64 LE -> Montgomery in place; flags values >= r
+__global__ void k_canon_to_mont(Fr* io, size_t n, uint32_t* err) {
+  const size_t i = (size_t)blockIdx.x * blockDim.x + threadIdx.x;
+  if (i >= n) return;
+  const Fr x = io[i];
+  if (!limbs_gt(FrP::P, x.v)) {
+    atomicOr(err, 1u);
+    return;
+  }
+  io[i] = to_mont(x);
+}
+
+// first index i < n with a[i] != b[i] (atomicMin; n if none)
+__global__ void k_first_mismatch(const Fr* a, const Fr* b, size_t n, unsigned long long* first) {
+  const size_t i = (size_t)blockIdx.x * blockDim.x + threadIdx.x;
+  if (i >= n) return;
+  const Fr x = a[i], y = b[i];
+  bool eq = true;
+  for (int l = 0; l < 8; l++) eq &= x.v[l] == y.v[l];
+  if (!eq) atomicMin(first, (unsigned long long)i);
+}
+
 }  // namespace qg
 
 extern "C" {
@@ -237,7 +270,7 @@ int qg_buf_create(qg_ctx* ctx, size_t n, qg_buf** out) {
 
 int qg_buf_destroy(qg_buf* buf) {
   if (!buf) return QG_OK;
-  (void)hipFree(buf->d);
+  if (buf->owned) (void)hipFree(buf->d);
   delete buf;
   return QG_OK;
 }
@@ -269,6 +302,93 @@ int qg_buf_fill_random(qg_buf* buf, uint64_t seed) {
                        buf->d, buf->n, seed);
     QG_LAUNCH_CHECK();
     buf->ctx->sync();
+  });
+}
+
+int qg_buf_view(qg_buf* base, size_t offset, size_t n, qg_buf** out) {
+  if (!base || !out || offset > base->n || n > base->n - offset) return QG_ERR_INVALID;
+  *out = nullptr;
+  return qg_guard(base->ctx, [&] {
+    qg_buf* b = new qg_buf();
+    b->ctx = base->ctx;
+    b->n = n;
+    b->d = base->d + offset;
+    b->owned = false;
+    *out = b;
+  });
+}
+
+int qg_buf_upload_at(qg_buf* buf, size_t offset, const uint64_t* fr, size_t n) {
+  if (!buf || (!fr && n) || offset > buf->n || n > buf->n - offset) return QG_ERR_INVALID;
+  return qg_guard(buf->ctx, [&] {
+    fr_upload(buf->ctx, buf->d + offset, fr, n);
+    buf->ctx->sync();
+  });
+}
+
+int qg_buf_upload_canonical(qg_buf* buf, size_t offset, const uint64_t* canon, size_t n) {
+  if (!buf || (!canon && n) || offset > buf->n || n > buf->n - offset) return QG_ERR_INVALID;
+  return qg_guard(buf->ctx, [&] {
+    if (n == 0) return;
+    qg_ctx* ctx = buf->ctx;
+    uint32_t* d_err = ctx->scratch_as<uint32_t>("canon_err", 1);
+    QG_HIP(hipMemsetAsync(d_err, 0, 4, ctx->stream));
+    fr_upload(ctx, buf->d + offset, canon, n);
+    hipLaunchKernelGGL(k_canon_to_mont, dim3(div_up(n, 256)), dim3(256), 0, ctx->stream,
+                       buf->d + offset, n, d_err);
+    QG_LAUNCH_CHECK();
+    uint32_t err = 0;
+    QG_HIP(hipMemcpyAsync(&err, d_err, 4, hipMemcpyDeviceToHost, ctx->stream));
+    ctx->sync();
+    QG_CHECK(!err, QG_ERR_INVALID, "canonical value >= r");
+  });
+}
+
+int qg_buf_upload_u64(qg_buf* buf, size_t offset, const uint64_t* v, size_t n) {
+  if (!buf || (!v && n) || offset > buf->n || n > buf->n - offset) return QG_ERR_INVALID;
+  return qg_guard(buf->ctx, [&] {
+    if (n == 0) return;
+    qg_ctx* ctx = buf->ctx;
+    uint64_t* d_v = ctx->scratch_as<uint64_t>("u64_stage", n);
+    QG_HIP(hipMemcpyAsync(d_v, v, n * 8, hipMemcpyHostToDevice, ctx->stream));
+    hipLaunchKernelGGL(k_from_u64, dim3(div_up(n, 256)), dim3(256), 0, ctx->stream,
+                       buf->d + offset, d_v, n);
+    QG_LAUNCH_CHECK();
+    ctx->sync();
+  });
+}
+
+int qg_buf_copy(qg_buf* dst, size_t dst_off, const qg_buf* src, size_t src_off, size_t n) {
+  if (!dst || !src || dst_off > dst->n || n > dst->n - dst_off || src_off > src->n ||
+      n > src->n - src_off)
+    return QG_ERR_INVALID;
+  return qg_guard(dst->ctx, [&] {
+    if (n == 0) return;
+    QG_HIP(hipMemcpyAsync(dst->d + dst_off, src->d + src_off, n * sizeof(Fr),
+                          hipMemcpyDeviceToDevice, dst->ctx->stream));
+    dst->ctx->sync();
+  });
+}
+
+int qg_buf_first_mismatch(const qg_buf* a, size_t a_off, const qg_buf* b, size_t b_off, size_t n,
+                          int64_t* first) {
+  if (!a || !b || !first || a_off > a->n || n > a->n - a_off || b_off > b->n ||
+      n > b->n - b_off)
+    return QG_ERR_INVALID;
+  return qg_guard(a->ctx, [&] {
+    *first = -1;
+    if (n == 0) return;
+    qg_ctx* ctx = a->ctx;
+    unsigned long long* d_f = ctx->scratch_as<unsigned long long>("mismatch", 1);
+    const unsigned long long init = n;
+    QG_HIP(hipMemcpyAsync(d_f, &init, 8, hipMemcpyHostToDevice, ctx->stream));
+    hipLaunchKernelGGL(k_first_mismatch, dim3(div_up(n, 256)), dim3(256), 0, ctx->stream,
+                       a->d + a_off, b->d + b_off, n, d_f);
+    QG_LAUNCH_CHECK();
+    unsigned long long f = 0;
+    QG_HIP(hipMemcpyAsync(&f, d_f, 8, hipMemcpyDeviceToHost, ctx->stream));
+    ctx->sync();
+    *first = f >= n ? -1 : (int64_t)f;
   });
 }
 

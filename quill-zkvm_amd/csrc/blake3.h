@@ -298,6 +298,8 @@ QG_HD Fr transcript_draw_fr_words(uint32_t st[8]) {
   for (int i = 0; i < 4; i++) hi.v[i] = ch[8 + i];
 #pragma unroll
   for (int i = 4; i < 8; i++) hi.v[i] = 0;
+  // lo may be >= r (any 256-bit value): reduce before the Montgomery product
+  reduce_full<FrP>(lo.v);
   return lo * Fr::from_raw(FrP::R2) + hi * Fr::from_raw(FrP::R3);
 }
 
@@ -442,6 +444,8 @@ QG_HD Fr fr_from_le48(const uint8_t b[48]) {
   for (int i = 0; i < 4; i++) hi.v[i] = b3_load32(b + 32 + 4 * i);
   for (int i = 4; i < 8; i++) hi.v[i] = 0;
   // lo*R^2*R^-1 = lo*R ; hi*R^3*R^-1 = hi*R^2 = (hi*2^256)*R
+  // lo may be >= r (any 256-bit value): reduce before the Montgomery product
+  reduce_full<FrP>(lo.v);
   return lo * Fr::from_raw(FrP::R2) + hi * Fr::from_raw(FrP::R3);
 }
 

@@ -140,6 +140,7 @@ struct qg_buf {
   qg_ctx* ctx = nullptr;
   size_t n = 0;
   qg::Fr* d = nullptr;
+  bool owned = true;  // false: a view into another buffer (qg_buf_view)
 };
 
 struct qg_srs {

@@ -200,8 +200,9 @@ __device__ __forceinline__ Fp<C> mont_mul_dev(const Fp<C>& a, const Fp<C>& b) {
 #endif
 
 // Montgomery product a*b*R^{-1} mod P.  Device: FIPS (above).  Host: CIOS,
-// no-carry variant.  Valid for inputs with a*b < P*R (in particular a, b < P;
-// also a < 2^256, b < P).
+// no-carry variant.  Operands must be < P (the no-carry CIOS drops the top
+// carry when an operand's high word is large; callers reduce unreduced
+// 256-bit values with reduce_full / to_mont first).
 template <class C>
 QG_HD Fp<C> operator*(const Fp<C>& a, const Fp<C>& b) {
 #if defined(__HIP_DEVICE_COMPILE__)
@@ -245,10 +246,21 @@ QG_HD Fp<C> from_mont(const Fp<C>& a) {
   return a * one;
 }
 
-// canonical (< 2^256, may exceed P) -> Montgomery
+// t mod P for any t < 2^256 (both BN254 moduli exceed 2^256 / 5.3, so five
+// conditional subtractions suffice)
+template <class C>
+QG_HD void reduce_full(uint32_t t[8]) {
+#pragma unroll
+  for (int k = 0; k < 5; k++) reduce_once<C>(t);
+}
+
+// canonical (< 2^256, may exceed P) -> Montgomery.  The operand is reduced
+// first: the host CIOS product below loses its top carry for inputs >= P.
 template <class C>
 QG_HD Fp<C> to_mont(const Fp<C>& a) {
-  return a * Fp<C>::from_raw(C::R2);
+  Fp<C> r = a;
+  reduce_full<C>(r.v);
+  return r * Fp<C>::from_raw(C::R2);
 }
 
 template <class C>

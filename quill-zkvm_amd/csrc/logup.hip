@@ -250,6 +250,15 @@ __global__ __launch_bounds__(256) void k_logup_sum(const Fr* __restrict__ bsum, 
   }
 }
 
+// first row whose expression value (slot 0, no beta) is nonzero; atomicMin
+__global__ __launch_bounds__(256) void k_expr_first_nonzero(const LgDev* __restrict__ g, size_t n,
+                                                            unsigned long long* first) {
+  const size_t row = (size_t)blockIdx.x * 256 + threadIdx.x;
+  if (row >= n) return;
+  const R29 v = canon29(lg_eval(g, 0, row));
+  if (!is_zero29(v)) atomicMin(first, (unsigned long long)row);
+}
+
 // ---------------------------------------------------------------- host
 static Fr lg_plain_mul(const Fr& x, const Fr& y) { return from_mont(to_mont(x) * to_mont(y)); }
 static L9 lg_l9(const Fr& plain) {
@@ -435,6 +444,45 @@ int qg_logup_column_dev(qg_ctx* ctx, uint32_t nvars, uint32_t ntables, const qg_
     const Fr s = logup_run(ctx, nvars, ntables, tabs, h_prog, h_len, h_consts, h_nconsts, m_prog,
                            m_len, m_consts, m_nconsts, beta, out->d);
     if (out_sum) fr_export(s, out_sum);
+  });
+}
+
+// Circuit::check_constraints (transition_circuit.rs:153-172): first row x
+// (this rank's block) with h(x) != 0, or -1.
+int qg_expr_first_nonzero_dev(qg_ctx* ctx, uint32_t nvars, uint32_t ntables,
+                              const qg_buf* const* tables, const qg_expr_op* prog, size_t len,
+                              const uint64_t* consts, size_t nconsts, int64_t* first_row) {
+  return qg_guard(ctx, [&] {
+    QG_CHECK(ctx && prog && len && first_row, QG_ERR_INVALID, "null argument");
+    QG_CHECK(ntables == 0 || tables, QG_ERR_INVALID, "null tables");
+    const size_t n = lg_local_size(ctx, nvars);
+    *first_row = -1;
+    LgDev img;
+    memset(&img, 0, sizeof(img));
+    std::vector<uint32_t> used;
+    uint32_t nfac = 0;
+    const SopProgram sp = compile_program(prog, len, consts, nconsts, ntables);
+    if (sp.mono_len.empty()) return;  // identically zero
+    // scale 256 + 5f: values come out in arkworks form (x 2^256); zero test only
+    lg_compile(img, 0, sp, Fr::zero(), false, 256, used, nfac);
+    for (size_t s = 0; s < used.size(); s++) {
+      QG_CHECK(tables[used[s]] && tables[used[s]]->n >= n, QG_ERR_INVALID,
+               "table buffer missing or too short");
+      img.tab[s] = tables[used[s]]->d;
+    }
+    uint8_t* io = ctx->scratch_as<uint8_t>("lg_io", sizeof(LgDev) + 64);
+    LgDev* d_img = reinterpret_cast<LgDev*>(io);
+    unsigned long long* d_first = reinterpret_cast<unsigned long long*>(io + sizeof(LgDev));
+    const unsigned long long init = n;
+    QG_HIP(hipMemcpyAsync(d_img, &img, sizeof(img), hipMemcpyHostToDevice, ctx->stream));
+    QG_HIP(hipMemcpyAsync(d_first, &init, 8, hipMemcpyHostToDevice, ctx->stream));
+    hipLaunchKernelGGL(k_expr_first_nonzero, dim3(div_up(n, 256)), dim3(256), 0, ctx->stream,
+                       d_img, n, d_first);
+    QG_LAUNCH_CHECK();
+    unsigned long long f = 0;
+    QG_HIP(hipMemcpyAsync(&f, d_first, 8, hipMemcpyDeviceToHost, ctx->stream));
+    ctx->sync();
+    *first_row = f >= n ? -1 : (int64_t)f;
   });
 }
 

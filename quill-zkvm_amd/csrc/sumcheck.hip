@@ -1188,6 +1188,18 @@ int qg_eq_table(qg_ctx* ctx, const uint64_t* point, size_t nvars, uint64_t* out)
   });
 }
 
+int qg_eq_table_dev(qg_ctx* ctx, const uint64_t* point, size_t nvars, qg_buf* out) {
+  if (!ctx || (!point && nvars) || !out || nvars > 34) return QG_ERR_INVALID;
+  return qg_guard(ctx, [&] {
+    QG_HIP(hipSetDevice(ctx->device));
+    QG_CHECK(out->n >= ((size_t)1 << nvars), QG_ERR_INVALID, "output buffer too short");
+    Fr* d_z = ctx->scratch_as<Fr>("eq_z", nvars ? nvars : 1);
+    fr_upload(ctx, d_z, point, nvars);
+    eq_table_device(ctx, d_z, (uint32_t)nvars, out->d);
+    ctx->sync();
+  });
+}
+
 int qg_sumcheck_prove(qg_ctx* ctx, uint32_t nvars, uint32_t ntables,
                       const uint64_t* const* tables, const qg_expr_op* prog, size_t prog_len,
                       const uint64_t* consts, size_t nconsts, const uint64_t claimed_sum[4],

@@ -12,3 +12,6 @@ from .pcs import KZG, EvaluationClaim, KZGOpeningProof, MLEvalProof  # noqa: F40
 from .transcript import Transcript  # noqa: F401
 from .logup import (LookupMode, LookupProof, MultisetEqualityProof,  # noqa: F401
                     PermutationCheckProof, SetInclusionProof)
+from .frontend import StateCell, TransitionCircuit, TransitionCircuitTarget  # noqa: F401
+from .proof import (HyperPlonk, HyperPlonkProof, TracePK, TraceProof, TraceVK,  # noqa: F401
+                    TraceWitness)

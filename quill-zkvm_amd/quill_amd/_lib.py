@@ -80,6 +80,12 @@ PROTOTYPES = {
     "qg_buf_upload": (C.c_int, [P, U64P, SZ]),
     "qg_buf_download": (C.c_int, [P, U64P, SZ]),
     "qg_buf_fill_random": (C.c_int, [P, C.c_uint64]),
+    "qg_buf_view": (C.c_int, [P, SZ, SZ, C.POINTER(P)]),
+    "qg_buf_upload_at": (C.c_int, [P, SZ, U64P, SZ]),
+    "qg_buf_upload_canonical": (C.c_int, [P, SZ, U64P, SZ]),
+    "qg_buf_upload_u64": (C.c_int, [P, SZ, U64P, SZ]),
+    "qg_buf_copy": (C.c_int, [P, SZ, P, SZ, SZ]),
+    "qg_buf_first_mismatch": (C.c_int, [P, SZ, P, SZ, SZ, C.POINTER(C.c_int64)]),
     "qg_msm_g1": (C.c_int, [P, P, U64P, SZ, U64P, U8P]),
     "qg_msm_g1_dev": (C.c_int, [P, P, P, SZ, U64P, U8P]),
     "qg_kzg_commit": (C.c_int, [P, P, U64P, SZ, U64P, U8P]),
@@ -87,6 +93,7 @@ PROTOTYPES = {
     "qg_mle_open": (C.c_int, [P, P, U64P, SZ, U64P, SZ, U8P, C.POINTER(MleProof)]),
     "qg_mle_open_dev": (C.c_int, [P, P, P, SZ, U64P, SZ, U8P, C.POINTER(MleProof)]),
     "qg_eq_table": (C.c_int, [P, U64P, SZ, U64P]),
+    "qg_eq_table_dev": (C.c_int, [P, U64P, SZ, P]),
     "qg_s_polynomial": (C.c_int, [P, U64P, SZ, U64P, SZ, U64P]),
     "qg_inner_product": (C.c_int, [P, U64P, SZ, U64P, SZ, U64P]),
     "qg_expr_degree": (C.c_int, [C.POINTER(ExprOp), SZ, U32P]),
@@ -108,6 +115,9 @@ PROTOTYPES = {
     "qg_logup_column_dev": (C.c_int, [P, C.c_uint32, C.c_uint32, C.POINTER(P),
                                       C.POINTER(ExprOp), SZ, U64P, SZ, C.POINTER(ExprOp), SZ,
                                       U64P, SZ, U64P, P, U64P]),
+    "qg_expr_first_nonzero_dev": (C.c_int, [P, C.c_uint32, C.c_uint32, C.POINTER(P),
+                                            C.POINTER(ExprOp), SZ, U64P, SZ,
+                                            C.POINTER(C.c_int64)]),
     "qg_ctx_enable_timing": (C.c_int, [P, C.c_int]),
     "qg_microbench_fq_mul": (C.c_int, [P, C.POINTER(C.c_double)]),
     "qg_ctx_kernel_time": (C.c_int, [P, C.c_char_p, C.POINTER(C.c_double), U32P]),

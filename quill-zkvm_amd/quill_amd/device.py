@@ -62,6 +62,14 @@ class Device:
         return ms.value, n.value
 
     # ---- device math building blocks (mlpcs.rs / ipa.rs / eq_eval.rs) ----
+    def eq_table_dev(self, point, out: "DeviceVec" = None) -> "DeviceVec":
+        """fast_eq_eval_hypercube (eq_eval.rs:6-31) into a device vector"""
+        n = len(point)
+        pt = fr_array(point) if n else np.zeros((1, 4), dtype=np.uint64)
+        out = out if out is not None else DeviceVec(self, 1 << n)
+        check(lib().qg_eq_table_dev(self.h, u64p(pt), n, out.h), self.h)
+        return out
+
     def eq_table(self, point):
         n = len(point)
         pt = fr_array(point)
@@ -90,8 +98,52 @@ class DeviceVec:
     def __init__(self, dev: Device, n: int):
         self.dev = dev
         self.n = n
+        self.base = None  # the owning buffer when this is a view
         self.h = C.c_void_p()
         check(lib().qg_buf_create(dev.h, n, C.byref(self.h)), dev.h)
+
+    def view(self, offset: int, n: int) -> "DeviceVec":
+        """Entries [offset, offset+n) without a copy (qg_buf_view); keeps this
+        buffer alive."""
+        v = DeviceVec.__new__(DeviceVec)
+        v.dev, v.n, v.base = self.dev, n, self
+        v.h = C.c_void_p()
+        check(lib().qg_buf_view(self.h, offset, n, C.byref(v.h)), self.dev.h)
+        return v
+
+    @classmethod
+    def from_canonical(cls, dev: Device, limbs: np.ndarray, out: "DeviceVec" = None,
+                       offset: int = 0):
+        """(n, 4) uint64 canonical little-endian limbs (values < r) ->
+        Montgomery on the device (qg_buf_upload_canonical)."""
+        limbs = np.ascontiguousarray(limbs, dtype=np.uint64)
+        n = limbs.shape[0]
+        v = out if out is not None else cls(dev, n)
+        check(lib().qg_buf_upload_canonical(v.h, offset, u64p(limbs), n), dev.h)
+        return v
+
+    @classmethod
+    def from_u64(cls, dev: Device, vals, out: "DeviceVec" = None, offset: int = 0):
+        """F::from(u64) of every value (qg_buf_upload_u64)."""
+        arr = np.ascontiguousarray(vals, dtype=np.uint64)
+        v = out if out is not None else cls(dev, arr.shape[0])
+        check(lib().qg_buf_upload_u64(v.h, offset, arr.ctypes.data_as(C.POINTER(C.c_uint64)),
+                                      arr.shape[0]), dev.h)
+        return v
+
+    def copy_from(self, src: "DeviceVec", dst_off: int = 0, src_off: int = 0, n: int = None):
+        n = src.n - src_off if n is None else n
+        check(lib().qg_buf_copy(self.h, dst_off, src.h, src_off, n), self.dev.h)
+        return self
+
+    def first_mismatch(self, other: "DeviceVec", off: int = 0, other_off: int = 0,
+                       n: int = None) -> int:
+        """first i with self[off+i] != other[other_off+i], or -1"""
+        n = self.n - off if n is None else n
+        r = C.c_int64()
+        check(lib().qg_buf_first_mismatch(self.h, off, other.h, other_off, n, C.byref(r)),
+              self.dev.h)
+        return r.value
 
     @classmethod
     def from_list(cls, dev: Device, xs):

@@ -48,6 +48,28 @@ def fr_array(xs) -> np.ndarray:
     return out
 
 
+def fr_canonical_array(xs) -> np.ndarray:
+    """list of ints -> (n, 4) uint64 canonical limbs (reduced mod r); the device
+    converts to Montgomery form (DeviceVec.from_canonical)."""
+    b = b"".join((int(x) % R_MOD).to_bytes(32, "little") for x in xs)
+    return np.frombuffer(b, dtype="<u8").reshape(len(xs), 4).copy()
+
+
+def fr_inv(x: int) -> int:
+    x %= R_MOD
+    if x == 0:
+        raise ZeroDivisionError("inverse of zero in Fr")
+    return pow(x, R_MOD - 2, R_MOD)
+
+
+def eq_eval(x, y) -> int:
+    """eq(x, y) = prod_i (x_i y_i + (1 - x_i)(1 - y_i))  (eq_eval.rs:33-43)"""
+    acc = 1
+    for a, b in zip(x, y):
+        acc = acc * (a * b + (1 - a) * (1 - b)) % R_MOD
+    return acc
+
+
 def fr_list(arr) -> list:
     a = np.asarray(arr, dtype=np.uint64).reshape(-1, 4)
     return [fr_from_mont_limbs(row) for row in a]

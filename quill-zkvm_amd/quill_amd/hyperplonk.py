@@ -12,7 +12,7 @@ import numpy as np
 
 from ._lib import ExprOp, check, lib
 from .device import Device, DeviceVec
-from .field import R_MOD, fr_array, fr_c, fr_list, u64p
+from .field import R_MOD, eq_eval, fr_array, fr_c, fr_canonical_array, fr_inv, fr_list, u64p
 from .pcs import EvaluationClaim
 from .transcript import Transcript
 
@@ -86,17 +86,35 @@ def expr_degree(expr: VirtualPolyExpr) -> int:
 
 
 class VirtualPolynomialStore:
-    """virtual_polynomial.rs:142-331.  Tables are lists of canonical ints."""
+    """virtual_polynomial.rs:142-331.
 
-    def __init__(self, num_vars: int):
+    Host store (dev=None): tables are lists of canonical ints, uploaded per call.
+    Device store (dev given): tables are DeviceVec (HBM-resident; host lists are
+    uploaded once at allocation) and every prover below runs on them in place.
+    The reference clones each table into the store (:161-171); tables are never
+    mutated here, so the device store keeps a reference instead of a copy."""
+
+    def __init__(self, num_vars: int, dev: Device = None):
         self.num_vars = num_vars
+        self.dev = dev
         self.polynomials = []
         self.virtual_polys = []
+
+    @property
+    def on_device(self) -> bool:
+        return self.dev is not None
 
     def allocate_polynomial(self, evals):
         assert len(evals) == 1 << self.num_vars, \
             "Input polynomial evaluations length does not match number of variables"
-        self.polynomials.append([int(e) % R_MOD for e in evals])
+        if self.dev is not None:
+            if not isinstance(evals, DeviceVec):
+                evals = DeviceVec.from_canonical(self.dev, fr_canonical_array(evals))
+            self.polynomials.append(evals)
+        else:
+            if isinstance(evals, DeviceVec):
+                evals = evals.to_list()
+            self.polynomials.append([int(e) % R_MOD for e in evals])
         return len(self.polynomials) - 1
 
     def new_virtual_from_input(self, g):
@@ -158,6 +176,11 @@ class SumcheckProof:
     def prove(num_vars, store: VirtualPolynomialStore, h, claimed_sum, transcript: Transcript,
               dev: Device = None):
         """sumcheck.rs:28-114 on the device; returns (proof, EvaluationClaim)."""
+        if store.on_device:
+            r_polys, pt, e = _unpack_dev(num_vars, store.virtual_polys[h], *sumcheck_prove_device(
+                store.dev, num_vars, store.polynomials, store.virtual_polys[h], claimed_sum,
+                transcript))
+            return SumcheckProof(num_vars, claimed_sum % R_MOD, r_polys), EvaluationClaim(pt, e)
         dev = dev or _default_device()
         expr = store.virtual_polys[h]
         prog, plen, carr, nc = _program_c(expr)
@@ -185,6 +208,8 @@ class ZeroCheckProof:
     def prove(store: VirtualPolynomialStore, h, transcript: Transcript, dev: Device = None):
         """zerocheck.rs:14-49 on the device.  Mutates `store` exactly like the
         reference: appends the eq table and the virtual polynomial h * eq."""
+        if store.on_device:
+            return ZeroCheckProof._prove_dev(store, h, transcript)
         dev = dev or _default_device()
         n = store.num_vars
         expr = store.virtual_polys[h]
@@ -206,6 +231,26 @@ class ZeroCheckProof:
         store.mul_in_place(h_hat, eq_idx)
         r_polys, pt, e = _unpack(n, width, coeffs, lens, point, ev)
         return (ZeroCheckProof(n, SumcheckProof(n, 0, r_polys)), EvaluationClaim(pt, e))
+
+
+def _prove_dev_zc(store, h, transcript):
+    """zerocheck.rs:14-49 over a device store, step for step: draw z, eq table
+    on the device, store mutation, sumcheck of h * eq with sum 0, claim / eq(z, pt)."""
+    n = store.num_vars
+    z = [transcript.draw_field_element() for _ in range(n)]
+    eq_idx = store.allocate_polynomial(store.dev.eq_table_dev(z))
+    h_hat = store.new_virtual_from_virtual(h)
+    store.mul_in_place(h_hat, eq_idx)
+    proof, claim = SumcheckProof.prove(n, store, h_hat, 0, transcript)
+    ev = claim.evaluation * fr_inv(eq_eval(z, claim.point)) % R_MOD
+    return ZeroCheckProof(n, proof), EvaluationClaim(claim.point, ev)
+
+
+ZeroCheckProof._prove_dev = staticmethod(_prove_dev_zc)
+
+
+def _unpack_dev(num_vars, expr, coeffs, lens, point, ev):
+    return _unpack(num_vars, expr_degree(expr) + 1, coeffs, lens, point, ev)
 
 
 def sumcheck_prove_tables(dev: Device, num_vars: int, tables, expr: VirtualPolyExpr,

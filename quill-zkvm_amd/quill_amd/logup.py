@@ -40,6 +40,12 @@ def logup_column(store: VirtualPolynomialStore, h, beta: int, m=None, dev: Devic
     `store` (m = None: 1).  Returns (column, sum of the column).  Raises
     QuillGpuError(QG_ERR_ASSERT) on a zero denominator, where the reference
     panics in inverse().unwrap()."""
+    if store.on_device:
+        out = DeviceVec(store.dev, 1 << store.num_vars)
+        s = logup_column_device(store.dev, store.num_vars, store.polynomials,
+                                store.virtual_polys[h], beta, out,
+                                store.virtual_polys[m] if m is not None else None)
+        return out, s
     dev = dev or _default_device()
     n = store.num_vars
     hp = _expr_args(store.virtual_polys[h])
@@ -64,6 +70,11 @@ def logup_column_device(dev: Device, num_vars: int, tables, h_expr: VirtualPolyE
                                     hp[3], mp[0], mp[1], mp[2], mp[3], fr_c(beta), out.h, s),
           dev.h)
     return fr_from_mont_limbs(list(s))
+
+
+def _eq_for(store: VirtualPolynomialStore, dev: Device, z):
+    """eq(., z) table in the store's residency (device vector or host list)"""
+    return store.dev.eq_table_dev(z) if store.on_device else dev.eq_table(z)
 
 
 @dataclass
@@ -105,7 +116,7 @@ class MultisetEqualityProof:
         zc = (E.Input(dl) * (E.Const(beta) + store.virtual_polys[h_left]) - E.Const(1)
               + E.Const(lam) * (E.Input(dr) * (E.Const(beta) + store.virtual_polys[h_right]) - m))
         z = [transcript.draw_field_element() for _ in range(n)]
-        eq_idx = store.allocate_polynomial(dev.eq_table(z))
+        eq_idx = store.allocate_polynomial(_eq_for(store, dev, z))
         h_hat = store.new_virtual_from_expr(zc)
         store.mul_in_place(h_hat, eq_idx)
         store.mul_const_in_place(h_hat, alpha)
@@ -147,7 +158,7 @@ class SetInclusionProof:
         m_expr = store_right.virtual_polys[multiplicities]
         hl = store_left.virtual_polys[h_left]
         hr = store_right.virtual_polys[h_right]
-        eq1 = store_left.allocate_polynomial(dev.eq_table(z1))
+        eq1 = store_left.allocate_polynomial(_eq_for(store_left, dev, z1))
         el = E.Input(dl) * (E.Const(gamma) + hl) - E.Const(1)
         el = el * E.Input(eq1) + E.Input(dl) * E.Const(alpha)
         vl = store_left.new_virtual_from_expr(el)
@@ -155,7 +166,7 @@ class SetInclusionProof:
                                        dev)
         z2 = [transcript.draw_field_element() for _ in range(nr)]
         beta = transcript.draw_field_element()
-        eq2 = store_right.allocate_polynomial(dev.eq_table(z2))
+        eq2 = store_right.allocate_polynomial(_eq_for(store_right, dev, z2))
         er = E.Input(dr) * (E.Const(gamma) + hr) - m_expr
         er = er * E.Input(eq2) + E.Input(dr) * E.Const(beta)
         vr = store_right.new_virtual_from_expr(er)

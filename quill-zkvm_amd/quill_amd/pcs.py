@@ -10,7 +10,7 @@ from dataclasses import dataclass
 import numpy as np
 
 from ._lib import KzgOpening, MleProof, QuillGpuError, check, lib
-from .device import Device, Srs
+from .device import Device, DeviceVec, Srs
 from .field import fr_array, fr_c, fr_from_mont_limbs, g1_from_abi, u64p
 from .transcript import Transcript
 
@@ -84,6 +84,8 @@ class KZG:
     def commit(self, poly):
         if len(poly) > self._max_degree + 1:
             raise QuillGpuError(-1, "Polynomial degree exceeds max degree")
+        if isinstance(poly, DeviceVec):
+            return self.srs.msm_dev(poly, len(poly))
         arr = fr_array(poly) if len(poly) else np.zeros((1, 4), dtype=np.uint64)
         xy = (C.c_uint64 * 8)()
         inf = C.c_uint8()
@@ -112,6 +114,8 @@ class KZG:
                            _opening(out.s_opening), _opening(out.s_opening_inv))
 
     def open(self, poly, eval_point, transcript: Transcript) -> MLEvalProof:
+        if isinstance(poly, DeviceVec):
+            return self.open_dev(poly, len(poly), eval_point, transcript)
         arr = fr_array(poly) if len(poly) else np.zeros((1, 4), dtype=np.uint64)
         pt = fr_array(eval_point) if len(eval_point) else np.zeros((1, 4), dtype=np.uint64)
         out = MleProof()

@@ -186,7 +186,34 @@ def main():
                     "s_opening": op(proof.s_opening), "s_opening_inv": op(proof.s_opening_inv),
                     "state_after": t.state.hex()})
     write("mlpcs.json", mls)
+    hyperplonk_fixture()
     print("golden fixtures written to", HERE)
+
+
+def hyperplonk_fixture():
+    """HyperPlonk multitrace proof (test_basic_proof.rs:165-196: fibonacci +
+    modified fibonacci at 8 rows) with a fixed trapdoor; the oracle verifier
+    must accept it."""
+    import hyperplonk_oracle as ho
+    tau = 0x48595045524C4F4E4B  # tests/test_gpu_hyperplonk.py TAU
+    c1, w1 = ho.fibonacci_circuit_and_trace(8)
+    c2, w2 = ho.modified_fibonacci_circuit_and_trace(8)
+    pcs = o.KZG(max(c1.num_cols() * c1.num_rows(), c2.num_cols() * c2.num_rows()), tau)
+    hp = ho.HyperPlonk.preprocess([c1, c2], pcs)
+    proof, t = hp.prove(pcs, [w1, w2])
+    assert ho.hyperplonk_verify(proof, hp.to_vk(), pcs).state == t.state
+    write("hyperplonk.json", {
+        "rows": 8, "circuits": ["fib", "mod"], "tau": s(tau),
+        "witness": [[[s(x) for x in col] for col in w] for w in (w1, w2)],
+        "witness_commitments": [pt(C) for C in proof.witness_commitment],
+        "id_commitments": [pt(vk.id_commitment) for vk in hp.trace_vks],
+        "permutation_commitments": [pt(vk.permutation_commitment) for vk in hp.trace_vks],
+        "zerocheck_r_polys": [[[s(x) for x in m] for m in tp.zero_check_proof.sumcheck_proof.r_polys]
+                              for tp in proof.trace_proofs],
+        "permcheck_r_polys": [[[s(x) for x in m]
+                               for m in tp.permutation_check_proof.sumcheck_proof.r_polys]
+                              for tp in proof.trace_proofs],
+        "final_state": t.state.hex()})
 
 
 if __name__ == "__main__":
