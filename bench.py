@@ -44,6 +44,9 @@ def parse():
                     help="config C4: ML-PCS commit + open at 2^k evaluations (0: skip)")
     ap.add_argument("--log-logup", type=int, default=22,
                     help="Logup column rows per GPU (log2); 0 disables")
+    ap.add_argument("--log-hp-rows", type=int, default=20,
+                    help="config C5: HyperPlonk prove, fibonacci + modified fibonacci traces "
+                         "at 2^k rows (0: skip)")
     ap.add_argument("--no-cpu-baseline", action="store_true")
     ap.add_argument("--cpu-sample-log", type=int, default=20,
                     help="log2 size of the CPU-baseline MSM sample (a prefix of the workload)")
@@ -219,6 +222,9 @@ def main():
     if args.log_logup > 0:
         out["logup"] = bench_logup(q, dev, args, barrier_sync, max_over_ranks, rank, world,
                                    traffic)
+    if args.log_hp_rows > 0:
+        out["hyperplonk"] = bench_hyperplonk(q, dev, args, barrier_sync, max_over_ranks, rank,
+                                             world)
     if rank == 0 and not args.no_cpu_baseline:
         out["cpu_baseline"] = cpu_baseline(args, srs, scalars)
         if not args.no_sumcheck:
@@ -357,6 +363,90 @@ def bench_logup(q, dev, args, barrier_sync, max_over_ranks, rank=0, world=1, tra
     for t in tabs + [out]:
         t.close()
     return res
+
+
+HP_PHASES = ("msm_bucketing", "msm_accumulate", "msm_reduce", "sumcheck_round", "sumcheck_tail",
+             "logup_column", "eq_table", "inner_product", "s_polynomial", "kzg_division")
+
+
+def bench_hyperplonk(q, dev, args, barrier_sync, max_over_ranks, rank=0, world=1):
+    """Config C5: HyperPlonk::prove (hyperplonk/src/proof/proof.rs:239-301) over
+    the reference's two test circuits (test_basic_proof.rs:17-105) scaled to
+    2^k rows: fibonacci (4 columns, trace 2^(k+2)) + modified fibonacci (5 -> 8
+    columns, trace 2^(k+3)); SRS max_degree 2^(k+3).  The witnesses are resident
+    in HBM before the timed region; constraint checks, commitments, zero-checks,
+    permutation checks and all ML-PCS openings are inside it.  With N ranks
+    each rank proves its own copy (replicas: one transcript orders the traces,
+    SURVEY §8(e)); value = proofs/s over all ranks."""
+    from quill_amd import KZG, HyperPlonk, TraceWitness
+    from quill_amd import examples as ex
+    k = args.log_hp_rows
+    rows = 1 << k
+    t0 = time.perf_counter()
+    cws = [ex.fibonacci_circuit_and_trace(rows), ex.modified_fibonacci_circuit_and_trace(rows)]
+    maxdeg = max(c.num_cols() * c.num_rows() for c, _ in cws)
+    pcs = KZG.trusted_setup(maxdeg, TAU, dev)
+    hp = HyperPlonk.preprocess([c for c, _ in cws], pcs)
+    wits = []
+    for c, w in cws:
+        full = q.DeviceVec(dev, rows * c.num_cols())
+        for i, col in enumerate(w):
+            q.DeviceVec.from_canonical(dev, col, out=full, offset=i * rows)
+        wits.append(TraceWitness.from_full(full, c.num_cols()))
+    del cws
+    setup_s = time.perf_counter() - t0
+    for _ in range(max(1, min(args.warmup, 1))):
+        proof = hp.prove(pcs, wits)
+    steps = max(1, min(args.steps, 2))
+    dev.enable_timing(True)
+    barrier_sync()
+    t0 = time.perf_counter()
+    for _ in range(steps):
+        proof = hp.prove(pcs, wits)
+    barrier_sync()
+    dt = max_over_ranks(time.perf_counter() - t0)
+    parts = {nm: dev.kernel_time(nm)[0] / steps for nm in HP_PHASES}
+    dev.enable_timing(False)
+    nopen = sum(len(tp.openings_zero_check) + len(tp.openings_public) + 5
+                for tp in proof.trace_proofs)
+    res = {"metric": f"HyperPlonk prove ms, fibonacci + modified-fibonacci traces at 2^{k} rows "
+                     f"(2^{k + 2} + 2^{k + 3} cells)",
+           "ms": dt / steps * 1e3, "higher_is_better": False,
+           "proofs_per_s": world * steps / dt, "steps": steps, "setup_s": setup_s,
+           "ml_openings_per_proof": nopen, "parts_ms_rank0": parts,
+           "final_transcript_state": hp.last_transcript.state.hex(),
+           "parallelism": f"replicas x{world}"}
+    if rank == 0 and not args.no_cpu_baseline:
+        res["cpu_baseline"] = cpu_baseline_hyperplonk()
+    for w in wits:
+        w.full.close()
+    for pk in hp.trace_pks:
+        for v in [pk.id_poly, pk.permutation_poly] + pk.public_values:
+            v.close()
+    pcs.srs.close()
+    return res
+
+
+def cpu_baseline_hyperplonk():
+    """The oracle's pure-Python restatement of the same prove (hyperplonk_oracle)
+    at 2^6 rows: a bounded sample; the reference (Rust) cannot run here."""
+    try:
+        sys.path.insert(0, os.path.join(ROOT, "oracle"))
+        import hyperplonk_oracle as ho
+        import quill_oracle as qo
+    except Exception as e:
+        return {"ms": None, "error": f"oracle unavailable: {e}"}
+    rows = 64
+    c1, w1 = ho.fibonacci_circuit_and_trace(rows)
+    c2, w2 = ho.modified_fibonacci_circuit_and_trace(rows)
+    pcs = qo.KZG(max(c1.num_cols(), c2.num_cols()) * rows, TAU)
+    hp = ho.HyperPlonk.preprocess([c1, c2], pcs)
+    t0 = time.perf_counter()
+    hp.prove(pcs, [w1, w2])
+    sec = time.perf_counter() - t0
+    return {"ms": sec * 1e3, "cores": 1, "kind": "port",
+            "sample": f"pure-Python oracle prove at {rows} rows (2^8 + 2^9 cells), single "
+                      "thread; not size-comparable (O(N^2) S polynomial, trapdoor KZG)"}
 
 
 def cpu_baseline_logup(args, tabs, out):

@@ -66,6 +66,16 @@ class TraceWitness:
 
     def __init__(self, columns):
         self.columns = list(columns)
+        self.full = None
+
+    @classmethod
+    def from_full(cls, full: DeviceVec, num_cols: int) -> "TraceWitness":
+        """A trace already resident in HBM as its full witness (column-major,
+        num_cols x rows): proving reads it in place."""
+        rows = full.n // num_cols
+        tw = cls([full.view(c * rows, rows) for c in range(num_cols)])
+        tw.full = full
+        return tw
 
     def __len__(self):
         return len(self.columns)
@@ -73,6 +83,9 @@ class TraceWitness:
     def to_device(self, dev: Device, rows: int) -> DeviceVec:
         """full witness (proof.rs:270) as one device vector"""
         from .field import fr_canonical_array
+        if self.full is not None:
+            assert self.full.n == rows * len(self.columns), "Padded witness length mismatch"
+            return self.full
         full = DeviceVec(dev, rows * len(self.columns))
         for c, col in enumerate(self.columns):
             assert len(col) == rows, "Witness column row length mismatch"
@@ -188,7 +201,8 @@ class HyperPlonk:
         proofs = []
         for full, vk, pk in zip(fulls, self.trace_vks, self.trace_pks):
             proofs.append(self.prove_trace(pcs, full, t, pk, vk.circuit))
-        for full in fulls:
-            full.close()
+        for tw, full in zip(witness_traces, fulls):
+            if not (isinstance(tw, TraceWitness) and tw.full is full):
+                full.close()  # uploaded here; a caller-resident trace stays
         self.last_transcript = t
         return HyperPlonkProof(comms, proofs)
