@@ -69,6 +69,19 @@ typedef struct qg_loopback qg_loopback;
 int qg_loopback_create(int world, qg_loopback** out);
 int qg_loopback_destroy(qg_loopback* lb);
 int qg_ctx_attach_loopback(qg_ctx* ctx, qg_loopback* lb, int rank);
+/* Allgather of `bytes` host bytes from every rank into recv (world * bytes, rank
+ * order) over the attached communicator: the host-side agreement steps of the
+ * sharded prover (constraint-check verdicts, boundary rows). */
+int qg_comm_allgather_host(qg_ctx* ctx, const void* send, size_t bytes, void* recv);
+/* The full witness of a trace, concat(columns) (hyperplonk/src/proof/proof.rs:270),
+ * as this rank's block: every rank passes its row block (rows / world entries)
+ * of each of the `ncols` columns and receives entries
+ * [rank * ncols * rows / world, (rank + 1) * ncols * rows / world) of the
+ * column-major flattening (exchanged with one RCCL allgather of the packed
+ * row blocks, then a local extraction).
+ * world == 1: the plain concatenation. */
+int qg_trace_full_witness(qg_ctx* ctx, const qg_buf* const* col_blocks, uint32_t ncols,
+                          uint64_t rows, qg_buf* full_block);
 
 /* ---------------------------------------------------------------- transcript */
 /* Transcript::new(domain)                  transcript/src/transcript.rs:14-22 */
@@ -193,7 +206,9 @@ int qg_mle_open_dev(qg_ctx* ctx, const qg_srs* srs, const qg_buf* poly, size_t n
  *  compute_pr (mlpcs.rs:68-78) == eq(bin(i), point) table, untrimmed (2^nvars) */
 int qg_eq_table(qg_ctx* ctx, const uint64_t* point, size_t nvars, uint64_t* out);
 /*  fast_eq_eval_hypercube (hyperplonk/src/utils/eq_eval.rs:6-31) into a device
- *  vector (first 2^nvars entries of `out`). */
+ *  vector (first 2^nvars entries of `out`).  With a communicator attached:
+ *  this rank's block, the 2^(nvars - log2 world) entries whose high index bits
+ *  equal the rank. */
 int qg_eq_table_dev(qg_ctx* ctx, const uint64_t* point, size_t nvars, qg_buf* out);
 /*  InnerProductProof::compute_s_polynomial (pcs/src/ipa.rs:122-157), untrimmed:
  *  out has max(nf, ng) - 1 entries (caller trims trailing zeros). */

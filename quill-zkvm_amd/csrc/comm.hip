@@ -14,6 +14,9 @@
 
 #include <rccl/rccl.h>
 
+#include <algorithm>
+#include <vector>
+
 #include "common.h"
 
 // In-process loopback group: `world` contexts driven by `world` host threads
@@ -76,6 +79,67 @@ void comm_allgather_bytes(qg_ctx* ctx, const void* d_send, void* d_recv, size_t 
   QG_NCCL(ncclAllGather(d_send, d_recv, bytes, ncclUint8, ctx->comm->comm, ctx->stream));
 }
 
+// One contiguous piece of a sharded column-major full witness: rows [a, b) of
+// column c travel from rank `src` (its row block of c) to rank `dst` (its block
+// of the flattened trace).
+struct TraceChunk {
+  uint32_t c, src, dst;
+  size_t a, b;
+};
+
+static std::vector<TraceChunk> trace_chunks(uint32_t ncols, size_t rows, int world) {
+  std::vector<TraceChunk> out;
+  const size_t RL = rows / world, B = (size_t)ncols * rows / world;
+  for (uint32_t c = 0; c < ncols; c++)
+    for (int src = 0; src < world; src++) {
+      size_t a = src * RL;
+      const size_t end = a + RL;
+      while (a < end) {  // split the source rows at destination-block boundaries
+        const size_t flat = (size_t)c * rows + a;
+        const uint32_t dst = (uint32_t)(flat / B);
+        const size_t dst_end_row = ((size_t)(dst + 1) * B) - (size_t)c * rows;
+        const size_t b = std::min(end, dst_end_row);
+        out.push_back({c, (uint32_t)src, dst, a, b});
+        a = b;
+      }
+    }
+  return out;
+}
+
+// full_block = this rank's block of concat(columns) (hyperplonk/src/proof/proof.rs:270),
+// from every rank's row block of each column
+void trace_full_witness(qg_ctx* ctx, const std::vector<const Fr*>& cols, size_t rows, Fr* full) {
+  const uint32_t ncols = (uint32_t)cols.size();
+  const int world = ctx->world, rank = ctx->rank;
+  if (world <= 1) {
+    for (uint32_t c = 0; c < ncols; c++)
+      QG_HIP(hipMemcpyAsync(full + (size_t)c * rows, cols[c], rows * sizeof(Fr),
+                            hipMemcpyDeviceToDevice, ctx->stream));
+    ctx->sync();
+    return;
+  }
+  QG_CHECK(ctx->comm, QG_ERR_COMM, "no communicator attached");
+  const size_t RL = rows / world, B = (size_t)ncols * rows / world;
+  // One allgather of every rank's packed row blocks (the collective the MSM
+  // already uses), then each rank copies out its block of the flattening.  The
+  // exchange moves the whole trace to every rank (N x the data of an
+  // all-to-all) but is a few ms next to the proof, over one well-trodden path.
+  const size_t per = (size_t)ncols * RL;
+  Fr* pack = ctx->scratch_as<Fr>("tw_pack", per);
+  Fr* all = ctx->scratch_as<Fr>("tw_all", per * world);
+  for (uint32_t c = 0; c < ncols; c++)
+    QG_HIP(hipMemcpyAsync(pack + (size_t)c * RL, cols[c], RL * sizeof(Fr), hipMemcpyDeviceToDevice,
+                          ctx->stream));
+  comm_allgather_bytes(ctx, pack, all, per * sizeof(Fr));
+  for (const TraceChunk& k : trace_chunks(ncols, rows, world)) {
+    if ((int)k.dst != rank) continue;
+    const Fr* src = all + (size_t)k.src * per + (size_t)k.c * RL + (k.a - (size_t)k.src * RL);
+    QG_HIP(hipMemcpyAsync(full + ((size_t)k.c * rows + k.a - (size_t)rank * B), src,
+                          (k.b - k.a) * sizeof(Fr), hipMemcpyDeviceToDevice, ctx->stream));
+  }
+  ctx->sync();
+}
+
 void comm_release(qg_ctx* ctx) {
   if (!ctx->comm) return;
   if (ctx->comm->comm) (void)ncclCommDestroy(ctx->comm->comm);
@@ -84,6 +148,8 @@ void comm_release(qg_ctx* ctx) {
 }
 
 }  // namespace qg
+
+using namespace qg;
 
 extern "C" {
 
@@ -115,6 +181,42 @@ int qg_ctx_attach_comm(qg_ctx* ctx, int rank, int world, const uint8_t unique_id
     memcpy(&id, unique_id, 128);
     ctx->comm = new qg_comm_state();
     QG_NCCL(ncclCommInitRank(&ctx->comm->comm, world, id, rank));
+  });
+}
+
+int qg_comm_allgather_host(qg_ctx* ctx, const void* send, size_t bytes, void* recv) {
+  if (!ctx || (!send && bytes) || (!recv && bytes)) return QG_ERR_INVALID;
+  return qg_guard(ctx, [&] {
+    if (bytes == 0) return;
+    QG_HIP(hipSetDevice(ctx->device));
+    uint8_t* d = ctx->scratch_as<uint8_t>("ag_host", bytes * (size_t)(ctx->world + 1));
+    QG_HIP(hipMemcpyAsync(d, send, bytes, hipMemcpyHostToDevice, ctx->stream));
+    comm_allgather_bytes(ctx, d, d + bytes, bytes);
+    QG_HIP(hipMemcpyAsync(recv, d + bytes, bytes * (size_t)ctx->world, hipMemcpyDeviceToHost,
+                          ctx->stream));
+    ctx->sync();
+  });
+}
+
+int qg_trace_full_witness(qg_ctx* ctx, const qg_buf* const* col_blocks, uint32_t ncols,
+                          uint64_t rows, qg_buf* full_block) {
+  if (!ctx || !col_blocks || !ncols || !full_block) return QG_ERR_INVALID;
+  return qg_guard(ctx, [&] {
+    QG_HIP(hipSetDevice(ctx->device));
+    const int world = ctx->world;
+    QG_CHECK(rows % world == 0 && ((size_t)ncols * rows) % world == 0, QG_ERR_INVALID,
+             "rows and cells must divide by the world size");
+    const size_t RL = rows / world, B = (size_t)ncols * rows / world;
+    QG_CHECK(full_block->n >= B, QG_ERR_INVALID, "full-witness block too short");
+    std::vector<const Fr*> cols;
+    for (uint32_t c = 0; c < ncols; c++) {
+      QG_CHECK(col_blocks[c] && col_blocks[c]->n >= RL, QG_ERR_INVALID,
+               "column block missing or too short");
+      QG_CHECK(col_blocks[c]->d + RL <= full_block->d || full_block->d + B <= col_blocks[c]->d,
+               QG_ERR_INVALID, "full witness aliases a column block");
+      cols.push_back(col_blocks[c]->d);
+    }
+    trace_full_witness(ctx, cols, rows, full_block->d);
   });
 }
 

@@ -1189,13 +1189,31 @@ int qg_eq_table(qg_ctx* ctx, const uint64_t* point, size_t nvars, uint64_t* out)
 }
 
 int qg_eq_table_dev(qg_ctx* ctx, const uint64_t* point, size_t nvars, qg_buf* out) {
-  if (!ctx || (!point && nvars) || !out || nvars > 34) return QG_ERR_INVALID;
+  if (!ctx || (!point && nvars) || !out || nvars > 40) return QG_ERR_INVALID;
   return qg_guard(ctx, [&] {
     QG_HIP(hipSetDevice(ctx->device));
-    QG_CHECK(out->n >= ((size_t)1 << nvars), QG_ERR_INVALID, "output buffer too short");
+    // with a communicator: this rank's block (high index bits = rank)
+    uint32_t lw = 0;
+    while ((1 << lw) < ctx->world) lw++;
+    QG_CHECK((1 << lw) == ctx->world, QG_ERR_INVALID, "world size must be a power of two");
+    QG_CHECK(nvars >= lw, QG_ERR_INVALID, "nvars must be at least log2(world)");
+    const uint32_t m = (uint32_t)nvars - lw;
+    const size_t N = (size_t)1 << m;
+    QG_CHECK(out->n >= N, QG_ERR_INVALID, "output buffer too short");
     Fr* d_z = ctx->scratch_as<Fr>("eq_z", nvars ? nvars : 1);
     fr_upload(ctx, d_z, point, nvars);
-    eq_table_device(ctx, d_z, (uint32_t)nvars, out->d);
+    eq_table_device(ctx, d_z, m, out->d);
+    if (lw) {
+      Fr f = Fr::one();
+      for (uint32_t j = m; j < nvars; j++) {
+        const Fr zj = fr_import(point + 4 * j);
+        f = f * ((((uint32_t)ctx->rank >> (j - m)) & 1u) ? zj : Fr::one() - zj);
+      }
+      Fr* d_f = ctx->scratch_as<Fr>("eq_f", 1);
+      QG_HIP(hipMemcpyAsync(d_f, &f, sizeof(Fr), hipMemcpyHostToDevice, ctx->stream));
+      hipLaunchKernelGGL(k_scale, dim3(div_up(N, 256)), dim3(256), 0, ctx->stream, out->d, N, d_f);
+      QG_LAUNCH_CHECK();
+    }
     ctx->sync();
   });
 }

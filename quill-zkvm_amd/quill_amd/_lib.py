@@ -61,6 +61,8 @@ PROTOTYPES = {
     "qg_loopback_create": (C.c_int, [C.c_int, C.POINTER(P)]),
     "qg_loopback_destroy": (C.c_int, [P]),
     "qg_ctx_attach_loopback": (C.c_int, [P, P, C.c_int]),
+    "qg_comm_allgather_host": (C.c_int, [P, P, SZ, P]),
+    "qg_trace_full_witness": (C.c_int, [P, C.POINTER(P), C.c_uint32, C.c_uint64, P]),
     "qg_transcript_new": (C.c_int, [C.c_char_p, SZ, U8P]),
     "qg_transcript_append": (C.c_int, [U8P, C.c_char_p, SZ]),
     "qg_transcript_draw": (C.c_int, [U8P, U8P, SZ]),

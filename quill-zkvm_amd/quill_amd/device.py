@@ -16,6 +16,7 @@ class Device:
         self.h = C.c_void_p()
         check(lib().qg_ctx_create(device, C.byref(self.h)))
         self.device = device
+        self.rank, self.world = 0, 1
 
     def close(self):
         if self.h:
@@ -31,14 +32,32 @@ class Device:
     def attach_comm(self, rank: int, world: int, unique_id: bytes):
         buf = (C.c_uint8 * 128).from_buffer_copy(unique_id)
         check(lib().qg_ctx_attach_comm(self.h, rank, world, buf), self.h)
+        self.rank, self.world = rank, world
 
-    def attach_loopback(self, group, rank: int):
+    def attach_loopback(self, group, rank: int, world: int = None):
         check(lib().qg_ctx_attach_loopback(self.h, group, rank), self.h)
+        self.rank = rank
+        self.world = world if world is not None else self._loopback_worlds.get(
+            group.value if hasattr(group, "value") else group, 1)
+
+    _loopback_worlds = {}
+
+    def allgather_bytes(self, data: bytes) -> list:
+        """every rank's `data` (equal lengths), in rank order (qg_comm_allgather_host)"""
+        n = len(data)
+        if self.world == 1 or n == 0:
+            return [bytes(data)]
+        src = C.create_string_buffer(bytes(data), n)
+        dst = C.create_string_buffer(n * self.world)
+        check(lib().qg_comm_allgather_host(self.h, src, n, dst), self.h)
+        raw = dst.raw
+        return [raw[i * n:(i + 1) * n] for i in range(self.world)]
 
     @staticmethod
     def loopback_group(world: int):
         g = C.c_void_p()
         check(lib().qg_loopback_create(world, C.byref(g)))
+        Device._loopback_worlds[g.value] = world
         return g
 
     @staticmethod
@@ -66,7 +85,7 @@ class Device:
         """fast_eq_eval_hypercube (eq_eval.rs:6-31) into a device vector"""
         n = len(point)
         pt = fr_array(point) if n else np.zeros((1, 4), dtype=np.uint64)
-        out = out if out is not None else DeviceVec(self, 1 << n)
+        out = out if out is not None else DeviceVec(self, (1 << n) // self.world)
         check(lib().qg_eq_table_dev(self.h, u64p(pt), n, out.h), self.h)
         return out
 

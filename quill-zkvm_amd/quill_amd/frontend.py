@@ -94,12 +94,16 @@ class TransitionCircuit:
         return pub
 
     def public_values_dev(self, dev: Device, length: int = None):
-        """public_values() zero-padded to `length` rows, as device vectors"""
+        """public_values() zero-padded to `length` rows, as device vectors
+        (with a communicator attached: this rank's block of each)"""
         length = self.num_rows() if length is None else length
+        B = length // dev.world
+        lo = dev.rank * B
         out = []
         for row, _ in self.boundary_constraints:
-            v = np.zeros(length, dtype=np.uint64)
-            v[row] = 1
+            v = np.zeros(B, dtype=np.uint64)
+            if lo <= row < lo + B:
+                v[row - lo] = 1
             out.append(DeviceVec.from_u64(dev, v))
         return out
 
@@ -131,31 +135,62 @@ class TransitionCircuit:
         return [int(x) for x in ids], [int(x) for x in perm]
 
     def check_constraints(self, witness) -> None:
-        """:153-204 on device-resident columns (list of DeviceVec of num_rows
-        entries); raises ValueError on the first violation, in the reference's
-        order (recurring, boundary, permutation)."""
+        """:153-204 on device-resident columns (list of DeviceVec: all num_rows
+        entries, or with a communicator attached this rank's row block of each
+        column); raises ValueError on the first violation, in the reference's
+        order (recurring, boundary, permutation).  Sharded, every rank reaches
+        the same verdict: first bad rows are allgathered, and the copy
+        constraint across a block boundary uses the next rank's first row."""
         rows = self.num_rows()
         nv = rows.bit_length() - 1
         dev = witness[0].dev
+        RL = rows // dev.world
+        base = dev.rank * RL
         ptrs = (C.c_void_p * len(witness))(*[w.h for w in witness])
-        first = None
+
+        def global_min(local):  # smallest non-negative over ranks, or -1
+            vals = [int.from_bytes(b, "little", signed=True)
+                    for b in dev.allgather_bytes(int(local).to_bytes(8, "little", signed=True))]
+            vals = [v for v in vals if v >= 0]
+            return min(vals) if vals else -1
+
+        first = -1
         for c in self.recurring_constraints:
             prog, plen, carr, nc = _program_c(c)
             r = C.c_int64()
             check(lib().qg_expr_first_nonzero_dev(
                 dev.h, nv, len(witness), ptrs, prog, plen,
                 carr.ctypes.data_as(C.POINTER(C.c_uint64)), nc, C.byref(r)), dev.h)
-            if r.value >= 0 and (first is None or r.value < first):
-                first = r.value
-        if first is not None:
+            if r.value >= 0 and (first < 0 or base + r.value < first):
+                first = base + r.value
+        first = global_min(first)
+        if first >= 0:
             raise ValueError(f"Recurring constraint not satisfied at row {first}")
-        for row, c in self.boundary_constraints:
-            vals = [fr_from_mont_limbs(list(w.view(row, 1).to_numpy()[0])) for w in witness]
-            if c.evaluate(vals) != 0:
+        for i, (row, c) in enumerate(self.boundary_constraints):
+            bad = 0
+            if base <= row < base + RL:
+                vals = [fr_from_mont_limbs(list(w.view(row - base, 1).to_numpy()[0]))
+                        for w in witness]
+                bad = 1 if c.evaluate(vals) != 0 else 0
+            if global_min(row if bad else -1) >= 0:
                 raise ValueError(f"Boundary constraint {c} not satisfied at row {row}")
+        first = -1
         for sc in self.state_cells:
             cur, nxt = witness[sc.current.col], witness[sc.next.col]
-            bad = nxt.first_mismatch(cur, 0, 1, rows - 1)
+            bad = nxt.first_mismatch(cur, 0, 1, RL - 1)
             if bad >= 0:
-                raise ValueError(f"Permutation constraint not satisfied for state cell at row "
-                                 f"{bad}")
+                bad += base
+            if dev.world > 1:  # every rank joins the allgather
+                # next(last row of this block) == current(first row of the next block)
+                firsts = dev.allgather_bytes(cur.view(0, 1).to_numpy().tobytes())
+                if bad < 0 and dev.rank + 1 < dev.world:
+                    mine = nxt.view(RL - 1, 1).to_numpy().tobytes()
+                    if mine != firsts[dev.rank + 1]:
+                        bad = base + RL - 1
+            if bad >= 0 and (first < 0 or bad < first):
+                first = bad
+        # (every rank runs the same allgathers above: the loop shape is rank-independent)
+        first = global_min(first)
+        if first >= 0:
+            raise ValueError(f"Permutation constraint not satisfied for state cell at row "
+                             f"{first}")

@@ -104,8 +104,14 @@ class VirtualPolynomialStore:
     def on_device(self) -> bool:
         return self.dev is not None
 
+    @property
+    def local_len(self) -> int:
+        """entries per table held here: 2^num_vars, or this rank's block of
+        2^num_vars / world with a communicator attached"""
+        return (1 << self.num_vars) // (self.dev.world if self.dev is not None else 1)
+
     def allocate_polynomial(self, evals):
-        assert len(evals) == 1 << self.num_vars, \
+        assert len(evals) == self.local_len, \
             "Input polynomial evaluations length does not match number of variables"
         if self.dev is not None:
             if not isinstance(evals, DeviceVec):

@@ -41,7 +41,7 @@ def logup_column(store: VirtualPolynomialStore, h, beta: int, m=None, dev: Devic
     QuillGpuError(QG_ERR_ASSERT) on a zero denominator, where the reference
     panics in inverse().unwrap()."""
     if store.on_device:
-        out = DeviceVec(store.dev, 1 << store.num_vars)
+        out = DeviceVec(store.dev, store.local_len)
         s = logup_column_device(store.dev, store.num_vars, store.polynomials,
                                 store.virtual_polys[h], beta, out,
                                 store.virtual_polys[m] if m is not None else None)
@@ -187,7 +187,7 @@ class PermutationCheckProof:
               transcript: Transcript, pcs):
         """permutation_check.rs:13-59 -> (proof, evaluation point)."""
         n = store.num_vars
-        assert len(id_indices) == 1 << n and len(permutation_indices) == 1 << n
+        assert len(id_indices) == store.local_len and len(permutation_indices) == store.local_len
         id_ref = store.allocate_polynomial(id_indices)
         perm_ref = store.allocate_polynomial(permutation_indices)
         alpha = transcript.draw_field_element()

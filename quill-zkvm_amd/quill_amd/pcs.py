@@ -61,15 +61,45 @@ class KZG:
     (kzg.rs:35-59 with an explicit tau instead of an rng; MultilinearPCS's
     thread_rng setup (mlpcs.rs:178-182) is not reproducible and is not offered)."""
 
-    def __init__(self, dev: Device, srs: Srs, max_degree: int):
+    def __init__(self, dev: Device, srs: Srs, max_degree: int, tau: int = None, g=None):
         self.dev = dev
         self.srs = srs
         self._max_degree = max_degree
+        self._tau, self._g = tau, g
+        self._shards = {}
 
     @classmethod
     def trusted_setup(cls, max_degree: int, tau: int, dev: Device = None, g=None):
+        """With a communicator attached (dev.world > 1) the SRS is held as shards:
+        a polynomial of global length L is split over the ranks (rank r owns
+        entries [r L/world, (r+1) L/world)) and each rank keeps the matching
+        slice [tau^(r L/world + i)] g of the bases, generated on first use per L."""
         dev = dev or Device(0)
-        return cls(dev, Srs.generate(dev, tau, max_degree + 1, g), max_degree)
+        if dev.world > 1:
+            return cls(dev, None, max_degree, tau, g)
+        return cls(dev, Srs.generate(dev, tau, max_degree + 1, g), max_degree, tau, g)
+
+    def srs_for(self, n_local: int) -> Srs:
+        """the bases a local vector of n_local entries is committed against"""
+        if self.dev.world == 1:
+            return self.srs
+        if self.srs is not None and len(self.srs) == n_local:
+            return self.srs  # a caller-provided shard of this length
+        L = n_local * self.dev.world
+        if L > self._max_degree + 1:
+            raise QuillGpuError(-1, "Polynomial degree exceeds max degree")
+        if self._tau is None:
+            raise QuillGpuError(-4, "sharded commitments need a generated (tau) SRS")
+        if n_local not in self._shards:
+            self._shards[n_local] = Srs.generate(self.dev, self._tau, n_local, self._g,
+                                                 offset=self.dev.rank * n_local)
+        return self._shards[n_local]
+
+    def close(self):
+        for s in [self.srs] + list(self._shards.values()):
+            if s is not None:
+                s.close()
+        self._shards = {}
 
     @classmethod
     def from_points(cls, g1_points, dev: Device = None):
@@ -85,7 +115,7 @@ class KZG:
         if len(poly) > self._max_degree + 1:
             raise QuillGpuError(-1, "Polynomial degree exceeds max degree")
         if isinstance(poly, DeviceVec):
-            return self.srs.msm_dev(poly, len(poly))
+            return self.srs_for(len(poly)).msm_dev(poly, len(poly))
         arr = fr_array(poly) if len(poly) else np.zeros((1, 4), dtype=np.uint64)
         xy = (C.c_uint64 * 8)()
         inf = C.c_uint8()
@@ -106,7 +136,8 @@ class KZG:
         """open() on the first n entries of a device-resident DeviceVec"""
         pt = fr_array(eval_point) if len(eval_point) else np.zeros((1, 4), dtype=np.uint64)
         out = MleProof()
-        check(lib().qg_mle_open_dev(self.dev.h, self.srs.h, vec.h, n, u64p(pt), len(eval_point),
+        check(lib().qg_mle_open_dev(self.dev.h, self.srs_for(n).h, vec.h, n, u64p(pt),
+                                    len(eval_point),
                                     transcript.c_state(), C.byref(out)), self.dev.h)
         return MLEvalProof(list(eval_point), fr_from_mont_limbs(list(out.evaluation)),
                            g1_from_abi(out.s_comm_xy, out.s_comm_inf),

@@ -11,10 +11,12 @@ device vectors.  The verifier is not mirrored (CPU-only in the reference's
 model; the oracle's restatement checks these proofs in tests)."""
 from __future__ import annotations
 
+import ctypes as C
 from dataclasses import dataclass, field
 
 import numpy as np
 
+from ._lib import check, lib
 from .device import Device, DeviceVec
 from .field import R_MOD
 from .frontend import TransitionCircuit
@@ -54,15 +56,21 @@ class TraceVK:
 
 @dataclass
 class TracePK:
-    """proof.rs:50-54 (device vectors of 2^trace_num_vars entries)"""
+    """proof.rs:50-54 (device vectors of 2^trace_num_vars entries, or this
+    rank's blocks of them).  `public_rows`: the unpadded public columns
+    (circuit.public_values(), num_rows entries or this rank's row block) that
+    the zero-check store and the public openings use."""
     id_poly: DeviceVec
     permutation_poly: DeviceVec
     public_values: list = field(default_factory=list)
+    public_rows: list = field(default_factory=list)
 
 
 class TraceWitness:
-    """proof.rs:60: the trace's columns.  Accepted column forms: DeviceVec,
-    (rows, 4) uint64 numpy arrays of canonical limbs, or lists of ints."""
+    """proof.rs:60: the trace's columns.  Host columns (all num_rows entries):
+    (rows, 4) uint64 numpy arrays of canonical limbs or lists of ints.  Device
+    columns: DeviceVec of num_rows entries, or with a communicator attached
+    this rank's row block (rows / world entries) of each column."""
 
     def __init__(self, columns):
         self.columns = list(columns)
@@ -70,8 +78,8 @@ class TraceWitness:
 
     @classmethod
     def from_full(cls, full: DeviceVec, num_cols: int) -> "TraceWitness":
-        """A trace already resident in HBM as its full witness (column-major,
-        num_cols x rows): proving reads it in place."""
+        """A single-GPU trace already resident in HBM as its full witness
+        (column-major, num_cols x rows): proving reads it in place."""
         rows = full.n // num_cols
         tw = cls([full.view(c * rows, rows) for c in range(num_cols)])
         tw.full = full
@@ -80,21 +88,44 @@ class TraceWitness:
     def __len__(self):
         return len(self.columns)
 
-    def to_device(self, dev: Device, rows: int) -> DeviceVec:
-        """full witness (proof.rs:270) as one device vector"""
+    def to_device(self, dev: Device, rows: int):
+        """-> (column blocks, full-witness block, owned buffers).  The full
+        witness (proof.rs:270) is the column-major concatenation; sharded, each
+        rank holds the row block of every column (zero-check) and its block of
+        the flattening (permutation check, openings), exchanged by one
+        all-to-all (qg_trace_full_witness)."""
         from .field import fr_canonical_array
+        ncols = len(self.columns)
         if self.full is not None:
-            assert self.full.n == rows * len(self.columns), "Padded witness length mismatch"
-            return self.full
-        full = DeviceVec(dev, rows * len(self.columns))
-        for c, col in enumerate(self.columns):
-            assert len(col) == rows, "Witness column row length mismatch"
-            if isinstance(col, DeviceVec):
-                full.copy_from(col, c * rows, 0, rows)
-            else:
-                arr = col if isinstance(col, np.ndarray) else fr_canonical_array(col)
-                DeviceVec.from_canonical(dev, arr, out=full, offset=c * rows)
-        return full
+            assert dev.world == 1 and self.full.n == rows * ncols, "Padded witness length mismatch"
+            return self.columns, self.full, []
+        owned = []
+        RL = rows // dev.world
+        lo = dev.rank * RL
+        if all(isinstance(c, DeviceVec) for c in self.columns):
+            cols = self.columns
+            for col in cols:
+                assert len(col) == RL, "Witness column row length mismatch"
+        else:
+            store = DeviceVec(dev, RL * ncols)
+            owned.append(store)
+            cols = [store.view(c * RL, RL) for c in range(ncols)]
+            for c, col in enumerate(self.columns):
+                assert len(col) == rows, "Witness column row length mismatch"
+                if isinstance(col, DeviceVec):
+                    cols[c].copy_from(col, 0, lo if col.n == rows else 0, RL)
+                else:
+                    arr = col if isinstance(col, np.ndarray) else fr_canonical_array(col[lo:lo + RL])
+                    if isinstance(col, np.ndarray):
+                        arr = arr[lo:lo + RL]
+                    DeviceVec.from_canonical(dev, arr, out=store, offset=c * RL)
+        if dev.world == 1 and owned:
+            return cols, owned[0], owned  # the column store IS the flattening
+        full = DeviceVec(dev, rows * ncols // dev.world)
+        owned.append(full)
+        ptrs = (C.c_void_p * ncols)(*[c.h for c in cols])
+        check(lib().qg_trace_full_witness(dev.h, ptrs, ncols, rows, full.h), dev.h)
+        return cols, full, owned
 
 
 def _log2(n: int) -> int:
@@ -114,15 +145,26 @@ class HyperPlonk:
         assert rows & (rows - 1) == 0, "Number of rows must be a power of two"
         assert cols & (cols - 1) == 0, "Number of columns must be a power of two"
         N = rows * cols
-        pub = circuit.public_values_dev(pcs.dev, N)  # padded with zeros (:76-85)
-        pub_comms = [pcs.commit(p) for p in pub]
+        dev = pcs.dev
+        if dev.world == 1:
+            pub = circuit.public_values_dev(dev, N)  # padded with zeros (:76-85)
+            pub_rows = [p.view(0, rows) for p in pub]
+            pub_comms = [pcs.commit(p) for p in pub]
+        else:
+            # sharded: only the unpadded row blocks are kept; the commitment of
+            # the zero-padded column is the same group element (zeros add nothing)
+            pub = []
+            pub_rows = circuit.public_values_dev(dev, rows)
+            pub_comms = [pcs.commit(p) for p in pub_rows]
         ids, perm = circuit.permutation_u64()
         assert len(ids) == N, "ID polynomial length mismatch"
         assert len(perm) == N, "Permutation polynomial length mismatch"
-        id_dev = DeviceVec.from_u64(pcs.dev, ids)
-        perm_dev = DeviceVec.from_u64(pcs.dev, perm)
+        B = N // dev.world
+        sl = slice(dev.rank * B, (dev.rank + 1) * B)
+        id_dev = DeviceVec.from_u64(dev, ids[sl])
+        perm_dev = DeviceVec.from_u64(dev, perm[sl])
         vk = TraceVK(circuit, pub_comms, pcs.commit(id_dev), pcs.commit(perm_dev))
-        return TracePK(id_dev, perm_dev, pub), vk
+        return TracePK(id_dev, perm_dev, pub, pub_rows), vk
 
     @staticmethod
     def preprocess(circuits, pcs: KZG) -> "HyperPlonk":
@@ -138,17 +180,18 @@ class HyperPlonk:
         """proof.rs:139-143"""
         return list(self.trace_vks)
 
-    def prove_trace(self, pcs: KZG, full: DeviceVec, transcript: Transcript, pk: TracePK,
-                    circuit: TransitionCircuit) -> TraceProof:
-        """proof.rs:145-237"""
+    def prove_trace(self, pcs: KZG, columns, full: DeviceVec, transcript: Transcript,
+                    pk: TracePK, circuit: TransitionCircuit) -> TraceProof:
+        """proof.rs:145-237 (`columns`: the witness columns on the device, or
+        this rank's row blocks; `full`: the full witness or this rank's block)"""
         dev = pcs.dev
         rows, cols = circuit.num_rows(), circuit.num_cols()
         log2_rows, log2_cols = _log2(rows), _log2(cols)
         store = VirtualPolynomialStore(log2_rows, dev)
         for c in range(cols):
-            store.allocate_polynomial(full.view(c * rows, rows))
-        for p in pk.public_values:  # circuit.public_values(): the first `rows` entries
-            store.allocate_polynomial(p.view(0, rows))
+            store.allocate_polynomial(columns[c])
+        for p in pk.public_rows:  # circuit.public_values()
+            store.allocate_polynomial(p)
         exprs = circuit.zero_check_expressions()
         alpha = transcript.draw_field_element()
         E = VirtualPolyExpr
@@ -168,12 +211,11 @@ class HyperPlonk:
         for col in range(cols):
             point = list(zclaim.point) + [(col >> i) & 1 for i in range(log2_cols)]
             open_zc.append(pcs.open(full, point, transcript))
-        open_pub = [pcs.open(p.view(0, rows), zclaim.point, transcript)
-                    for p in pk.public_values]
+        open_pub = [pcs.open(p, zclaim.point, transcript) for p in pk.public_rows]
         o_id = pcs.open(pk.id_poly, ppoint, transcript)
         o_perm = pcs.open(pk.permutation_poly, ppoint, transcript)
         o_pt = pcs.open(full, ppoint, transcript)
-        for p in store.polynomials[cols + len(pk.public_values):]:
+        for p in store.polynomials[cols + len(pk.public_rows):]:
             p.close()  # eq table (zero-check)
         for p in store2.polynomials[3:]:
             p.close()  # Logup columns + eq table (permutation check)
@@ -184,25 +226,23 @@ class HyperPlonk:
         """proof.rs:239-301.  `witness_traces`: TraceWitness (or column lists),
         one per circuit."""
         t = transcript if transcript is not None else Transcript(b"hyperplonk_proof")
-        comms, fulls = [], []
+        comms, layouts, owned = [], [], []
         for tw, vk in zip(witness_traces, self.trace_vks):
             tw = tw if isinstance(tw, TraceWitness) else TraceWitness(tw)
             circuit = vk.circuit
             assert len(tw) == circuit.num_cols(), "Witness columns length mismatch"
-            rows = circuit.num_rows()
-            full = tw.to_device(pcs.dev, rows)
+            cols, full, own = tw.to_device(pcs.dev, circuit.num_rows())
+            owned += own
             if check_constraints:
-                circuit.check_constraints([full.view(c * rows, rows)
-                                           for c in range(circuit.num_cols())])
-            C = pcs.commit(full)
-            t.append_g1(C)
-            comms.append(C)
-            fulls.append(full)
+                circuit.check_constraints(cols)
+            Cm = pcs.commit(full)
+            t.append_g1(Cm)
+            comms.append(Cm)
+            layouts.append((cols, full))
         proofs = []
-        for full, vk, pk in zip(fulls, self.trace_vks, self.trace_pks):
-            proofs.append(self.prove_trace(pcs, full, t, pk, vk.circuit))
-        for tw, full in zip(witness_traces, fulls):
-            if not (isinstance(tw, TraceWitness) and tw.full is full):
-                full.close()  # uploaded here; a caller-resident trace stays
+        for (cols, full), vk, pk in zip(layouts, self.trace_vks, self.trace_pks):
+            proofs.append(self.prove_trace(pcs, cols, full, t, pk, vk.circuit))
+        for b in owned:
+            b.close()  # built here; caller-resident traces stay
         self.last_transcript = t
         return HyperPlonkProof(comms, proofs)

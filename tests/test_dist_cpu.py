@@ -135,3 +135,78 @@ def test_sharded_protocols_gloo(world):
     assert sorted(r[0] for r in results) == list(range(world))
     assert all(r[1] for r in results), results
     assert all(r[2] for r in results), results
+
+
+def trace_chunks(ncols, rows, world):
+    """csrc/comm.hip trace_chunks: rows [a, b) of column c go from rank src
+    (its row block) to rank dst (its block of the column-major flattening)."""
+    RL, B = rows // world, ncols * rows // world
+    out = []
+    for c in range(ncols):
+        for src in range(world):
+            a, end = src * RL, (src + 1) * RL
+            while a < end:
+                dst = (c * rows + a) // B
+                b = min(end, (dst + 1) * B - c * rows)
+                out.append((c, src, dst, a, b))
+                a = b
+    return out
+
+
+def _trace_worker(rank, world, port, q):
+    """qg_trace_full_witness's exchange (allgather of packed row blocks, local
+    extraction) and the sharded check_constraints boundary exchange."""
+    os.environ["MASTER_ADDR"] = "127.0.0.1"
+    os.environ["MASTER_PORT"] = str(port)
+    dist.init_process_group("gloo", rank=rank, world_size=world)
+    try:
+        ok = True
+        for ncols, rows in ((8, 64), (4, 32), (2, 16), (1, 8)):
+            cols = [[1000 * c + r for r in range(rows)] for c in range(ncols)]
+            RL, B = rows // world, ncols * rows // world
+            mine = [col[rank * RL:(rank + 1) * RL] for col in cols]
+            packed = [v for blk in mine for v in blk]
+            allp = _allgather_obj(packed, world)
+            full = [None] * B
+            for c, src, dst, a, b in trace_chunks(ncols, rows, world):
+                if dst != rank:
+                    continue
+                for i in range(a, b):
+                    full[c * rows + i - rank * B] = allp[src][c * RL + i - src * RL]
+            flat = [v for col in cols for v in col]
+            ok &= full == flat[rank * B:(rank + 1) * B]
+        # copy constraint across the block boundary: next(last row of block r)
+        # vs current(first row of block r + 1), via an allgather of first rows
+        rows = 16
+        RL = rows // world
+        cur = list(range(1, rows + 1))
+        nxt = cur[1:] + [0]
+        nxt[RL - 1] += 1  # break the constraint at the boundary of blocks 0 / 1
+        firsts = _allgather_obj(cur[rank * RL], world)
+        bad = -1
+        for i in range(RL - 1):
+            if nxt[rank * RL + i] != cur[rank * RL + i + 1]:
+                bad = rank * RL + i
+                break
+        if bad < 0 and rank + 1 < world and nxt[rank * RL + RL - 1] != firsts[rank + 1]:
+            bad = rank * RL + RL - 1
+        verdicts = [v for v in _allgather_obj(bad, world) if v >= 0]
+        ok &= verdicts == [RL - 1]
+        q.put((rank, ok))
+    finally:
+        dist.destroy_process_group()
+
+
+@pytest.mark.parametrize("world", [2, 4])
+def test_sharded_trace_exchange_gloo(world):
+    ctx = mp.get_context("spawn")
+    q = ctx.Queue()
+    port = _free_port()
+    procs = [ctx.Process(target=_trace_worker, args=(r, world, port, q)) for r in range(world)]
+    for p in procs:
+        p.start()
+    results = [q.get(timeout=300) for _ in range(world)]
+    for p in procs:
+        p.join(timeout=60)
+    assert sorted(r[0] for r in results) == list(range(world))
+    assert all(r[1] for r in results), results
