@@ -9,8 +9,10 @@ commitment is to a degree N*2^24 polynomial: rank r owns bases/scalars
 allgather (weak scaling; value = N*2^24 / max-over-ranks time).
 
 Alongside, the sumcheck prover (SumcheckProof::prove, h = g1*g2*g3, degree 3)
-at 2^20 variables is timed on each rank (replicas) and reported in
-`sumcheck` with its own HBM roofline.  The CPU baseline is the oracle's C
+at 2^20 variables is reported in `sumcheck` with its own HBM roofline (with N
+ranks the 2^20 tables are sharded by the high index bits: strong scaling), and
+configs C4 (ML-PCS commit + open, 2^22), the Logup column and C5 (HyperPlonk
+prove, 2^20-row traces) get their own entries.  The CPU baseline is the oracle's C
 restatement of the reference algorithm (single thread, like the reference,
 which has no rayon), timed on a bounded sample on rank 0.
 
@@ -241,7 +243,8 @@ def main():
 def bench_sumcheck(q, dev, args, barrier_sync, max_over_ranks, rank):
     from quill_amd.hyperplonk import VirtualPolyExpr as E, sumcheck_prove_device
     nv = args.log_sumcheck
-    N = 1 << nv
+    world = dev.world
+    N = (1 << nv) // world  # this rank's block of every table (sharded by the high bits)
     tabs = [q.DeviceVec(dev, N).fill_random(0x5155494C4C + 3 + 7 * i + 100 * rank) for i in range(3)]
     expr = E.Input(0) * E.Input(1) * E.Input(2)
     claimed = 0  # the prover is deterministic in its inputs; the claim is absorbed as-is
@@ -262,7 +265,9 @@ def bench_sumcheck(q, dev, args, barrier_sync, max_over_ranks, rank):
         t.close()
     # algorithmic bytes: round j reads k*32*2^(n-j) B, writes half that
     k = 3
-    total_bytes = sum(k * 32 * (N >> j) + (k * 32 * (N >> j) // 2 if j > 0 else 0) for j in range(nv))
+    NG = 1 << nv
+    total_bytes = sum(k * 32 * (NG >> j) + (k * 32 * (NG >> j) // 2 if j > 0 else 0)
+                      for j in range(nv))
     per_call_gbps = total_bytes / (ms * 1e-3) / 1e9
     return {"metric": f"sumcheck-prover ms at 2^{nv} vars (h = g1*g2*g3, degree 3)",
             "ms": ms, "higher_is_better": False,
@@ -270,6 +275,7 @@ def bench_sumcheck(q, dev, args, barrier_sync, max_over_ranks, rank):
                          "achieved": per_call_gbps, "peak": HBM_PEAK_GBPS, "unit": "GB/s",
                          "frac": per_call_gbps / HBM_PEAK_GBPS, "traffic": None,
                          "algorithmic_bytes": total_bytes},
+            "parallelism": f"sharded x{world} (strong scaling)" if world > 1 else "single GPU",
             "round_kernels_ms_per_call": rk_ms / max(args.steps, 1),
             "tail_kernel_ms_per_call": tl_ms / max(args.steps, 1)}
 

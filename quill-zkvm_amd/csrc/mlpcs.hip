@@ -15,10 +15,13 @@
 //  * Every commitment is the device MSM (msm.hip) over device-resident data.
 #include <string.h>
 
+#include <algorithm>
+#include <string>
 #include <vector>
 
 #include "blake3.h"
 #include "common.h"
+#include "field29.h"
 
 using namespace qg;
 
@@ -142,76 +145,151 @@ static void suffix_horner(qg_ctx* ctx, const Fr* c, size_t L, const Fr& x, Fr* s
 }
 
 // ---------------------------------------------------------------- NTT
-__global__ void k_bitrev_copy(const Fr* __restrict__ in, size_t nin, Fr* __restrict__ out,
-                              int logn, int reverse_input, size_t rev_len) {
-  size_t i = (size_t)blockIdx.x * blockDim.x + threadIdx.x;
-  size_t n = (size_t)1 << logn;
-  if (i >= n) return;
-  size_t j = __brevll((unsigned long long)i) >> (64 - logn);
-  Fr v = Fr::zero();
-  // source element i (optionally of the reversed length-rev_len sequence)
-  size_t src = i;
-  bool ok = true;
-  if (reverse_input) {
-    if (i < rev_len) src = rev_len - 1 - i;
-    else ok = false;
+// Radix-2 NTT passes of up to 11 stages each on LDS tiles of 2048 elements
+// held as 9 x 29-bit limbs (SoA: conflict-free), so a 2^23-point transform is
+// three HBM round trips instead of one per stage.  A pass over stages
+// [s0, s0 + B) works on tiles of 2^B "mid" indices x L consecutive "lo"
+// indices (L = 2048 / 2^B): element (mid, l) is index
+//   hi 2^(s0+B) + mid 2^s0 + lo0 + l,
+// so every global access is a run of L consecutive Fr (L >= 16 above the first
+// pass).  Forward: DIF (natural in, bit-reversed out); inverse: DIT
+// (bit-reversed in, natural out) -- no bit-reversal pass at all.  Data stay in
+// arkworks form (x 2^256): twiddles are stored as w^k 2^261, so mul29 keeps the
+// scale.  Every value is < 2p inside a pass, canonical (< p) when stored.
+static constexpr int NTT_T = 2048;      // elements per tile
+static constexpr int NTT_LGT = 11;
+static constexpr int NTT_THREADS = 256;
+using R29 = F29<FrP>;
+
+struct NttPass {
+  int s0, B, lgL;
+};
+
+// stage ranges: [0, min(11, logn)) first (contiguous tiles), then chunks of at
+// most 7 stages (runs of >= 16 elements)
+static std::vector<NttPass> ntt_plan(int logn) {
+  std::vector<NttPass> v;
+  int s = 0;
+  while (s < logn) {
+    const int B = std::min(s == 0 ? NTT_LGT : 7, logn - s);
+    int lgL = std::min(NTT_LGT - B, s);  // L <= 2^s0 (lo range)
+    lgL = std::min(lgL, logn - B);       // tile <= n
+    v.push_back({s, B, lgL});
+    s += B;
   }
-  if (ok && src < nin) v = in[src];
-  out[j] = v;
+  return v;
 }
 
-// radix-2 DIT stages with half-span m < 512 done in LDS on 1024-element tiles
-__global__ void __launch_bounds__(512)
-    k_ntt_tile(Fr* __restrict__ a, const Fr* __restrict__ tw, int logn, int stages) {
-  __shared__ Fr sh[1024];
-  const size_t base = (size_t)blockIdx.x * 1024;
-  sh[threadIdx.x] = a[base + threadIdx.x];
-  sh[threadIdx.x + 512] = a[base + threadIdx.x + 512];
+QG_DEV R29 lds_get29(const uint32_t* sh, int e) {
+  R29 r;
+#pragma unroll
+  for (int i = 0; i < 9; i++) r.l[i] = sh[i * NTT_T + e];
+  return r;
+}
+QG_DEV void lds_put29(uint32_t* sh, int e, const R29& v) {
+#pragma unroll
+  for (int i = 0; i < 9; i++) sh[i * NTT_T + e] = v.l[i];
+}
+
+// DIF (forward) or DIT (inverse) stages [s0, s0+B) on every tile.
+//   in:  n entries (entries >= nin read as zero)
+//   out: n entries, or only indices [win_lo, win_hi) written to out - win_lo
+//   tw:  w^k 2^261 (Fr words), k < n/2
+template <bool DIF>
+__global__ void __launch_bounds__(NTT_THREADS)
+    k_ntt_pass(const Fr* __restrict__ in, size_t nin, Fr* __restrict__ out,
+               const Fr* __restrict__ tw, int logn, int s0, int B, int lgL, size_t win_lo,
+               size_t win_hi) {
+  __shared__ uint32_t sh[9 * NTT_T];
+  const int lgT = B + lgL, T = 1 << lgT;
+  const int L = 1 << lgL;
+  const size_t tid = threadIdx.x;
+  // tile id -> (hi, lo group)
+  const size_t ngroups = ((size_t)1 << s0) >> lgL;
+  const size_t hi = blockIdx.x / ngroups, lo0 = (blockIdx.x % ngroups) << lgL;
+  const size_t base = (hi << (s0 + B)) + lo0;
+  for (int e = (int)tid; e < T; e += NTT_THREADS) {
+    const size_t i = base + ((size_t)(e >> lgL) << s0) + (e & (L - 1));
+    R29 v = R29::zero();
+    if (i < nin) v = to29(in[i]);
+    lds_put29(sh, e, v);
+  }
   __syncthreads();
-  for (int s = 0; s < stages; s++) {
-    const uint32_t m = 1u << s;  // half span
-    const uint32_t t = threadIdx.x;
-    const uint32_t grp = t >> s, j = t & (m - 1);
-    const uint32_t i0 = grp * 2 * m + j, i1 = i0 + m;
-    // twiddle w_{2m}^j = w_N^{j * N/(2m)}
-    const Fr w = tw[(size_t)j << (logn - 1 - s)];
-    Fr u = sh[i0], v = sh[i1] * w;
-    sh[i0] = u + v;
-    sh[i1] = u - v;
+  for (int k = 0; k < B; k++) {
+    const int b = DIF ? B - 1 - k : k;  // mid bit of this stage
+    const int s = s0 + b;
+    for (int p = (int)tid; p < T / 2; p += NTT_THREADS) {
+      const int l = p & (L - 1), q = p >> lgL;
+      const int mid0 = ((q >> b) << (b + 1)) | (q & ((1 << b) - 1));
+      const int e0 = (mid0 << lgL) | l, e1 = e0 | (1 << (b + lgL));
+      const size_t j = ((size_t)(mid0 & ((1 << b) - 1)) << s0) + lo0 + l;  // i0 mod 2^s
+      const R29 w = to29(tw[j << (logn - 1 - s)]);
+      const R29 u = lds_get29(sh, e0), v = lds_get29(sh, e1);
+      if (DIF) {
+        lds_put29(sh, e0, red2p29(add29(u, v)));
+        lds_put29(sh, e1, mul29(sub29(u, v), w));
+      } else {
+        const R29 t = mul29(v, w);
+        lds_put29(sh, e0, red2p29(add29(u, t)));
+        lds_put29(sh, e1, red6p29(sub29(u, t)));
+      }
+    }
     __syncthreads();
   }
-  a[base + threadIdx.x] = sh[threadIdx.x];
-  a[base + threadIdx.x + 512] = sh[threadIdx.x + 512];
+  for (int e = (int)tid; e < T; e += NTT_THREADS) {
+    const size_t i = base + ((size_t)(e >> lgL) << s0) + (e & (L - 1));
+    if (i >= win_lo && i < win_hi) out[i - win_lo] = from29(canon29(lds_get29(sh, e)));
+  }
 }
 
-__global__ void k_ntt_stage(Fr* __restrict__ a, const Fr* __restrict__ tw, int logn, int s) {
-  size_t t = (size_t)blockIdx.x * blockDim.x + threadIdx.x;
+// runs every pass in place on `a` (the first pass reads `in`), direction by DIF
+static void ntt_run(qg_ctx* ctx, bool dif, const Fr* in, size_t nin, Fr* a, const Fr* tw, int logn,
+                    size_t win_lo, size_t win_hi, Fr* win_out) {
+  std::vector<NttPass> plan = ntt_plan(logn);
+  if (dif) std::reverse(plan.begin(), plan.end());
   const size_t n = (size_t)1 << logn;
-  if (t >= n / 2) return;
-  const size_t m = (size_t)1 << s;
-  const size_t grp = t >> s, j = t & (m - 1);
-  const size_t i0 = grp * 2 * m + j, i1 = i0 + m;
-  const Fr w = tw[j << (logn - 1 - s)];
-  Fr u = a[i0], v = a[i1] * w;
-  a[i0] = u + v;
-  a[i1] = u - v;
+  for (size_t k = 0; k < plan.size(); k++) {
+    const NttPass& P = plan[k];
+    const bool last = k + 1 == plan.size();
+    const Fr* src = k == 0 ? in : a;
+    const size_t ns = k == 0 ? nin : n;
+    Fr* dst = last && win_out ? win_out : a;
+    const size_t lo = last && win_out ? win_lo : 0, hi = last && win_out ? win_hi : n;
+    const unsigned blocks = (unsigned)(n >> (P.B + P.lgL));
+    if (dif)
+      hipLaunchKernelGGL(k_ntt_pass<true>, dim3(blocks), dim3(NTT_THREADS), 0, ctx->stream, src, ns,
+                         dst, tw, logn, P.s0, P.B, P.lgL, lo, hi);
+    else
+      hipLaunchKernelGGL(k_ntt_pass<false>, dim3(blocks), dim3(NTT_THREADS), 0, ctx->stream, src,
+                         ns, dst, tw, logn, P.s0, P.B, P.lgL, lo, hi);
+    QG_LAUNCH_CHECK();
+  }
 }
 
-// in-place NTT of a (already bit-reversed) with twiddle table tw[k] = w^k, k < n/2
-static void ntt_bitreversed(qg_ctx* ctx, Fr* a, const Fr* tw, int logn) {
+// x 2^256 (arkworks) -> x 2^261 in place: mul29 by 2^266
+__global__ void k_fr_to261(Fr* __restrict__ a, size_t n, L9 c) {
+  const size_t i = (size_t)blockIdx.x * blockDim.x + threadIdx.x;
+  if (i < n) a[i] = from29(canon29(mul29(to29(a[i]), R29::from_l9(c))));
+}
+
+// bit-reversed domain: H_br[k] = twM[j] (F[j] G[-j] + F[-j] G[j]), j = bitrev(k);
+// bitrev(-j) = k with every bit below k's top set bit flipped.  twM carries
+// w^{j(M-1)} n^-1 2^266, so mul29 of the 2^251-scaled products lands in
+// arkworks form with 1/n folded in.
+__global__ void k_s_combine_br(const Fr* __restrict__ F, const Fr* __restrict__ G,
+                               const Fr* __restrict__ twM, int logn, Fr* __restrict__ H) {
+  const size_t k = (size_t)blockIdx.x * blockDim.x + threadIdx.x;
   const size_t n = (size_t)1 << logn;
-  int s = 0;
-  if (logn >= 10) {
-    hipLaunchKernelGGL(k_ntt_tile, dim3((unsigned)(n / 1024)), dim3(512), 0, ctx->stream, a, tw,
-                       logn, 10);
-    QG_LAUNCH_CHECK();
-    s = 10;
+  if (k >= n) return;
+  size_t kn = 0;
+  if (k) {
+    const int hb = 63 - __clzll((unsigned long long)k);
+    kn = k ^ (((size_t)1 << hb) - 1);
   }
-  for (; s < logn; s++) {
-    hipLaunchKernelGGL(k_ntt_stage, dim3(div_up(n / 2, 256)), dim3(256), 0, ctx->stream, a, tw,
-                       logn, s);
-    QG_LAUNCH_CHECK();
-  }
+  const size_t j = (size_t)(__brevll((unsigned long long)k) >> (64 - logn));
+  const R29 a = to29(F[k]), bb = to29(G[kn]), c = to29(F[kn]), d = to29(G[k]);
+  const R29 v = red2p29(add29(mul29(a, bb), mul29(c, d)));
+  H[k] = from29(canon29(mul29(v, to29(twM[j]))));
 }
 
 __global__ void k_powers_ml(Fr base, size_t n, int K, Fr* out) {
@@ -263,6 +341,34 @@ static Fr root_of_unity(int logn) {
   return fr_pow_big(from_u64<FrP>(5), e);
 }
 
+// plain-integer product x y mod r (host)
+static Fr ml_plain_mul(const Fr& x, const Fr& y) { return from_mont(to_mont(x) * to_mont(y)); }
+
+// twiddle tables w^k 2^261 (k < n/2) for w = root_of_unity(logn) and its
+// inverse, cached per transform size
+static void ntt_twiddles(qg_ctx* ctx, int logn, Fr** tw, Fr** twi) {
+  const size_t n = (size_t)1 << logn, h = std::max<size_t>(n / 2, 1);
+  *tw = ctx->scratch_as<Fr>("ntt_tw", h);
+  *twi = ctx->scratch_as<Fr>("ntt_twi", h);
+  const std::string memo = std::to_string(logn) + "@" + std::to_string((uintptr_t)*tw) + "," +
+                           std::to_string((uintptr_t)*twi);
+  if (ctx->memo["ntt_tw"] == memo) return;
+  const Fr w = root_of_unity(logn), wi = finv(w);
+  const int K = 64;
+  const L9 c = F29P<FrP>::TO261;
+  hipLaunchKernelGGL(k_powers_ml, dim3(div_up(div_up(h, K), 256)), dim3(256), 0, ctx->stream, w, h,
+                     K, *tw);
+  QG_LAUNCH_CHECK();
+  hipLaunchKernelGGL(k_powers_ml, dim3(div_up(div_up(h, K), 256)), dim3(256), 0, ctx->stream, wi,
+                     h, K, *twi);
+  QG_LAUNCH_CHECK();
+  hipLaunchKernelGGL(k_fr_to261, dim3(div_up(h, 256)), dim3(256), 0, ctx->stream, *tw, h, c);
+  QG_LAUNCH_CHECK();
+  hipLaunchKernelGGL(k_fr_to261, dim3(div_up(h, 256)), dim3(256), 0, ctx->stream, *twi, h, c);
+  QG_LAUNCH_CHECK();
+  ctx->memo["ntt_tw"] = memo;
+}
+
 // S polynomial (M - 1 coefficients, untrimmed) of f (nf) and g (ng), device in/out
 static void s_poly_device(qg_ctx* ctx, const Fr* f, size_t nf, const Fr* g, size_t ng, Fr* S) {
   const size_t M = nf > ng ? nf : ng;
@@ -276,44 +382,34 @@ static void s_poly_device(qg_ctx* ctx, const Fr* f, size_t nf, const Fr* g, size
   Fr* F = ctx->scratch_as<Fr>("ntt_F", n);
   Fr* G = ctx->scratch_as<Fr>("ntt_G", n);
   Fr* H = ctx->scratch_as<Fr>("ntt_H", n);
-  Fr* tw = ctx->scratch_as<Fr>("ntt_tw", n / 2 + 1);
-  Fr* twi = ctx->scratch_as<Fr>("ntt_twi", n / 2 + 1);
   Fr* twM = ctx->scratch_as<Fr>("ntt_twM", n);
-  Fr w = root_of_unity(logn);
-  Fr wi = finv(w);
+  Fr *tw, *twi;
+  ntt_twiddles(ctx, logn, &tw, &twi);
+  // w^{j(M-1)} n^-1 2^266 for j < n: powers of w^{M-1} (x 2^256), then x n^-1 2^271 via mul29
+  const Fr w = root_of_unity(logn);
+  const Fr wM = fpow_small(w, (uint64_t)(M - 1));
   const int K = 64;
-  hipLaunchKernelGGL(k_powers_ml, dim3(div_up(div_up(n / 2, K), 256)), dim3(256), 0, ctx->stream,
-                     w, n / 2, K, tw);
-  QG_LAUNCH_CHECK();
-  hipLaunchKernelGGL(k_powers_ml, dim3(div_up(div_up(n / 2, K), 256)), dim3(256), 0, ctx->stream,
-                     wi, n / 2, K, twi);
-  QG_LAUNCH_CHECK();
-  // w^{j(M-1)} for j < n
-  Fr wM = fpow_small(w, (uint64_t)(M - 1));
   hipLaunchKernelGGL(k_powers_ml, dim3(div_up(div_up(n, K), 256)), dim3(256), 0, ctx->stream, wM,
                      n, K, twM);
   QG_LAUNCH_CHECK();
-  hipLaunchKernelGGL(k_bitrev_copy, dim3(div_up(n, 256)), dim3(256), 0, ctx->stream, f, nf, F,
-                     logn, 0, (size_t)0);
+  const Fr ninv_plain = from_mont(finv(from_u64<FrP>(n)));
+  const Fr cM = ml_plain_mul(ninv_plain, pow2_mod_plain<FrP>(271));
+  L9 c9{};
+  {
+    const R29 t = to29(cM);
+    for (int i = 0; i < 9; i++) c9.v[i] = t.l[i];
+  }
+  hipLaunchKernelGGL(k_fr_to261, dim3(div_up(n, 256)), dim3(256), 0, ctx->stream, twM, n, c9);
   QG_LAUNCH_CHECK();
-  hipLaunchKernelGGL(k_bitrev_copy, dim3(div_up(n, 256)), dim3(256), 0, ctx->stream, g, ng, G,
-                     logn, 0, (size_t)0);
+  // forward DIF of f and g (zero-extended), bit-reversed outputs
+  ntt_run(ctx, true, f, nf, F, tw, logn, 0, 0, nullptr);
+  ntt_run(ctx, true, g, ng, G, tw, logn, 0, 0, nullptr);
+  hipLaunchKernelGGL(k_s_combine_br, dim3(div_up(n, 256)), dim3(256), 0, ctx->stream, F, G, twM,
+                     logn, H);
   QG_LAUNCH_CHECK();
-  ntt_bitreversed(ctx, F, tw, logn);
-  ntt_bitreversed(ctx, G, tw, logn);
-  hipLaunchKernelGGL(k_s_combine, dim3(div_up(n, 256)), dim3(256), 0, ctx->stream, F, G, twM, n,
-                     H);
-  QG_LAUNCH_CHECK();
-  // inverse NTT: bit-reverse H into F, transform with w^{-1}
-  hipLaunchKernelGGL(k_bitrev_copy, dim3(div_up(n, 256)), dim3(256), 0, ctx->stream, H, n, F, logn,
-                     0, (size_t)0);
-  QG_LAUNCH_CHECK();
-  ntt_bitreversed(ctx, F, twi, logn);
-  // h has 2M-1 meaningful coefficients (< n); S = h[M .. 2M-1), scaled by 1/n
-  Fr ninv = finv(from_u64<FrP>(n));
-  hipLaunchKernelGGL(k_scale_copy, dim3(div_up(M - 1, 256)), dim3(256), 0, ctx->stream, F + M,
-                     ninv, M - 1, S);
-  QG_LAUNCH_CHECK();
+  // inverse DIT of H (bit-reversed in, natural out); the last pass writes only
+  // h[M .. 2M-1) = S
+  ntt_run(ctx, false, H, n, H, twi, logn, M, 2 * M - 1, S);
 }
 
 // highest nonzero index + 1: per-thread max over a grid-stride range, wave max

@@ -156,6 +156,23 @@ def test_s_polynomial_large(dev):
         assert S[k] == exp
 
 
+@pytest.mark.parametrize("nf,ng", [(1 << 15, 1 << 15), ((1 << 15) + 3, (1 << 14) - 5), (5000, 1)])
+def test_s_polynomial_multi_pass(dev, nf, ng):
+    """NTT sizes 2^16 / 2^17 run three LDS passes (11 + 7 + rest stages): spot
+    coefficients of S_k = sum_i (f_{i+k+1} g_i + g_{i+k+1} f_i) (ipa.rs:122-157)."""
+    rnd = random.Random(nf + ng)
+    f = [rnd.randrange(R) for _ in range(nf)]
+    g = [rnd.randrange(R) for _ in range(ng)]
+    M = max(nf, ng)
+    fp = f + [0] * (M - nf)
+    gp = g + [0] * (M - ng)
+    S = dev.s_polynomial(f, g)
+    assert len(S) == M - 1
+    for k in (0, 1, 2, 777, M // 2, M - 3, M - 2):
+        exp = sum(fp[i + k + 1] * gp[i] + gp[i + k + 1] * fp[i] for i in range(M - k - 1)) % R
+        assert S[k] == exp, k
+
+
 def test_kzg_open_golden(dev):
     from quill_amd import KZG
     g = load("kzg.json")
