@@ -140,6 +140,8 @@ void trace_full_witness(qg_ctx* ctx, const std::vector<const Fr*>& cols, size_t 
   ctx->sync();
 }
 
+bool comm_is_loopback(const qg_ctx* ctx) { return ctx->comm && ctx->comm->lb; }
+
 void comm_release(qg_ctx* ctx) {
   if (!ctx->comm) return;
   if (ctx->comm->comm) (void)ncclCommDestroy(ctx->comm->comm);

@@ -198,4 +198,6 @@ void eq_table_device(qg_ctx* ctx, const Fr* d_z, uint32_t nvars, Fr* d_out);
 // RCCL helpers (comm.hip); no-ops when world == 1
 void comm_allgather_bytes(qg_ctx* ctx, const void* d_send, void* d_recv, size_t bytes);
 void comm_release(qg_ctx* ctx);
+// true when the attached communicator is the in-process loopback (ranks share a device)
+bool comm_is_loopback(const qg_ctx* ctx);
 }  // namespace qg

@@ -64,8 +64,8 @@ QG_HD X29 x29_add_affine(const X29& p, const A29& a) {
   const Q29 S2 = mul29(a.y, p.ZZZ);
   const Q29 P = normfull29(sub29(U2, p.X));  // value in (2p, 6p)
   const Q29 R = normfull29(sub29(S2, p.Y));
-  if (is_zero_mod29(P)) {
-    if (is_zero_mod29(R)) return x29_dbl_affine(a);
+  if (is_zero_mod29_fast<FqP, 8>(P)) {
+    if (is_zero_mod29_fast<FqP, 8>(R)) return x29_dbl_affine(a);
     return x29_inf();
   }
   const Q29 PP = sqr29(P);
@@ -86,8 +86,8 @@ QG_HD X29 x29_acc_madd(const X29& p, const A29& a) {
   const Q29 S2 = mul29(a.y, p.ZZZ);
   const Q29 P = normfull29(subk29(U2, p.X, F29P<FqP>::K17));  // (p, 19p)
   const Q29 R = normfull29(subk29(S2, p.Y, F29P<FqP>::K9));   // (p, 11p)
-  if (is_zero_mod29_20(P)) {
-    if (is_zero_mod29_20(R)) return x29_dbl_affine(a);
+  if (is_zero_mod29_fast<FqP, 20>(P)) {
+    if (is_zero_mod29_fast<FqP, 20>(R)) return x29_dbl_affine(a);
     return x29_inf();
   }
   const Q29 PP = sqr29(P);                 // < 3p
@@ -115,8 +115,8 @@ QG_HD X29 x29_add(const X29& p, const X29& q) {
   const Q29 S2 = mul29(q.Y, p.ZZZ);
   const Q29 P = normfull29(sub29(U2, U1));
   const Q29 R = normfull29(sub29(S2, S1));
-  if (is_zero_mod29(P)) {
-    if (is_zero_mod29(R)) return x29_dbl(p);
+  if (is_zero_mod29_fast<FqP, 8>(P)) {
+    if (is_zero_mod29_fast<FqP, 8>(R)) return x29_dbl(p);
     return x29_inf();
   }
   const Q29 PP = sqr29(P);

@@ -383,6 +383,26 @@ QG_HD bool is_zero_mod29(const F29<C>& a) {
   return z;
 }
 
+// normalized value < K p (K <= 20): is it 0 mod p?  a = k p forces
+// k == l0 p^-1 (mod 2^29), so one multiply rejects every nonzero residue but a
+// K / 2^29 fraction, and only those run the exact limb comparison with k p
+// (the compare loops of is_zero_mod29 cost ~100 VALU + exec-mask SALU per test).
+template <class C, int K>
+QG_HD bool is_zero_mod29_fast(const F29<C>& a) {
+  const uint32_t k = (0u - a.l[0] * F29P<C>::INV) & M29;
+  if (k >= (uint32_t)K) return false;
+  uint64_t c = 0;
+  bool eq = true;
+#pragma unroll
+  for (int i = 0; i < 9; i++) {
+    const uint64_t t = (uint64_t)F29P<C>::P.v[i] * k + c;
+    const uint32_t limb = i < 8 ? (uint32_t)(t & M29) : (uint32_t)t;
+    c = t >> 29;
+    eq = eq && limb == a.l[i];
+  }
+  return eq;
+}
+
 // normalized value < 20p: is it 0 mod p?
 template <class C>
 QG_HD bool is_zero_mod29_20(const F29<C>& a) {

@@ -19,6 +19,8 @@
 //  * Bucket reduction sum_j (j+1) B_j runs as independent running sums over
 //    segments of L buckets; segment s contributes acc_s + lo_s * run_s; blocks
 //    tree-reduce in LDS; one final block sums block results.
+#include <stdlib.h>
+
 #include "common.h"
 #include "curve29.h"
 
@@ -661,7 +663,9 @@ static qg_srs* srs_alloc(qg_ctx* ctx, size_t n) {
   srs->n = n;
   // balanced signed windows: W = ceil(255 / c_target), c = ceil(255 / W), so the
   // top window is not a sliver that funnels every scalar into a few buckets
-  const int ct = msm_window_bits(n);
+  int ct = msm_window_bits(n);
+  if (const char* ov = getenv("QG_MSM_WINDOW_BITS")) ct = atoi(ov);  // tuning experiments
+  QG_CHECK(ct >= 4 && ct <= 26, QG_ERR_INVALID, "MSM window bits out of range");
   srs->W = (255 + ct - 1) / ct;
   srs->c = (255 + srs->W - 1) / srs->W;
   hipError_t e = hipMalloc(&srs->d_table, (size_t)srs->W * n * sizeof(G1Affine));

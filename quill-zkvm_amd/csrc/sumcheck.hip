@@ -670,25 +670,6 @@ __global__ void k_eq_combine(const Fr* __restrict__ low, const Fr* __restrict__ 
   out[i] = low[i & (((size_t)1 << lbits) - 1)] * high[i >> lbits];
 }
 
-// multi-GPU: fold each slot's last local pair with r (size 2 -> 1)
-__global__ void k_sc_fold_last(TablePtrs cur, uint32_t nslots, const Fr* __restrict__ chal,
-                               Fr* __restrict__ out) {
-  const uint32_t i = threadIdx.x;
-  if (i >= nslots) return;
-  const Fr r = *chal;
-  const Fr a = lt_p(cur.src[i][0]), b = lt_p(cur.src[i][1]);
-  out[i] = a + r * (b - a);
-}
-
-// gathered [rank][slot] -> per-slot tables [slot][rank]
-__global__ void k_sc_transpose(const Fr* __restrict__ in, uint32_t world, uint32_t nslots,
-                               Fr* __restrict__ out) {
-  const uint32_t idx = blockIdx.x * blockDim.x + threadIdx.x;
-  if (idx >= world * nslots) return;
-  const uint32_t rk = idx / nslots, sl = idx % nslots;
-  out[(size_t)sl * world + rk] = in[(size_t)rk * 8 + sl];
-}
-
 __global__ void k_scale(Fr* __restrict__ a, size_t n, const Fr* __restrict__ s) {
   const size_t i = (size_t)blockIdx.x * blockDim.x + threadIdx.x;
   if (i < n) a[i] = a[i] * (*s);
@@ -920,11 +901,27 @@ static void run_rounds(qg_ctx* ctx, uint32_t nvars, const std::vector<const Fr*>
   }
 }
 
+// gathered [rank][slot][e] (S entries per rank and slot) -> per-slot tables
+// [slot][rank * S + e]: the rank is the high index bits
+__global__ void k_sc_gather_tables(const Fr* __restrict__ in, uint32_t world, uint32_t nslots,
+                                   size_t S, Fr* __restrict__ out) {
+  const size_t idx = (size_t)blockIdx.x * blockDim.x + threadIdx.x;
+  const size_t total = (size_t)world * nslots * S;
+  if (idx >= total) return;
+  const size_t e = idx % S, sl = (idx / S) % nslots, rk = idx / (S * nslots);
+  out[sl * world * S + rk * S + e] = in[idx];
+}
+
 // Sharded rounds: this rank holds the block of every table whose
-// high log2(world) index bits equal its rank.  Rounds 0..m-1 (m = local bits)
-// pair local entries only: one allgather of the (d+1) round sums per round, then
-// every rank runs the identical device transcript.  The last log2(world) rounds
-// run redundantly on the allgathered single values.
+// high log2(world) index bits equal its rank.  The large rounds 0..js-1 pair
+// local entries only: one allgather of the (d+1) round sums per round, then
+// every rank runs the identical device transcript (k_sc_finish).  Once the
+// folded tables are small (global size <= 2^(SC_GATHER_LOG)) every rank
+// allgathers its block and runs the remaining rounds redundantly in the
+// single-GPU persistent kernel — no per-round collective on the
+// latency-bound tail (which does not shrink with more GPUs anyway).
+static constexpr uint32_t SC_GATHER_LOG = 16;
+
 template <int K, int NP>
 static void run_rounds_dist(qg_ctx* ctx, uint32_t nvars, const std::vector<const Fr*>& src,
                             const SopDev* d_sp, SopHdr h, RoundOut ro, uint32_t* bar, Fr* d_final,
@@ -937,16 +934,16 @@ static void run_rounds_dist(qg_ctx* ctx, uint32_t nvars, const std::vector<const
   QG_CHECK(nvars > lw, QG_ERR_INVALID, "sharded sumcheck needs nvars > log2(world)");
   const uint32_t m = nvars - lw;
   const size_t NL = (size_t)1 << m;
+  // sharded rounds: until the source tables of round js (folded through
+  // r_{js-2}, global size 2^(nvars - js + 1)) fit the gather size; at most m
+  // (local tables of 2 entries)
+  uint32_t js = nvars + 1 > SC_GATHER_LOG ? nvars + 1 - SC_GATHER_LOG : 0;
+  if (js > m) js = m;
   Fr* X = ctx->scratch_as<Fr>("sc_x", std::max<size_t>(1, (NL / 2) * std::max(nslots, 1u)));
   Fr* Y = ctx->scratch_as<Fr>("sc_y", std::max<size_t>(1, (NL / 4) * std::max(nslots, 1u)));
   Fr* partial = ctx->scratch_as<Fr>("sc_partial", (size_t)SC_MAX_BLOCKS * NP);
   Fr* loc = ctx->scratch_as<Fr>("sc_loc", NP);
   Fr* all = ctx->scratch_as<Fr>("sc_all", (size_t)world * NP);
-  Fr* last = ctx->scratch_as<Fr>("sc_last", 8);
-  Fr* graw = ctx->scratch_as<Fr>("sc_graw", (size_t)world * 8);
-  Fr* gt = ctx->scratch_as<Fr>("sc_gt", (size_t)world * 8);
-  Fr* gA = ctx->scratch_as<Fr>("sc_gA", (size_t)world * 8);
-  Fr* gB = ctx->scratch_as<Fr>("sc_gB", (size_t)world * 8);
   TablePtrs cur{};
   for (uint32_t i = 0; i < 8; i++) cur.src[i] = i < src.size() ? src[i] : nullptr;
   auto bufs = [&](Fr* base, size_t per) {
@@ -958,7 +955,7 @@ static void run_rounds_dist(qg_ctx* ctx, uint32_t nvars, const std::vector<const
   int fold = 0, parity = 0;
   {
     QgTimed tm(ctx, "sumcheck_round");
-    for (uint32_t j = 0; j < m; j++) {
+    for (uint32_t j = 0; j < js; j++) {
       const size_t npairs = (NL >> j) / 2;
       const unsigned blocks = (unsigned)std::min<size_t>(SC_MAX_BLOCKS, div_up(npairs, SC_BLOCK));
       TablePtrs tp = cur;
@@ -982,26 +979,53 @@ static void run_rounds_dist(qg_ctx* ctx, uint32_t nvars, const std::vector<const
   }
   {
     QgTimed tm(ctx, "sumcheck_tail");
-    // local tables have 2 entries (folded through r_{m-2}); fold with r_{m-1}
+    // this rank's source tables of round js: S entries per slot
+    const size_t S = js == 0 ? NL : NL >> (js - 1);
+    const size_t GN = (size_t)world * S;  // global size = 2^(nvars - js + 1) (js >= 1)
+    const uint32_t ns = std::max(nslots, 1u);
+    Fr* pack = ctx->scratch_as<Fr>("scg_pack", ns * S);
+    Fr* gat = ctx->scratch_as<Fr>("scg_all", (size_t)world * ns * S);
+    Fr* G = ctx->scratch_as<Fr>("scg_src", ns * GN);
+    for (uint32_t i = 0; i < nslots; i++)
+      QG_HIP(hipMemcpyAsync(pack + (size_t)i * S, cur.src[i], S * sizeof(Fr),
+                            hipMemcpyDeviceToDevice, ctx->stream));
     if (nslots) {
-      hipLaunchKernelGGL(k_sc_fold_last, dim3(1), dim3(64), 0, ctx->stream, cur, nslots,
-                         ro.chal + (m - 1), last);
+      comm_allgather_bytes(ctx, pack, gat, (size_t)nslots * S * sizeof(Fr));
+      hipLaunchKernelGGL(k_sc_gather_tables, dim3(div_up((size_t)world * nslots * S, 256)),
+                         dim3(256), 0, ctx->stream, gat, world, nslots, S, G);
       QG_LAUNCH_CHECK();
     }
-    comm_allgather_bytes(ctx, last, graw, sizeof(Fr) * 8);
-    if (nslots) {
-      hipLaunchKernelGGL(k_sc_transpose, dim3(div_up((size_t)world * nslots, 64)), dim3(64), 0,
-                         ctx->stream, graw, world, nslots, gt);
-      QG_LAUNCH_CHECK();
-    }
+    // ping-pong buffers of the persistent rounds (run_rounds' capacities):
+    // js == 0: round 0 does not fold, a >= GN/2, b >= GN/4 alternate from round 1;
+    // js >= 1: round js folds into a (>= GN/2), then b (>= GN/4), a, ...
+    Fr* A = ctx->scratch_as<Fr>("scg_a", ns * std::max<size_t>(1, GN / 2));
+    Fr* B = ctx->scratch_as<Fr>("scg_b", ns * std::max<size_t>(1, GN / 4));
     TablePtrs t0{}, bufA{}, bufB{};
     for (uint32_t i = 0; i < 8; i++) {
-      t0.src[i] = i < nslots ? gt + (size_t)world * i : nullptr;
-      bufA.dst[i] = i < nslots ? gA + (size_t)world * i : nullptr;
-      bufB.dst[i] = i < nslots ? gB + (size_t)world * i : nullptr;
+      const bool u = i < nslots;
+      t0.src[i] = u ? G + (size_t)i * GN : nullptr;
+      Fr* a = u ? A + (size_t)i * std::max<size_t>(1, GN / 2) : nullptr;
+      Fr* b = u ? B + (size_t)i * std::max<size_t>(1, GN / 4) : nullptr;
+      if (js == 0) {
+        bufA.dst[i] = a;
+        bufB.dst[i] = b;
+      } else {
+        t0.dst[i] = a;
+        bufA.dst[i] = b;
+        bufB.dst[i] = a;
+      }
     }
-    hipLaunchKernelGGL((k_sc_persist<K, NP>), dim3(1), dim3(TAIL_BLOCK), 0, ctx->stream, t0,
-                       bufA, bufB, d_sp, h, nvars, m, 0, 0, ro, partial, bar, d_final, d_eval);
+    constexpr size_t PB = TAIL_BLOCK / NP;
+    const size_t pairs0 = ((size_t)1 << nvars >> js) / 2;
+    // co-residency of the grid barrier: with the in-process loopback every rank
+    // shares one device, so each persistent grid takes a 1/world share of the CUs
+    const size_t cus = comm_is_loopback(ctx) ? std::max<size_t>(1, ctx->num_cus() / world)
+                                             : (size_t)ctx->num_cus();
+    const unsigned grid = (unsigned)std::max<size_t>(1, std::min<size_t>(cus, (pairs0 + PB - 1) / PB));
+    Fr* ppart = ctx->scratch_as<Fr>("sc_ppartial", (size_t)2 * grid * NP);
+    hipLaunchKernelGGL((k_sc_persist<K, NP>), dim3(grid), dim3(TAIL_BLOCK), 0, ctx->stream, t0,
+                       bufA, bufB, d_sp, h, nvars, js, js >= 1 ? 1 : 0, 0, ro, ppart, bar,
+                       d_final, d_eval);
     QG_LAUNCH_CHECK();
   }
 }

@@ -53,5 +53,20 @@ int main() {
     pr("ms", from29(ms));
     printf("\n");
   }
+  // is_zero_mod29_fast: k p (k < 20) is zero, k p + 1 and random values are not
+  int ok = 1;
+  for (uint32_t k = 0; k < 20; k++) {
+    F29<FqP> z = F29<FqP>::from_l9(l9_mul_small(F29P<FqP>::P, k));
+    ok &= is_zero_mod29_fast<FqP, 20>(z) ? 1 : 0;
+    ok &= is_zero_mod29_fast<FqP, 8>(z) == (k < 8) ? 1 : 0;
+    F29<FqP> z1 = z;
+    z1.l[0] += 1;
+    ok &= !is_zero_mod29_fast<FqP, 20>(normfull29(z1)) ? 1 : 0;
+  }
+  for (int it = 0; it < 20000; it++) {
+    const F29<FqP> a = to29(rnd_below<FqP>(254));
+    ok &= is_zero_mod29_fast<FqP, 20>(a) == is_zero_mod29_20(a) ? 1 : 0;
+  }
+  printf("zerotest=%x\n", ok);
   return 0;
 }

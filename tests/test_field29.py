@@ -14,7 +14,7 @@ RINV = pow(2, -261, P)
 
 
 @pytest.fixture(scope="module")
-def rows():
+def raw():
     gxx = shutil.which("g++")
     if gxx is None:
         pytest.skip("g++ not available")
@@ -28,6 +28,11 @@ def rows():
     for line in out.strip().splitlines():
         res.append({k: int(v, 16) for k, v in (kv.split("=") for kv in line.split())})
     return res
+
+
+@pytest.fixture(scope="module")
+def rows(raw):
+    return [r for r in raw if "a" in r]
 
 
 def test_mul29(rows):
@@ -63,3 +68,10 @@ def test_mulsub(rows):
     for r in rows:
         assert r["ms"] % P == (r["a"] * (r["b"] - r["c"]) - r["c"] * r["m"]) * RINV % P
         assert r["ms"] < 6 * P
+
+
+def test_fast_zero_mod_p(raw):
+    """is_zero_mod29_fast (the one-multiply residue filter used by the MSM's
+    curve additions) agrees with the exhaustive multiple-of-p comparison."""
+    z = [r for r in raw if "zerotest" in r]
+    assert z and z[0]["zerotest"] == 1

@@ -215,3 +215,36 @@ def test_sharded_hyperplonk_bad_copy_constraint_across_blocks(world):
 
     outs = run_ranks(world, fn)
     assert all(o_ is not None and "Permutation" in o_ and f"row {RL - 1}" in o_ for o_ in outs), outs
+
+
+@pytest.mark.parametrize("world,nv", [(2, 17), (4, 18), (2, 19)])
+def test_sharded_sumcheck_early_gather_matches_single(world, nv):
+    """nvars >= 17: the sharded prover runs nv - 15 rounds with per-round
+    allgathers, then gathers the folded tables (2^16 global entries) and
+    finishes redundantly on every rank.  Bit-exact against the single-context
+    device prover (itself pinned to the oracle), for a sumcheck and a zero-check."""
+    import quill_amd as q
+    from quill_amd.hyperplonk import VirtualPolyExpr as E, sumcheck_prove_tables
+    lw = world.bit_length() - 1
+    N, NL = 1 << nv, 1 << (nv - lw)
+    dev0 = q.Device(0)
+    tabs = [q.DeviceVec(dev0, N).fill_random(1000 + i) for i in range(3)]
+    host = [t.to_list() for t in tabs]
+    for t in tabs:
+        t.close()
+    me = E.Input(0) * E.Input(1) * E.Input(2) - E.Input(2) * E.Const(5)
+    rnd = random.Random(nv)
+    claimed = rnd.randrange(R)
+    ref = sumcheck_prove_tables(dev0, nv, host, me, claimed, q.Transcript(b"eg"))
+    zref = sumcheck_prove_tables(dev0, nv, host, me, 0, q.Transcript(b"egz"), zerocheck=True)
+    dev0.close()
+
+    def fn(dev, rank, world):
+        blk = [tb[rank * NL:(rank + 1) * NL] for tb in host]
+        a = sumcheck_prove_tables(dev, nv, blk, me, claimed, q.Transcript(b"eg"))
+        b = sumcheck_prove_tables(dev, nv, blk, me, 0, q.Transcript(b"egz"), zerocheck=True)
+        return a, b
+
+    for a, b in run_ranks(world, fn):
+        assert a == ref
+        assert b == zref
