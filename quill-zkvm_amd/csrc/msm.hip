@@ -29,7 +29,7 @@ using namespace qg;
 namespace qg {
 
 static constexpr int MSM_SEG = 8;       // buckets per reduction segment
-static constexpr int MSM_COMBINE_SEQ = 8;  // group sums a bucket's combine adds sequentially
+static constexpr int MSM_COMBINE_SEQ = 16;  // group sums a bucket's combine adds sequentially
 static constexpr int MSM_BLOCK = 256;
 
 // window size for an SRS of n bases (tuned later)
@@ -458,10 +458,14 @@ __global__ void __launch_bounds__(MSM_BLOCK)
     else hi = mid;
   }
   const uint32_t b = lo;
-  const uint32_t e0 = bstart[b] + ((t - tstart[b]) << elog);
-  uint32_t e1 = e0 + (1u << elog);
-  const uint32_t bend = bstart[b + 1];
-  if (e1 > bend) e1 = bend;
+  // the bucket's entries split into ceil(count / 2^elog) EQUAL chunks (not
+  // 2^elog-sized ones plus a remainder): every lane of a wave runs about the
+  // same trip count (+~15% lane efficiency for uniform scalars)
+  const uint32_t nch = tstart[b + 1] - tstart[b], cnt = bstart[b + 1] - bstart[b];
+  const uint32_t k = t - tstart[b];
+  const uint32_t e0 = bstart[b] + (uint32_t)(((uint64_t)k * cnt) / nch);
+  const uint32_t e1 = bstart[b] + (uint32_t)(((uint64_t)(k + 1) * cnt) / nch);
+  (void)elog;
   // 29-bit-limb XYZZ accumulator (lazily reduced); table points are in the
   // R = 2^261 domain
   X29 acc = x29_inf();
