@@ -25,6 +25,7 @@
 //    workgroup (fold + evaluate + transcript per round, synchronized by
 //    barriers), removing 2 launches per round.
 #include <stddef.h>
+#include <stdlib.h>
 #include <string.h>
 
 #include <algorithm>
@@ -58,7 +59,20 @@ __device__ unsigned long long g_sc_trace[2048];
 #endif
 
 static constexpr int SC_BLOCK = 256;
-static constexpr int SC_MAX_BLOCKS = 2048;
+static constexpr int SC_MAX_BLOCKS = 2048;  // partial-sum capacity (blocks per big round)
+
+// blocks of a big round: ~3 resident blocks per CU, each striding over many
+// pair groups (measured on MI355X at 2^20 vars: 768 blocks 0.764 ms vs 2048
+// blocks 0.798 ms; QG_SC_BLOCKS overrides, for tuning)
+static unsigned sc_round_blocks(qg_ctx* ctx, size_t npairs) {
+  static int ov = [] {
+    const char* e = getenv("QG_SC_BLOCKS");
+    return e ? atoi(e) : 0;
+  }();
+  size_t cap = ov > 0 ? (size_t)ov : (size_t)3 * ctx->num_cus();
+  cap = std::min<size_t>(cap, SC_MAX_BLOCKS);
+  return (unsigned)std::max<size_t>(1, std::min<size_t>(cap, div_up(npairs, SC_BLOCK)));
+}
 static constexpr int TAIL_BLOCK = 512;  // persistent-kernel block
 static constexpr int PERS_LOG = 16;     // tables of <= 2^16 entries: rounds run in one persistent launch
 
@@ -852,7 +866,7 @@ static void run_rounds(qg_ctx* ctx, uint32_t nvars, const std::vector<const Fr*>
       const size_t table = N >> j;  // entries per table evaluated in round j
       if (table <= ((size_t)1 << PERS_LOG)) break;
       const size_t npairs = table / 2;
-      const unsigned blocks = (unsigned)std::min<size_t>(SC_MAX_BLOCKS, div_up(npairs, SC_BLOCK));
+      const unsigned blocks = sc_round_blocks(ctx, npairs);
       TablePtrs tp = cur;
       if (fold) {
         const TablePtrs& d = parity ? tY : tX;
@@ -957,7 +971,7 @@ static void run_rounds_dist(qg_ctx* ctx, uint32_t nvars, const std::vector<const
     QgTimed tm(ctx, "sumcheck_round");
     for (uint32_t j = 0; j < js; j++) {
       const size_t npairs = (NL >> j) / 2;
-      const unsigned blocks = (unsigned)std::min<size_t>(SC_MAX_BLOCKS, div_up(npairs, SC_BLOCK));
+      const unsigned blocks = sc_round_blocks(ctx, npairs);
       TablePtrs tp = cur;
       if (fold) {
         const TablePtrs& d = parity ? tY : tX;
