@@ -13,9 +13,10 @@ R = o.R_MOD
 TAU = 0x1234567890ABCDEF1122334455667788
 
 
-def _stores(nv, tabs):
+def _stores(nv, tabs, dev=None):
+    """(mirror store, oracle store); dev given: the mirror's tables live in HBM"""
     from quill_amd import VirtualPolynomialStore
-    st, ost = VirtualPolynomialStore(nv), o.VirtualPolynomialStore(nv)
+    st, ost = VirtualPolynomialStore(nv, dev), o.VirtualPolynomialStore(nv)
     for tb in tabs:
         st.allocate_polynomial(tb)
         ost.allocate_polynomial(tb)
@@ -116,8 +117,9 @@ def _cmp_sumcheck(gs, os_):
     assert gs.r_polys == os_.r_polys
 
 
+@pytest.mark.parametrize("resident", [False, True])
 @pytest.mark.parametrize("mode", ["equality", "subset"])
-def test_multiset_equality_proof_matches_oracle(dev, mode):
+def test_multiset_equality_proof_matches_oracle(dev, mode, resident):
     """multiset_check.rs:310-385 scaled to 2^5: identical proof, point, store and
     transcript; the oracle verifier accepts the GPU proof."""
     from quill_amd import KZG, Transcript
@@ -139,7 +141,7 @@ def test_multiset_equality_proof_matches_oracle(dev, mode):
             left.append(right[j])
             mult[j] += 1
         tabs = [left, right, mult]
-    st, ost = _stores(nv, tabs)
+    st, ost = _stores(nv, tabs, dev if resident else None)
     hl, hr = st.new_virtual_from_input(0), st.new_virtual_from_input(1)
     ohl, ohr = ost.new_virtual_from_input(0), ost.new_virtual_from_input(1)
     hm = ohm = None
@@ -158,7 +160,8 @@ def test_multiset_equality_proof_matches_oracle(dev, mode):
     _cmp_sumcheck(proof.sumcheck_proof, oproof.sumcheck_proof)
     _cmp_mle(proof.opening_proof_denom_left, oproof.opening_proof_denom_left)
     _cmp_mle(proof.opening_proof_denom_right, oproof.opening_proof_denom_right)
-    assert st.polynomials == ost.polynomials and len(st.virtual_polys) == len(ost.virtual_polys)
+    polys = [p.to_list() for p in st.polynomials] if resident else st.polynomials
+    assert polys == ost.polynomials and len(st.virtual_polys) == len(ost.virtual_polys)
     vt = o.Transcript(b"multiset_equality_test")
     mc = (pt, o.mle_evaluate(tabs[2], pt)) if mode == "subset" else None
     oproof.verify(vt, okzg, (pt, o.mle_evaluate(left, pt)), (pt, o.mle_evaluate(right, pt)),
@@ -226,9 +229,11 @@ def test_permutation_check_matches_oracle(dev):
                                (pt, o.mle_evaluate(perm, pt)))
 
 
-def test_lookup_byte_xor_matches_oracle(dev):
+@pytest.mark.parametrize("resident", [False, True])
+def test_lookup_byte_xor_matches_oracle(dev, resident):
     """lookup.rs:197-297 (XOR-42 byte table, 2 columns) with 2^6 source rows:
-    set inclusion with different table sizes on both sides."""
+    set inclusion with different table sizes on both sides; host-table and
+    device-resident stores."""
     from quill_amd import KZG, Transcript, VirtualPolynomialStore
     from quill_amd.logup import LookupProof
     rnd = random.Random(42)
@@ -239,8 +244,8 @@ def test_lookup_byte_xor_matches_oracle(dev):
     mult = [0] * 256
     for b in by:
         mult[b] += 1
-    ss, oss = _stores(ns, [s1, s2])
-    ds, ods = _stores(nd, [c1, c2, mult])
+    ss, oss = _stores(ns, [s1, s2], dev if resident else None)
+    ds, ods = _stores(nd, [c1, c2, mult], dev if resident else None)
     sc = [ss.new_virtual_from_input(0), ss.new_virtual_from_input(1)]
     dc = [ds.new_virtual_from_input(0), ds.new_virtual_from_input(1)]
     m = ds.new_virtual_from_input(2)
