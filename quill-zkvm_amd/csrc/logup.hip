@@ -11,12 +11,17 @@
 //    raw arkworks table entries (x 2^256) with mul29 (x 2^-261) lands the
 //    denominator in the R = 2^261 domain and the multiplier in arkworks form
 //    with no conversion multiplies.
-//  * Batch inversion (Montgomery's trick) at three levels: each thread keeps
-//    the running prefix of its LG_K rows in registers (the row values go to
-//    LDS), the wave scans the thread products with shuffles (prefix and
-//    suffix), wave 0 inverts the block product (Fermat, sqr29), and every
-//    thread recovers its own inverse as inv(total) x prefix x suffix.  One
-//    inversion per LG_ROWS rows; ~3 multiplies per row otherwise.
+//  * Batch inversion (Montgomery's trick) at four levels, ONE field inversion
+//    per column: phase 1 (k_logup_den) stores every row's beta + h(x) in the
+//    output buffer and multiplies each block's rows together; phase 2
+//    (k_logup_scan, one block) forms the exclusive prefix / suffix products of
+//    the block products and their total, which the host inverts (one finv);
+//    phase 3 (k_logup) gives each block 1/(its product) = 1/total x prefix x
+//    suffix, then within the block as before: each thread's running prefix of
+//    its LG_K rows in registers (row values in LDS), wave shuffle scans of the
+//    thread products, back-substitution.  (A per-block Fermat inversion, ~330
+//    dependent multiplies on one wave per 2048 rows, bounded the one-pass
+//    version at 0.42 TB/s.)
 //  * A zero denominator makes the block product zero: the kernel flags it and
 //    the call returns QG_ERR_ASSERT (the reference panics in unwrap()).
 //  * Per-block sums of the outputs feed SetInclusionProof's claimed sums
@@ -78,22 +83,6 @@ QG_DEV R29 shfl_down29(const R29& a, int d) {
   return r;
 }
 
-// a^(r-2), square-and-multiply (R = 2^261 domain; a < 2p normalized).  The
-// exponent is a compile-time constant, so every branch is uniform.
-QG_DEV R29 inv29_sq(const R29& a) {
-  uint32_t e[8];
-  uint32_t br = 0;
-  e[0] = subb32(FrP::P[0], 2u, 0, &br);
-#pragma unroll
-  for (int i = 1; i < 8; i++) e[i] = subb32(FrP::P[i], 0u, br, &br);
-  R29 r = a;  // top bit of r - 2 (bit 253)
-  for (int bit = 252; bit >= 0; bit--) {
-    r = sqr29(r);
-    if ((e[bit >> 5] >> (bit & 31)) & 1u) r = mul29(r, a);
-  }
-  return r;
-}
-
 QG_DEV R29 lds_row(const uint32_t* vs, int k, int tid) {
   R29 v;
 #pragma unroll
@@ -105,36 +94,164 @@ QG_DEV void lds_put(uint32_t* vs, int k, int tid, const R29& v) {
   for (int i = 0; i < 9; i++) vs[(k * 9 + i) * LG_BLOCK + tid] = v.l[i];
 }
 
+// Phase 1: per row v = beta + h(row) (x 2^261), stored (< 2p) into the output
+// buffer; the block's product of all its rows -> bprod[block].  A zero
+// denominator makes the product zero (flagged).
+__global__ __launch_bounds__(LG_BLOCK) void k_logup_den(const LgDev* __restrict__ g, size_t n,
+                                                        Fr* __restrict__ out, Fr* __restrict__ bprod,
+                                                        uint32_t* __restrict__ err) {
+  __shared__ uint32_t wtot[LG_BLOCK / 64][9];
+  const int tid = threadIdx.x, lane = tid & 63, wv = tid >> 6;
+  const size_t base = (size_t)blockIdx.x * LG_ROWS + tid;
+  const R29 one = R29::from_l9(F29P<FrP>::ONE);
+  R29 T = one;
+  bool zero = false;
+  for (int k = 0; k < LG_K; k++) {
+    const size_t row = base + (size_t)k * LG_BLOCK;
+    if (row >= n) break;
+    const R29 v = canon29(lg_eval(g, 0, row));
+    zero |= is_zero29(v);
+    out[row] = from29(v);
+    T = mul29(T, v);
+  }
+  if (zero) atomicOr(err, 1u);
+  for (int d = 32; d >= 1; d >>= 1) {
+    const R29 o = shfl_down29(T, d);
+    if (lane + d < 64) T = mul29(T, o);
+  }
+  if (lane == 0)
+#pragma unroll
+    for (int i = 0; i < 9; i++) wtot[wv][i] = T.l[i];
+  __syncthreads();
+  if (tid == 0) {
+    R29 p = one;
+    for (int w = 0; w < LG_BLOCK / 64; w++) {
+      R29 t;
+#pragma unroll
+      for (int i = 0; i < 9; i++) t.l[i] = wtot[w][i];
+      p = mul29(p, t);
+    }
+    bprod[blockIdx.x] = from29(canon29(p));
+  }
+}
+
+// Phase 2 (one block): exclusive prefix and suffix products of the nb block
+// products, and their total (the single value the host inverts).
+static constexpr int LG_SCAN = 1024;
+__global__ __launch_bounds__(LG_SCAN) void k_logup_scan(const Fr* __restrict__ bprod, uint32_t nb,
+                                                        Fr* __restrict__ pre, Fr* __restrict__ suf,
+                                                        Fr* __restrict__ total) {
+  __shared__ uint32_t sh[2][9][LG_SCAN];
+  const uint32_t tid = threadIdx.x;
+  const uint32_t per = (nb + LG_SCAN - 1) / LG_SCAN, lo = tid * per;
+  const R29 one = R29::from_l9(F29P<FrP>::ONE);
+  R29 tp = one;  // product of this thread's segment
+  for (uint32_t i = lo; i < lo + per && i < nb; i++) tp = mul29(tp, to29(bprod[i]));
+#pragma unroll
+  for (int i = 0; i < 9; i++) sh[0][i][tid] = tp.l[i];
+  __syncthreads();
+  // Hillis-Steele inclusive scan of the segment products (ping-pong)
+  int cur = 0;
+  for (uint32_t off = 1; off < LG_SCAN; off <<= 1) {
+    R29 a, bb;
+#pragma unroll
+    for (int i = 0; i < 9; i++) a.l[i] = sh[cur][i][tid];
+    if (tid >= off) {
+#pragma unroll
+      for (int i = 0; i < 9; i++) bb.l[i] = sh[cur][i][tid - off];
+      a = mul29(bb, a);
+    }
+#pragma unroll
+    for (int i = 0; i < 9; i++) sh[cur ^ 1][i][tid] = a.l[i];
+    cur ^= 1;
+    __syncthreads();
+  }
+  R29 incl, excl = one, tot;
+#pragma unroll
+  for (int i = 0; i < 9; i++) {
+    incl.l[i] = sh[cur][i][tid];
+    tot.l[i] = sh[cur][i][LG_SCAN - 1];
+  }
+  if (tid > 0)
+#pragma unroll
+    for (int i = 0; i < 9; i++) excl.l[i] = sh[cur][i][tid - 1];
+  (void)incl;
+  // exclusive prefix within the segment
+  R29 run = excl;
+  for (uint32_t i = lo; i < lo + per && i < nb; i++) {
+    pre[i] = from29(canon29(run));
+    run = mul29(run, to29(bprod[i]));
+  }
+  if (tid == 0) *total = from29(canon29(tot));
+  __syncthreads();
+  // suffix: the same over the reversed order
+#pragma unroll
+  for (int i = 0; i < 9; i++) sh[0][i][LG_SCAN - 1 - tid] = tp.l[i];
+  __syncthreads();
+  cur = 0;
+  for (uint32_t off = 1; off < LG_SCAN; off <<= 1) {
+    R29 a, bb;
+#pragma unroll
+    for (int i = 0; i < 9; i++) a.l[i] = sh[cur][i][tid];
+    if (tid >= off) {
+#pragma unroll
+      for (int i = 0; i < 9; i++) bb.l[i] = sh[cur][i][tid - off];
+      a = mul29(bb, a);
+    }
+#pragma unroll
+    for (int i = 0; i < 9; i++) sh[cur ^ 1][i][tid] = a.l[i];
+    cur ^= 1;
+    __syncthreads();
+  }
+  // reversed position of this thread's segment: LG_SCAN - 1 - tid; exclusive = entry before it
+  const uint32_t rp = LG_SCAN - 1 - tid;
+  R29 sx = one;
+  if (rp > 0)
+#pragma unroll
+    for (int i = 0; i < 9; i++) sx.l[i] = sh[cur][i][rp - 1];
+  run = sx;
+  for (uint32_t k = per; k-- > 0;) {
+    const uint32_t i = lo + k;
+    if (i >= nb) continue;
+    suf[i] = from29(canon29(run));
+    run = mul29(run, to29(bprod[i]));
+  }
+}
+
+// Phase 3: 1/v for every row of the block from inv(total) x prefix x suffix of
+// the block products (block inverse), then the thread-level Montgomery trick
+// as in one pass: the rows' v values come back from the output buffer.
 __global__ __launch_bounds__(LG_BLOCK) void k_logup(const LgDev* __restrict__ g, size_t n,
-                                                    Fr* __restrict__ out, Fr* __restrict__ bsum,
-                                                    uint32_t* __restrict__ err) {
+                                                    Fr* __restrict__ out,
+                                                    const Fr* __restrict__ pre,
+                                                    const Fr* __restrict__ suf,
+                                                    const Fr* __restrict__ tinv,
+                                                    Fr* __restrict__ bsum) {
   __shared__ uint32_t vs[LG_K * 9 * LG_BLOCK];  // row denominators, [k][limb][thread]
   __shared__ uint32_t wtot[LG_BLOCK / 64][9];
-  __shared__ uint32_t winv[9];
   __shared__ uint32_t wsum[LG_BLOCK / 64][9];
   const int tid = threadIdx.x, lane = tid & 63, wv = tid >> 6;
   const size_t base = (size_t)blockIdx.x * LG_ROWS + tid;
   const R29 one = R29::from_l9(F29P<FrP>::ONE);
 
-  // 1. denominators to LDS, then the running prefix of this thread's rows
+  // 1. denominators back from HBM to LDS, then the running prefix of this thread's rows
   for (int k = 0; k < LG_K; k++) {
     const size_t row = base + (size_t)k * LG_BLOCK;
-    const R29 v = row < n ? lg_eval(g, 0, row) : one;
+    const R29 v = row < n ? to29(out[row]) : one;
 #pragma unroll
     for (int i = 0; i < 9; i++) vs[(k * 9 + i) * LG_BLOCK + tid] = v.l[i];
   }
-  // (written out: the unroller declines this loop and would spill pre[] to scratch)
   static_assert(LG_K == 8, "prefix chain is written out for 8 rows");
-  R29 pre[LG_K];
-  pre[0] = lds_row(vs, 0, tid);
-  pre[1] = mul29(pre[0], lds_row(vs, 1, tid));
-  pre[2] = mul29(pre[1], lds_row(vs, 2, tid));
-  pre[3] = mul29(pre[2], lds_row(vs, 3, tid));
-  pre[4] = mul29(pre[3], lds_row(vs, 4, tid));
-  pre[5] = mul29(pre[4], lds_row(vs, 5, tid));
-  pre[6] = mul29(pre[5], lds_row(vs, 6, tid));
-  pre[7] = mul29(pre[6], lds_row(vs, 7, tid));
-  const R29 T = pre[LG_K - 1];
+  R29 pre_r[LG_K];
+  pre_r[0] = lds_row(vs, 0, tid);
+  pre_r[1] = mul29(pre_r[0], lds_row(vs, 1, tid));
+  pre_r[2] = mul29(pre_r[1], lds_row(vs, 2, tid));
+  pre_r[3] = mul29(pre_r[2], lds_row(vs, 3, tid));
+  pre_r[4] = mul29(pre_r[3], lds_row(vs, 4, tid));
+  pre_r[5] = mul29(pre_r[4], lds_row(vs, 5, tid));
+  pre_r[6] = mul29(pre_r[5], lds_row(vs, 6, tid));
+  pre_r[7] = mul29(pre_r[6], lds_row(vs, 7, tid));
+  const R29 T = pre_r[LG_K - 1];
 
   // 2. exclusive prefix / suffix products of T across the block
   R29 ip = T, is = T;  // inclusive in-wave prefix / suffix
@@ -150,35 +267,21 @@ __global__ __launch_bounds__(LG_BLOCK) void k_logup(const LgDev* __restrict__ g,
   if (lane == 0) ep = one;
   if (lane == 63) es = one;
   __syncthreads();
-  R29 tot = one;
   for (int w = 0; w < LG_BLOCK / 64; w++) {  // wave products straight from LDS (uniform loop)
     R29 t;
 #pragma unroll
     for (int i = 0; i < 9; i++) t.l[i] = wtot[w][i];
     if (w < wv) ep = mul29(ep, t);
     if (w > wv) es = mul29(es, t);
-    if (wv == 0) tot = mul29(tot, t);
   }
-  if (wv == 0) {
-    tot = canon29(tot);
-    if (is_zero29(tot)) {
-      if (lane == 0) atomicOr(err, 1u);
-    }
-    const R29 ti = inv29_sq(tot);
-    if (lane == 0)
-#pragma unroll
-      for (int i = 0; i < 9; i++) winv[i] = ti.l[i];
-  }
-  __syncthreads();
-  R29 inv_run;
-#pragma unroll
-  for (int i = 0; i < 9; i++) inv_run.l[i] = winv[i];
-  inv_run = mul29(mul29(inv_run, ep), es);  // 1 / T
+  // 1 / (block product) = 1 / total x (other blocks' products)
+  const R29 binv = mul29(mul29(to29(*tinv), to29(pre[blockIdx.x])), to29(suf[blockIdx.x]));
+  R29 inv_run = mul29(mul29(binv, ep), es);  // 1 / T
 
   // 3. back-substitution: 1 / v_k overwrites v_k in LDS (own slots only)
 #define LG_BACK(k)                                        \
   {                                                       \
-    const R29 x = mul29(inv_run, pre[k - 1]);             \
+    const R29 x = mul29(inv_run, pre_r[k - 1]);           \
     inv_run = mul29(inv_run, lds_row(vs, k, tid));        \
     lds_put(vs, k, tid, x);                               \
   }
@@ -352,12 +455,43 @@ static Fr logup_run(qg_ctx* ctx, uint32_t nvars, uint32_t ntables, const std::ve
   Fr* d_res = reinterpret_cast<Fr*>(io + sizeof(LgDev));
   uint32_t* d_err = reinterpret_cast<uint32_t*>(io + sizeof(LgDev) + 32);
   Fr* d_bsum = ctx->scratch_as<Fr>("lg_bsum", nb);
+  // block products, their exclusive prefix / suffix products, total, 1/total
+  Fr* d_bp = ctx->scratch_as<Fr>("lg_bprod", 3 * (size_t)nb + 2);
+  Fr* d_pre = d_bp + nb;
+  Fr* d_suf = d_pre + nb;
+  Fr* d_tot = d_suf + nb;
+  Fr* d_tinv = d_tot + 1;
   QG_HIP(hipMemcpyAsync(d_img, &img, sizeof(img), hipMemcpyHostToDevice, ctx->stream));
   QG_HIP(hipMemsetAsync(d_err, 0, 4, ctx->stream));
+  struct {
+    Fr tot;
+    uint32_t err;
+  } ht;
   {
     QgTimed tm(ctx, "logup_column");
-    hipLaunchKernelGGL(k_logup, dim3(nb), dim3(LG_BLOCK), 0, ctx->stream, d_img, n, d_out, d_bsum,
-                       d_err);
+    hipLaunchKernelGGL(k_logup_den, dim3(nb), dim3(LG_BLOCK), 0, ctx->stream, d_img, n, d_out,
+                       d_bp, d_err);
+    QG_LAUNCH_CHECK();
+    hipLaunchKernelGGL(k_logup_scan, dim3(1), dim3(LG_SCAN), 0, ctx->stream, d_bp, nb, d_pre,
+                       d_suf, d_tot);
+    QG_LAUNCH_CHECK();
+    QG_HIP(hipMemcpyAsync(&ht.tot, d_tot, sizeof(Fr), hipMemcpyDeviceToHost, ctx->stream));
+    QG_HIP(hipMemcpyAsync(&ht.err, d_err, 4, hipMemcpyDeviceToHost, ctx->stream));
+    ctx->sync();
+  }
+  // one inversion for the whole column, of the product of every denominator:
+  // tot = P 2^261 (plain)  ->  (1 / P) 2^261 = 2^522 / tot
+  Fr tinv = Fr::zero();
+  if (!ht.err) {
+    const Fr tot_plain = ht.tot;  // nonzero: no denominator was zero
+    const Fr inv_plain = from_mont(finv(to_mont(tot_plain)));
+    tinv = lg_plain_mul(inv_plain, pow2_mod_plain<FrP>(522));
+  }
+  if (!ht.err) {
+    QG_HIP(hipMemcpyAsync(d_tinv, &tinv, sizeof(Fr), hipMemcpyHostToDevice, ctx->stream));
+    QgTimed tm(ctx, "logup_column");
+    hipLaunchKernelGGL(k_logup, dim3(nb), dim3(LG_BLOCK), 0, ctx->stream, d_img, n, d_out, d_pre,
+                       d_suf, d_tinv, d_bsum);
     QG_LAUNCH_CHECK();
     hipLaunchKernelGGL(k_logup_sum, dim3(1), dim3(256), 0, ctx->stream, d_bsum, nb, d_res);
     QG_LAUNCH_CHECK();
@@ -366,8 +500,10 @@ static Fr logup_run(qg_ctx* ctx, uint32_t nvars, uint32_t ntables, const std::ve
     Fr res;
     uint32_t err;
   } h;
-  QG_HIP(hipMemcpyAsync(&h.res, d_res, sizeof(Fr), hipMemcpyDeviceToHost, ctx->stream));
-  QG_HIP(hipMemcpyAsync(&h.err, d_err, 4, hipMemcpyDeviceToHost, ctx->stream));
+  h.res = Fr::zero();
+  h.err = ht.err;
+  if (!ht.err)
+    QG_HIP(hipMemcpyAsync(&h.res, d_res, sizeof(Fr), hipMemcpyDeviceToHost, ctx->stream));
   ctx->sync();
   // every rank learns whether any rank hit a zero denominator, and the global sum
   struct {
