@@ -288,7 +288,9 @@ int qg_zerocheck_prove_dev(qg_ctx* ctx, uint32_t nvars, uint32_t ntables,
  * and receives its 2^(nvars - log2(world)) block).  `out_sum` (nullable)
  * receives sum_x out[x] over all ranks — the claimed sums of
  * set_inclusion.rs:162-166,193-197.  Returns QG_ERR_ASSERT when some
- * beta + h(x) == 0 (the reference panics in inverse().unwrap(), :51/:63).
+ * beta + h(x) == 0 (the reference panics in inverse().unwrap(), :51/:63);
+ * on any error the contents of `out` are undefined (the reference aborts
+ * there, so no caller reads it).
  * Limits: <= 128 monomials per expression, <= 64 distinct tables. */
 int qg_logup_column(qg_ctx* ctx, uint32_t nvars, uint32_t ntables, const uint64_t* const* tables,
                     const qg_expr_op* h_prog, size_t h_len, const uint64_t* h_consts,

@@ -748,3 +748,81 @@ int oc_logup_column(const uint64_t* t0, const uint64_t* t1, const uint64_t* t2, 
   if (seconds) *seconds = now_s() - s;
   return 0;
 }
+
+/* ---------------------------------------------------------------- checkers
+ * Size-independent checks of full-size device results (tests/, bench.py):
+ * the trapdoor identity commit(p) = [p(tau)] g (kzg.rs:44-47, 61-73), MLE
+ * evaluations (DenseMultilinearExtension::evaluate, bit j <-> point[j],
+ * mlpcs.rs:91-94) and the sum of a product of tables (the claimed sum of
+ * sumcheck.rs:28-34).  Montgomery limbs in and out. */
+
+/* sum_i c_i x^i (Horner, ark-poly Polynomial::evaluate, kzg.rs:77-78) */
+int oc_fr_horner(const uint64_t* coeffs, size_t n, const uint64_t x[4], uint64_t out[4]) {
+  fp X, acc = {{0, 0, 0, 0}};
+  memcpy(X.v, x, 32);
+  for (size_t i = n; i-- > 0;) {
+    fp c;
+    memcpy(c.v, coeffs + 4 * i, 32);
+    acc = f_add(&FR, f_mul(&FR, acc, X), c);
+  }
+  memcpy(out, acc.v, 32);
+  return 0;
+}
+
+/* MLE of the first 2^nv entries at point (bit 0 folded first) */
+int oc_fr_mle_eval(const uint64_t* table, int nv, const uint64_t* point, uint64_t out[4]) {
+  size_t n = (size_t)1 << nv;
+  fp* t = (fp*)malloc(sizeof(fp) * n);
+  if (!t) return -1;
+  memcpy(t, table, sizeof(fp) * n);
+  for (int j = 0; j < nv; j++) {
+    fp r;
+    memcpy(r.v, point + 4 * j, 32);
+    n >>= 1;
+    for (size_t p = 0; p < n; p++)
+      t[p] = f_add(&FR, t[2 * p], f_mul(&FR, r, f_sub(&FR, t[2 * p + 1], t[2 * p])));
+  }
+  memcpy(out, t[0].v, 32);
+  free(t);
+  return 0;
+}
+
+/* sum_i prod_{j<k} tables[j][i] */
+int oc_fr_sum_prod(const uint64_t* const* tables, int k, size_t n, uint64_t out[4]) {
+  fp acc = {{0, 0, 0, 0}};
+  for (size_t i = 0; i < n; i++) {
+    fp p;
+    memcpy(p.v, tables[0] + 4 * i, 32);
+    for (int j = 1; j < k; j++) {
+      fp x;
+      memcpy(x.v, tables[j] + 4 * i, 32);
+      p = f_mul(&FR, p, x);
+    }
+    acc = f_add(&FR, acc, p);
+  }
+  memcpy(out, acc.v, 32);
+  return 0;
+}
+
+/* [s] P (double-and-add over the canonical scalar); P affine Montgomery */
+int oc_g1_mul(const uint64_t base_xy[8], uint8_t base_inf, const uint64_t s_mont[4],
+              uint64_t out_xy[8], uint8_t* out_inf) {
+  g1a b;
+  memcpy(b.x.v, base_xy, 32);
+  memcpy(b.y.v, base_xy + 4, 32);
+  b.inf = base_inf;
+  fp s;
+  memcpy(s.v, s_mont, 32);
+  s = f_from_mont(&FR, s);
+  g1j acc = j_zero();
+  for (int i = 3; i >= 0; i--)
+    for (int bit = 63; bit >= 0; bit--) {
+      j_double(&acc);
+      if ((s.v[i] >> bit) & 1) j_add_affine(&acc, &b);
+    }
+  g1a r = j_to_affine(&acc);
+  memcpy(out_xy, r.x.v, 32);
+  memcpy(out_xy + 4, r.y.v, 32);
+  *out_inf = (uint8_t)r.inf;
+  return 0;
+}

@@ -37,6 +37,10 @@ def lib():
         L.oc_bench_sumcheck.argtypes = [C.c_int, C.c_uint64, C.POINTER(C.c_double)]
         L.oc_logup_column.argtypes = [U64P, U64P, U64P, C.c_size_t, U64P, U64P, U64P,
                                       C.POINTER(C.c_double)]
+        L.oc_fr_horner.argtypes = [U64P, C.c_size_t, U64P, U64P]
+        L.oc_fr_mle_eval.argtypes = [U64P, C.c_int, U64P, U64P]
+        L.oc_fr_sum_prod.argtypes = [C.POINTER(U64P), C.c_int, C.c_size_t, U64P]
+        L.oc_g1_mul.argtypes = [U64P, C.c_uint8, U64P, U64P, C.POINTER(C.c_uint8)]
         _lib = L
     return _lib
 
@@ -165,3 +169,59 @@ def logup_column_arrays(t0, t1, t2, a_mont, beta_mont):
     if rc:
         raise ZeroDivisionError("logup denominator is zero")
     return out, s.value
+
+
+# ---------------------------------------------------------------- checkers
+# Full-size checks of device results on Montgomery-limb numpy arrays (n x 4
+# uint64, the layout DeviceVec.to_numpy returns): plain ints in and out.
+def _limbs(x, m=R_MOD):
+    return np.array(_mont(x, m), dtype=np.uint64)
+
+
+def _arr(a):
+    return np.ascontiguousarray(a, dtype=np.uint64).reshape(-1, 4)
+
+
+def fr_horner(coeffs, x: int) -> int:
+    """sum_i coeffs[i] x^i (kzg.rs:77-78); coeffs Montgomery limbs (n, 4)."""
+    c = _arr(coeffs)
+    xv, out = _limbs(x), np.zeros(4, dtype=np.uint64)
+    lib().oc_fr_horner(c.ctypes.data_as(U64P), c.shape[0], xv.ctypes.data_as(U64P),
+                       out.ctypes.data_as(U64P))
+    return _unmont(out, R_MOD)
+
+
+def fr_mle_eval(table, point) -> int:
+    """MLE of the first 2^len(point) entries of table at point (bit j <-> point[j])."""
+    t = _arr(table)
+    nv = len(point)
+    assert t.shape[0] >= 1 << nv
+    pt = np.array([_mont(p, R_MOD) for p in point], dtype=np.uint64).reshape(-1)
+    out = np.zeros(4, dtype=np.uint64)
+    lib().oc_fr_mle_eval(t.ctypes.data_as(U64P), nv, pt.ctypes.data_as(U64P),
+                         out.ctypes.data_as(U64P))
+    return _unmont(out, R_MOD)
+
+
+def fr_sum_prod(tables) -> int:
+    """sum_i prod_j tables[j][i]"""
+    ts = [_arr(t) for t in tables]
+    n = min(t.shape[0] for t in ts)
+    ptrs = (U64P * len(ts))(*[t.ctypes.data_as(U64P) for t in ts])
+    out = np.zeros(4, dtype=np.uint64)
+    lib().oc_fr_sum_prod(ptrs, len(ts), n, out.ctypes.data_as(U64P))
+    return _unmont(out, R_MOD)
+
+
+def g1_mul(P, s: int):
+    """[s] P for an affine canonical point P = (x, y) or None (infinity)."""
+    xy = np.zeros(8, dtype=np.uint64)
+    if P is not None:
+        xy[:4] = _mont(P[0], P_MOD)
+        xy[4:] = _mont(P[1], P_MOD)
+    sv, out, oinf = _limbs(s), np.zeros(8, dtype=np.uint64), C.c_uint8()
+    lib().oc_g1_mul(xy.ctypes.data_as(U64P), 1 if P is None else 0, sv.ctypes.data_as(U64P),
+                    out.ctypes.data_as(U64P), C.byref(oinf))
+    if oinf.value:
+        return None
+    return (_unmont(out[:4], P_MOD), _unmont(out[4:], P_MOD))

@@ -402,8 +402,14 @@ class KZG:
         self.max_degree = max_degree
         self.tau = tau % R_MOD
         self.g1 = g1
-        self.taus = [pow(self.tau, i, R_MOD) for i in range(max_degree + 1)]
+        self._taus = None
         self._points = points
+
+    @property
+    def taus(self):
+        if self._taus is None:
+            self._taus = [pow(self.tau, i, R_MOD) for i in range(self.max_degree + 1)]
+        return self._taus
 
     @property
     def g1_points(self):
@@ -417,8 +423,7 @@ class KZG:
         Evaluated through the trapdoor: the MSM denotes [p(tau)] g1, a unique
         group element; `commit_msm` runs the literal MSM for small sizes."""
         assert len(poly) <= self.max_degree + 1, "Polynomial degree exceeds max degree"
-        v = sum(c * t for c, t in zip(poly, self.taus)) % R_MOD
-        return g1_mul(self.g1, v)
+        return g1_mul(self.g1, poly_eval(poly, self.tau))
 
     def commit_msm(self, poly):
         assert len(poly) <= self.max_degree + 1

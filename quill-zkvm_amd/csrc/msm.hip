@@ -751,13 +751,14 @@ G1Affine msm_device(qg_ctx* ctx, const qg_srs* srs, const Fr* d_scalars, size_t 
       const size_t smemA = (size_t)tile * W * 8 + (((size_t)tile * W + 1) & ~(size_t)1) * 2 +
                            (3 * (size_t)H + SORT_BLOCK) * 4;
       QG_CHECK(smemA <= 160 * 1024, QG_ERR_UNSUPPORTED, "pass-A tile exceeds LDS");
-      static bool attr_set = false;
-      if (!attr_set) {
+      // the >64 KiB dynamic-LDS attribute, once per context (= per device and
+      // per calling thread: a context is used by one thread at a time)
+      if (ctx->memo.count("msm_lds_attr") == 0) {
         QG_HIP(hipFuncSetAttribute(reinterpret_cast<const void*>(&k_sortA_scatter),
                                    hipFuncAttributeMaxDynamicSharedMemorySize, 160 * 1024));
         QG_HIP(hipFuncSetAttribute(reinterpret_cast<const void*>(&k_sortB_scatter),
                                    hipFuncAttributeMaxDynamicSharedMemorySize, 160 * 1024));
-        attr_set = true;
+        ctx->memo["msm_lds_attr"] = "1";
       }
       hipLaunchKernelGGL(k_sortA_scatter, dim3(nblk), dim3(SORT_BLOCK), smemA, ctx->stream,
                          d_scalars, n, srs->n, c, W, LO, H, nblk, tile, ghist, goff, tmp);

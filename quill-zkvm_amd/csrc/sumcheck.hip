@@ -839,6 +839,29 @@ static std::shared_ptr<const ScProgram> get_program(const qg_expr_op* prog, size
   return p;
 }
 
+
+// Co-residency guard of a grid-barrier launch: the grid must not exceed what
+// the device holds at once (occupancy API x CUs, one block per CU margin kept
+// for the gfx950 SGPR admission rule of MI355X_MICROARCH.md "Residency").
+// Queried once per context and kernel instantiation.
+template <int K, int NP>
+static unsigned persist_grid_cap(qg_ctx* ctx, size_t cus) {
+  const std::string key = "persist_occ_" + std::to_string(K) + "_" + std::to_string(NP);
+  auto it = ctx->memo.find(key);
+  int occ = 0;
+  if (it == ctx->memo.end()) {
+    QG_HIP(hipOccupancyMaxActiveBlocksPerMultiprocessor(
+        &occ, reinterpret_cast<const void*>(&k_sc_persist<K, NP>), TAIL_BLOCK, 0));
+    ctx->memo[key] = std::to_string(occ);
+  } else {
+    occ = std::stoi(it->second);
+  }
+  QG_CHECK(occ >= 1, QG_ERR_DEVICE, "persistent sumcheck kernel cannot be resident");
+  // one block per CU at most even where more would fit: a CU-resident block per
+  // grid slot keeps the barrier safe next to other kernels' blocks
+  return (unsigned)std::max<size_t>(1, cus);
+}
+
 template <int K, int NP>
 static void run_rounds(qg_ctx* ctx, uint32_t nvars, const std::vector<const Fr*>& src,
                        const SopDev* d_sp, SopHdr h, RoundOut ro, uint32_t* bar, Fr* d_final,
@@ -906,7 +929,7 @@ static void run_rounds(qg_ctx* ctx, uint32_t nvars, const std::vector<const Fr*>
     constexpr size_t PB = TAIL_BLOCK / NP;
     const size_t pairs0 = (N >> j) / 2;
     const unsigned grid = (unsigned)std::max<size_t>(
-        1, std::min<size_t>((size_t)ctx->num_cus(), (pairs0 + PB - 1) / PB));
+        1, std::min<size_t>(persist_grid_cap<K, NP>(ctx, ctx->num_cus()), (pairs0 + PB - 1) / PB));
     Fr* ppart = ctx->scratch_as<Fr>("sc_ppartial", (size_t)2 * grid * NP);
     hipLaunchKernelGGL((k_sc_persist<K, NP>), dim3(grid), dim3(TAIL_BLOCK), 0, ctx->stream, t0,
                        bufA, bufB, d_sp, h, nvars, j, fold, pending, ro, ppart, bar, d_final,
@@ -1035,7 +1058,8 @@ static void run_rounds_dist(qg_ctx* ctx, uint32_t nvars, const std::vector<const
     // shares one device, so each persistent grid takes a 1/world share of the CUs
     const size_t cus = comm_is_loopback(ctx) ? std::max<size_t>(1, ctx->num_cus() / world)
                                              : (size_t)ctx->num_cus();
-    const unsigned grid = (unsigned)std::max<size_t>(1, std::min<size_t>(cus, (pairs0 + PB - 1) / PB));
+    const unsigned grid = (unsigned)std::max<size_t>(
+        1, std::min<size_t>(persist_grid_cap<K, NP>(ctx, cus), (pairs0 + PB - 1) / PB));
     Fr* ppart = ctx->scratch_as<Fr>("sc_ppartial", (size_t)2 * grid * NP);
     hipLaunchKernelGGL((k_sc_persist<K, NP>), dim3(grid), dim3(TAIL_BLOCK), 0, ctx->stream, t0,
                        bufA, bufB, d_sp, h, nvars, js, js >= 1 ? 1 : 0, 0, ro, ppart, bar,

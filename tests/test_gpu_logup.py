@@ -85,23 +85,34 @@ def test_logup_zero_denominator_is_an_error(dev):
         assert ei.value.code == -5
 
 
-def test_logup_column_2p20_property(dev):
-    """2^20 rows on device-resident tables: out * (beta + h) == m at sampled rows,
-    and the returned sum equals the sum of the downloaded column."""
+@pytest.mark.parametrize("nv", [20, 22])
+def test_logup_column_large_property(dev, nv):
+    """2^20 / 2^22 rows on device-resident tables: out * (beta + h) == m at rows
+    sampled in the first, middle and last blocks and at random, and the returned
+    sum equals the sum of the downloaded column.  At 2^22 rows (2048 blocks of
+    2048) k_logup_scan runs its multi-entry segments (per > 1), which pins the
+    per-segment prefix / suffix products."""
+    import oracle_c as oc
     from quill_amd import DeviceVec, VirtualPolyExpr as E
+    from quill_amd.field import fr_from_mont_limbs
     from quill_amd.logup import logup_column_device
-    nv = 20
     a = DeviceVec(dev, 1 << nv).fill_random(11)
     b = DeviceVec(dev, 1 << nv).fill_random(12)
     out = DeviceVec(dev, 1 << nv)
     beta = 0xBE7A
     s = logup_column_device(dev, nv, [a, b], E.Input(0) * E.Const(5) + E.Input(1), beta, out,
                             E.Input(1))
-    A, B, O = a.to_list(), b.to_list(), out.to_list()
-    assert s == sum(O) % R
+    A, B, O = a.to_numpy(), b.to_numpy(), out.to_numpy()
+    assert s == oc.fr_sum_prod([O])
+    n = 1 << nv
     rnd = random.Random(3)
-    for i in [0, 1, 2047, 2048, (1 << nv) - 1] + [rnd.randrange(1 << nv) for _ in range(2000)]:
-        assert O[i] * (beta + 5 * A[i] + B[i]) % R == B[i], i
+    rows = [0, 1, 2047, 2048, 4095, n // 2 - 1, n // 2, n // 2 + 2049, n - 2049, n - 2048, n - 1]
+    rows += [rnd.randrange(n) for _ in range(2000)]
+    for i in rows:
+        ai, bi, oi = (fr_from_mont_limbs(list(X[i])) for X in (A, B, O))
+        assert oi * (beta + 5 * ai + bi) % R == bi, i
+    for v in (a, b, out):
+        v.close()
 
 
 def _cmp_mle(gp, op):

@@ -156,10 +156,14 @@ def test_s_polynomial_large(dev):
         assert S[k] == exp
 
 
-@pytest.mark.parametrize("nf,ng", [(1 << 15, 1 << 15), ((1 << 15) + 3, (1 << 14) - 5), (5000, 1)])
+@pytest.mark.parametrize("nf,ng", [(1 << 15, 1 << 15), ((1 << 15) + 3, (1 << 14) - 5), (5000, 1),
+                                   ((1 << 18) + 3, (1 << 17) + 9)])
 def test_s_polynomial_multi_pass(dev, nf, ng):
-    """NTT sizes 2^16 / 2^17 run three LDS passes (11 + 7 + rest stages): spot
-    coefficients of S_k = sum_i (f_{i+k+1} g_i + g_{i+k+1} f_i) (ipa.rs:122-157)."""
+    """The NTT pass plan (mlpcs.hip ntt_plan) runs 11 stages in the first LDS
+    pass and up to 7 in each later one: 2^16 / 2^17-point transforms take two
+    passes (11 + 5, 11 + 6), M = 2^18 + 3 (a 2^20-point transform) takes three
+    (11 + 7 + 2) like every 2^20+ ML-open.  Spot coefficients of
+    S_k = sum_i (f_{i+k+1} g_i + g_{i+k+1} f_i) (ipa.rs:122-157)."""
     rnd = random.Random(nf + ng)
     f = [rnd.randrange(R) for _ in range(nf)]
     g = [rnd.randrange(R) for _ in range(ng)]

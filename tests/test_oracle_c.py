@@ -48,3 +48,29 @@ def test_c_sumcheck_matches_python():
 def test_c_baseline_runs_small():
     r = oc.bench_msm_baseline(8)
     assert r["value"] > 0 and r["cores"] == 1 and r["kind"] == "port"
+
+
+def _to_limbs(xs):
+    import numpy as np
+    return np.array([oc._mont(x, o.R_MOD) for x in xs], dtype=np.uint64)
+
+
+def test_c_checkers_match_python():
+    """The full-size checkers (Horner / MLE / sum of products / scalar mul) used
+    by the headline-size GPU tests and bench.py agree with the Python oracle."""
+    rnd = random.Random(5)
+    nv = 7
+    tabs = [[rnd.randrange(o.R_MOD) for _ in range(1 << nv)] for _ in range(3)]
+    x = rnd.randrange(o.R_MOD)
+    assert oc.fr_horner(_to_limbs(tabs[0]), x) == o.poly_eval(tabs[0], x)
+    pt = [rnd.randrange(o.R_MOD) for _ in range(nv)]
+    assert oc.fr_mle_eval(_to_limbs(tabs[1]), pt) == o.mle_evaluate(tabs[1], pt)
+    # a prefix of a longer table (mlpcs.rs:91-94 semantics)
+    assert oc.fr_mle_eval(_to_limbs(tabs[1]), pt[:4]) == o.mle_evaluate(tabs[1][:16], pt[:4])
+    assert oc.fr_sum_prod([_to_limbs(t) for t in tabs]) == \
+        sum(a * b % o.R_MOD * c for a, b, c in zip(*tabs)) % o.R_MOD
+    for s in (0, 1, o.R_MOD - 1, x):
+        assert oc.g1_mul(o.G1_GEN, s) == o.g1_mul(o.G1_GEN, s)
+    P = o.g1_mul(o.G1_GEN, 12345)
+    assert oc.g1_mul(P, x) == o.g1_mul(P, x)
+    assert oc.g1_mul(None, x) is None
