@@ -37,24 +37,50 @@ def _short(name):
 
 
 def run_pass(counter, probe_args, timeout=300):
+    """one rocprofv3 pass; `counter` is one name or a list that fits one pass
+    (MI355X_MICROARCH.md "rocprofv3 PMC slots": <= 8 SQ, 4 TCC, 2 GRBM)"""
+    counters = [counter] if isinstance(counter, str) else list(counter)
     exe = shutil.which("rocprofv3")
     if exe is None:
         raise RuntimeError("rocprofv3 not found")
-    outdir = tempfile.mkdtemp(prefix=f"qg_pmc_{counter}_")
+    outdir = tempfile.mkdtemp(prefix="qg_pmc_")
     try:
-        cmd = [exe, "--pmc", counter, "--kernel-trace", "-d", outdir, "-o", "pmc", "-f", "csv",
-               "--", sys.executable, os.path.join(ROOT, "bench.py"), "--traffic-probe"] + probe_args
+        cmd = [exe, "--pmc"] + counters + ["--kernel-trace", "-d", outdir, "-o", "pmc", "-f",
+                                           "csv", "--", sys.executable,
+                                           os.path.join(ROOT, "bench.py"), "--traffic-probe"]
+        cmd += probe_args
         p = subprocess.run(cmd, stdout=subprocess.PIPE, stderr=subprocess.STDOUT, timeout=timeout)
         if p.returncode != 0:
-            raise RuntimeError(f"rocprofv3 --pmc {counter} exited {p.returncode}: "
+            raise RuntimeError(f"rocprofv3 --pmc {counters} exited {p.returncode}: "
                                + p.stdout.decode(errors="replace")[-800:])
         rows = _read_counters(outdir)
         if not rows:
-            raise RuntimeError(f"no counter rows for {counter}")
-        return [(int(r["Dispatch_Id"]), _short(r["Kernel_Name"]), float(r["Counter_Value"]))
-                for r in rows if r["Counter_Name"] == counter]
+            raise RuntimeError(f"no counter rows for {counters}")
+        if isinstance(counter, str):
+            return [(int(r["Dispatch_Id"]), _short(r["Kernel_Name"]), float(r["Counter_Value"]))
+                    for r in rows if r["Counter_Name"] == counter]
+        return [(int(r["Dispatch_Id"]), _short(r["Kernel_Name"]), r["Counter_Name"],
+                 float(r["Counter_Value"])) for r in rows]
     finally:
         shutil.rmtree(outdir, ignore_errors=True)
+
+
+def kernel_counters(passes, probe_args, timeout=300):
+    """{kernel: {counter: value per launch}} over several passes (each a list)"""
+    out = {}
+    for counters in passes:
+        rows = run_pass(list(counters), probe_args, timeout)
+        launches = {}
+        for did, k, name, v in rows:
+            launches.setdefault(k, set()).add(did)
+            d = out.setdefault(k, {})
+            d[name] = d.get(name, 0.0) + v
+        for k, ids in launches.items():
+            for name in counters:
+                if name in out[k]:
+                    out[k][name] /= len(ids)
+            out[k]["launches"] = len(ids)
+    return out
 
 
 def collect(probe_args, timeout=300):
@@ -74,3 +100,12 @@ def collect(probe_args, timeout=300):
         d["read_bytes_per_launch"] = d.pop("read_bytes") / n
         d["write_bytes_per_launch"] = d.pop("write_bytes") / n
     return out
+
+
+if __name__ == "__main__":
+    # python pmc_traffic.py SQ_WAVES,SQ_INSTS_VALU GRBM_GUI_ACTIVE -- <bench.py probe args>
+    import json
+    argv = sys.argv[1:]
+    cut = argv.index("--") if "--" in argv else len(argv)
+    print(json.dumps(kernel_counters([a.split(",") for a in argv[:cut]], argv[cut + 1:]),
+                     indent=1))

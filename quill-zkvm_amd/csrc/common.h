@@ -148,8 +148,8 @@ struct qg_srs {
   size_t n = 0;  // number of bases
   int c = 0;     // MSM window bits (signed digits)
   int W = 0;     // number of windows = ceil(255 / c)
-  // W * n affine points; table[w * n + i] = 2^(c*w) * base_i   (infinity = (0,0))
-  qg::G1Affine* d_table = nullptr;
+  // W * n rows; table[w * n + i] = 2^(c*w) * base_i   (curve.h MsmPt layout)
+  qg::MsmPt* d_table = nullptr;
 };
 
 // scoped timer

@@ -16,6 +16,17 @@ struct G1Affine {
   QG_HD bool is_inf() const { return x.is_zero() && y.is_zero(); }
 };
 
+// One MSM window-table row (128 B = one HBM line): the affine point in the
+// 9 x 29-bit-limb Montgomery domain of curve29.h (R = 2^261), canonical, with
+// the negated point's y precomputed so a signed digit costs no arithmetic:
+//   w[0..7] x limbs 0..7, w[8..15] y limbs 0..7, w[16..23] (p - y) limbs 0..7,
+//   w[24] x limb 8, w[25] y limb 8, w[26] (p - y) limb 8,
+//   w[27] flags (bit 0: the point at infinity; the limbs are then zero).
+// A gather reads five 16-B aligned words: x, y or p - y, and the top limbs.
+struct MsmPt {
+  uint32_t w[32];
+};
+
 struct G1Xyzz {
   Fq X, Y, ZZ, ZZZ;
   QG_HD static G1Xyzz infinity() {

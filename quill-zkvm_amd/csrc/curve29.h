@@ -76,27 +76,121 @@ QG_HD X29 x29_add_affine(const X29& p, const A29& a) {
   return {X3, Y3, mul29(p.ZZ, PP), mul29(p.ZZZ, PPP)};
 }
 
-// madd-2008-s for a bucket accumulator kept lazily reduced between additions:
-// X normalized < 16p, Y normalized < 8p, ZZ/ZZZ < 2p (x29_acc_finish brings
-// it back to < 2p before it is stored).  Saves the X3/Y3 conditional
-// subtractions of every addition.
-QG_HD X29 x29_acc_madd(const X29& p, const A29& a) {
-  if (x29_is_inf(p)) return x29_from_affine(a);
-  const Q29 U2 = mul29(a.x, p.ZZ);
-  const Q29 S2 = mul29(a.y, p.ZZZ);
-  const Q29 P = normfull29(subk29(U2, p.X, F29P<FqP>::K17));  // (p, 19p)
-  const Q29 R = normfull29(subk29(S2, p.Y, F29P<FqP>::K9));   // (p, 11p)
-  if (is_zero_mod29_fast<FqP, 20>(P)) {
-    if (is_zero_mod29_fast<FqP, 20>(R)) return x29_dbl_affine(a);
-    return x29_inf();
-  }
-  const Q29 PP = sqr29(P);                 // < 3p
-  const Q29 PPP = mul29(P, PP);            // < 2p
-  const Q29 Q = mul29(p.X, PP);            // < 2p
-  const Q29 X3 = normfull29(sub29(sub29(sub29(sqr29(R), PPP), Q), Q));  // < 16p
-  const Q29 Y3 = normfull29(mulsub29(R, norm29(subk29(Q, X3, F29P<FqP>::K17)), p.Y, PPP));  // < 8p
-  return {X3, Y3, mul29(p.ZZ, PP), mul29(p.ZZZ, PPP)};
+// ---- bucket accumulation (k_msm_accumulate) ---------------------------
+// madd-2008-s (8M + 2S) on an accumulator kept lazily reduced between
+// additions.  Invariants (values in units of p; 2^261 ~ 170 p):
+//   X almost-normalized < 16p, Y normalized < 8p, ZZ / ZZZ normalized < 2p;
+// the added point (x, y) is canonical (the table holds y and p - y, so a
+// negative digit costs nothing).  Bounds (Montgomery output < a b / 170 + p):
+//   U2 = x ZZ < 1.02, S2 = y ZZZ < 1.02,
+//   P = U2 + 17p - X in (p, 18.1p) (normalized, zero-tested),
+//   R = S2 + 9p - Y in (p, 10.1p) (almost-normalized),
+//   PP < 3, PPP < 1.4, Q = X PP < 1.3, R^2 < 1.7,
+//   X3 = R^2 + 12p - PPP - 2Q in (8p, 13.7p) < 16p (one parallel carry pass),
+//   Y3 = R (Q + 17p - X3) - Y PPP + 4p < 10.1 * 18.3 / 170 + 5 < 6.1p < 8p
+//   (mulsub output is normalized), ZZ3, ZZZ3 < 2p.
+// Throughput multiplies (field29.h mul29t: one chain per column).  Returns
+// false (accumulator untouched) when P == 0 mod p: the caller runs the
+// exceptional cases (doubling / cancellation) off the main path.
+#if defined(__HIP_DEVICE_COMPILE__)
+__device__ __forceinline__ bool x29_acc_madd_tp(X29& p, const Q29& ax, const Q29& ay) {
+  const Q29 U2 = mul29t(ax, p.ZZ);
+  const Q29 S2 = mul29t(ay, p.ZZZ);
+  const Q29 P = normfull29(subk29(U2, p.X, F29P<FqP>::K17));
+  if (is_zero_mod29_fast<FqP, 20>(P)) return false;
+  const Q29 R = norm29(subk29(S2, p.Y, F29P<FqP>::K9));
+  const Q29 PP = sqr29t(P);
+  const Q29 PPP = mul29t(P, PP);
+  const Q29 Q = mul29t(p.X, PP);
+  const Q29 X3 = norm29(sub29(sub29(sub29(sqr29t(R), PPP), Q), Q));
+  const Q29 Y3 = mulsub29t(R, norm29(subk29(Q, X3, F29P<FqP>::K17)), p.Y, PPP);
+  p.ZZ = mul29t(p.ZZ, PP);
+  p.ZZZ = mul29t(p.ZZZ, PPP);
+  p.X = X3;
+  p.Y = Y3;
+  return true;
 }
+#else
+__device__ bool x29_acc_madd_tp(X29& p, const Q29& ax, const Q29& ay);
+#endif
+
+// the exceptional cases of x29_acc_madd_tp (P == 0 mod p): the point equals
+// the accumulator (R == 0: double it) or its negative (infinity -> *inf)
+QG_HD void x29_acc_madd_exc(X29& p, const Q29& ax, const Q29& ay, bool* inf) {
+  const Q29 S2 = mul29(ay, p.ZZZ);
+  const Q29 R = normfull29(subk29(S2, p.Y, F29P<FqP>::K9));
+  if (is_zero_mod29_fast<FqP, 20>(R)) {
+    A29 a;
+    a.x = ax;
+    a.y = ay;  // canonical
+    p = x29_dbl_affine(a);
+  } else {
+    *inf = true;
+  }
+}
+
+// ---- MSM table rows (curve.h MsmPt) ----------------------------------------
+// pack a canonical point (x, y < p, 29-bit limbs, R = 2^261) or infinity
+QG_HD MsmPt msm_pt_pack(const Q29& x, const Q29& y, bool inf) {
+  MsmPt r;
+#pragma unroll
+  for (int i = 0; i < 32; i++) r.w[i] = 0;
+  if (inf) {
+    r.w[27] = 1u;
+    return r;
+  }
+  // p - y (y in (0, p): BN254 G1 has no point with y = 0)
+  Q29 ny;
+  uint32_t br = 0;
+#pragma unroll
+  for (int i = 0; i < 9; i++) {
+    const uint32_t t = F29P<FqP>::P.v[i] - y.l[i] - br;
+    br = t >> 31;
+    ny.l[i] = i < 8 ? (t & M29) : t;
+  }
+#pragma unroll
+  for (int i = 0; i < 8; i++) {
+    r.w[i] = x.l[i];
+    r.w[8 + i] = y.l[i];
+    r.w[16 + i] = ny.l[i];
+  }
+  r.w[24] = x.l[8];
+  r.w[25] = y.l[8];
+  r.w[26] = ny.l[8];
+  return r;
+}
+
+QG_HD bool msm_pt_unpack(const MsmPt& a, Q29& x, Q29& y) {
+#pragma unroll
+  for (int i = 0; i < 8; i++) {
+    x.l[i] = a.w[i];
+    y.l[i] = a.w[8 + i];
+  }
+  x.l[8] = a.w[24];
+  y.l[8] = a.w[25];
+  return (a.w[27] & 1u) != 0u;
+}
+
+#if defined(__HIP_DEVICE_COMPILE__)
+// gather of one row for a signed digit: five aligned 16-B loads (80 of 128 B)
+__device__ __forceinline__ bool msm_pt_load(const MsmPt* __restrict__ table, uint32_t idx,
+                                            bool neg, Q29& x, Q29& y) {
+  const uint4* row = reinterpret_cast<const uint4*>(table + idx);
+  const uint4 x0 = row[0], x1 = row[1];
+  const uint4 y0 = row[neg ? 4 : 2], y1 = row[neg ? 5 : 3];
+  const uint4 top = row[6];
+  x.l[0] = x0.x; x.l[1] = x0.y; x.l[2] = x0.z; x.l[3] = x0.w;
+  x.l[4] = x1.x; x.l[5] = x1.y; x.l[6] = x1.z; x.l[7] = x1.w;
+  y.l[0] = y0.x; y.l[1] = y0.y; y.l[2] = y0.z; y.l[3] = y0.w;
+  y.l[4] = y1.x; y.l[5] = y1.y; y.l[6] = y1.z; y.l[7] = y1.w;
+  x.l[8] = top.x;
+  y.l[8] = neg ? top.z : top.y;
+  return (top.w & 1u) != 0u;
+}
+#else
+__device__ bool msm_pt_load(const MsmPt* __restrict__ table, uint32_t idx, bool neg, Q29& x,
+                            Q29& y);
+#endif
 
 // lazily reduced accumulator -> every coordinate < 2p
 QG_HD X29 x29_acc_finish(const X29& p) {

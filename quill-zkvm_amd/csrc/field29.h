@@ -257,7 +257,9 @@ QG_HD F29<C> mulsub29(const F29<C>& a, const F29<C>& b, const F29<C>& c, const F
 #pragma unroll
     for (int j = (k > 8 ? k - 8 : 0); j <= (k < 8 ? k : 8); j++) {
       acc += (int64_t)((uint64_t)a.l[j] * b.l[k - j]);
-      acc += (int64_t)c.l[j] * nd[k - j];
+      // both factors as int32 (c's limbs < 2^30): one v_mad_i64_i32, not an
+      // unsigned product plus a sign correction
+      acc += (int64_t)(int32_t)c.l[j] * (int64_t)nd[k - j];
     }
     if (k < 9) {
 #pragma unroll
@@ -275,6 +277,140 @@ QG_HD F29<C> mulsub29(const F29<C>& a, const F29<C>& b, const F29<C>& c, const F
   r.l[8] = (uint32_t)(acc + F29P<C>::P4.v[8]);
   return r;
 }
+
+#if defined(__HIP_DEVICE_COMPILE__)
+// ---- throughput variants (device only) -------------------------------------
+// Same arithmetic as mul29 / sqr29 / mulsub29, but every column is ONE
+// accumulation chain of v_mad_u64_u32 (inline asm: the compiler cannot
+// re-associate a column into two chains merged by v_lshl_add_u64), and the
+// modulus limbs are SGPR operands.  ~17 fewer VALU instructions per multiply
+// (+8 % multiplies/s in micro/fp29_bench.hip) at a longer dependent latency
+// (616 vs 383 ns): for kernels with many independent multiplies in flight
+// (the MSM bucket accumulation), not for latency-bound chains.
+// a * b + c with the result made opaque to the optimizer by an empty asm
+// statement (no instruction is emitted): the column stays one chain.  The
+// product itself is the compiler's v_mad_u64_u32.
+__device__ __forceinline__ uint64_t mad_vv(uint32_t a, uint32_t b, uint64_t c) {
+  uint64_t r = (uint64_t)a * b + c;
+  asm("" : "+v"(r));
+  return r;
+}
+__device__ __forceinline__ uint64_t mad_vs(uint32_t a, uint32_t b, uint64_t c) {
+  return mad_vv(a, b, c);
+}
+__device__ __forceinline__ int64_t mad_i_vv(int32_t a, int32_t b, int64_t c) {
+  int64_t r = (int64_t)a * b + c;
+  asm("" : "+v"(r));
+  return r;
+}
+__device__ __forceinline__ int64_t mad_u_signed(uint32_t a, uint32_t b, int64_t c) {
+  return (int64_t)mad_vv(a, b, (uint64_t)c);  // two's complement: same bits
+}
+__device__ __forceinline__ int64_t mad_s_signed(uint32_t a, uint32_t b, int64_t c) {
+  return (int64_t)mad_vs(a, b, (uint64_t)c);
+}
+
+template <class C>
+__device__ __forceinline__ F29<C> mul29t(const F29<C>& a, const F29<C>& b) {
+  uint32_t m[9];
+  F29<C> r;
+  uint64_t acc = 0;
+#pragma unroll
+  for (int k = 0; k < 9; k++) {
+#pragma unroll
+    for (int j = 0; j < k; j++) {
+      acc = mad_vv(a.l[j], b.l[k - j], acc);
+      acc = mad_vs(m[j], F29P<C>::P.v[k - j], acc);
+    }
+    acc = mad_vv(a.l[k], b.l[0], acc);
+    m[k] = ((uint32_t)acc * F29P<C>::INV) & M29;
+    acc = mad_vs(m[k], F29P<C>::P.v[0], acc);
+    acc >>= 29;
+  }
+#pragma unroll
+  for (int k = 9; k < 17; k++) {
+#pragma unroll
+    for (int j = k - 8; j < 9; j++) {
+      acc = mad_vv(a.l[j], b.l[k - j], acc);
+      acc = mad_vs(m[j], F29P<C>::P.v[k - j], acc);
+    }
+    r.l[k - 9] = (uint32_t)acc & M29;
+    acc >>= 29;
+  }
+  r.l[8] = (uint32_t)acc;
+  return r;
+}
+
+template <class C>
+__device__ __forceinline__ F29<C> sqr29t(const F29<C>& a) {
+  uint32_t a2[9], m[9];
+#pragma unroll
+  for (int i = 0; i < 9; i++) a2[i] = a.l[i] << 1;
+  F29<C> r;
+  uint64_t acc = 0;
+#pragma unroll
+  for (int k = 0; k < 17; k++) {
+#pragma unroll
+    for (int i = (k > 8 ? k - 8 : 0); 2 * i < k; i++) acc = mad_vv(a2[i], a.l[k - i], acc);
+    if ((k & 1) == 0) acc = mad_vv(a.l[k / 2], a.l[k / 2], acc);
+    if (k < 9) {
+#pragma unroll
+      for (int j = 0; j < k; j++) acc = mad_vs(m[j], F29P<C>::P.v[k - j], acc);
+      m[k] = ((uint32_t)acc * F29P<C>::INV) & M29;
+      acc = mad_vs(m[k], F29P<C>::P.v[0], acc);
+    } else {
+#pragma unroll
+      for (int j = k - 8; j < 9; j++) acc = mad_vs(m[j], F29P<C>::P.v[k - j], acc);
+      r.l[k - 9] = (uint32_t)acc & M29;
+    }
+    acc >>= 29;
+  }
+  r.l[8] = (uint32_t)acc;
+  return r;
+}
+
+// mulsub29 with one signed chain per column
+template <class C>
+__device__ __forceinline__ F29<C> mulsub29t(const F29<C>& a, const F29<C>& b, const F29<C>& c,
+                                            const F29<C>& d) {
+  int32_t nd[9];
+  uint32_t m[9];
+#pragma unroll
+  for (int i = 0; i < 9; i++) nd[i] = -(int32_t)d.l[i];
+  F29<C> r;
+  int64_t acc = 0;
+#pragma unroll
+  for (int k = 0; k < 17; k++) {
+#pragma unroll
+    for (int j = (k > 8 ? k - 8 : 0); j <= (k < 8 ? k : 8); j++) {
+      acc = mad_u_signed(a.l[j], b.l[k - j], acc);
+      acc = mad_i_vv((int32_t)c.l[j], nd[k - j], acc);
+    }
+    if (k < 9) {
+#pragma unroll
+      for (int j = 0; j < k; j++) acc = mad_s_signed(m[j], F29P<C>::P.v[k - j], acc);
+      m[k] = ((uint32_t)acc * F29P<C>::INV) & M29;
+      acc = mad_s_signed(m[k], F29P<C>::P.v[0], acc);
+    } else {
+#pragma unroll
+      for (int j = k - 8; j < 9; j++) acc = mad_s_signed(m[j], F29P<C>::P.v[k - j], acc);
+      acc += F29P<C>::P4.v[k - 9];
+      r.l[k - 9] = (uint32_t)acc & M29;
+    }
+    acc >>= 29;  // arithmetic
+  }
+  r.l[8] = (uint32_t)(acc + F29P<C>::P4.v[8]);
+  return r;
+}
+#else
+// host pass: declarations only (device code, never called from the host)
+template <class C>
+__device__ F29<C> mul29t(const F29<C>& a, const F29<C>& b);
+template <class C>
+__device__ F29<C> sqr29t(const F29<C>& a);
+template <class C>
+__device__ F29<C> mulsub29t(const F29<C>& a, const F29<C>& b, const F29<C>& c, const F29<C>& d);
+#endif
 
 // limb-wise sum (lazy)
 template <class C>

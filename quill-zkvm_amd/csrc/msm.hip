@@ -442,55 +442,91 @@ __global__ void k_scan_add(const uint2* __restrict__ tile_off, size_t nb, uint32
 }
 
 // ---- accumulation ---------------------------------------------------------
-__global__ void __launch_bounds__(MSM_BLOCK)
-    k_msm_accumulate(const G1Affine* __restrict__ table, const uint32_t* __restrict__ entries,
-                     const uint32_t* __restrict__ bstart, const uint32_t* __restrict__ tstart,
-                     uint32_t nb, int elog, G1Xyzz* __restrict__ partial,
-                     uint32_t* __restrict__ owner) {
-  const uint32_t t = blockIdx.x * blockDim.x + threadIdx.x;
-  const uint32_t total = tstart[nb];
-  if (t >= total) return;
-  // bucket b: largest with tstart[b] <= t
-  uint32_t lo = 0, hi = nb;
-  while (hi - lo > 1) {
-    uint32_t mid = (lo + hi) >> 1;
-    if (tstart[mid] <= t) lo = mid;
-    else hi = mid;
-  }
-  const uint32_t b = lo;
-  // the bucket's entries split into ceil(count / 2^elog) EQUAL chunks (not
-  // 2^elog-sized ones plus a remainder): every lane of a wave runs about the
-  // same trip count (+~15% lane efficiency for uniform scalars)
-  const uint32_t nch = tstart[b + 1] - tstart[b], cnt = bstart[b + 1] - bstart[b];
-  const uint32_t k = t - tstart[b];
-  const uint32_t e0 = bstart[b] + (uint32_t)(((uint64_t)k * cnt) / nch);
-  const uint32_t e1 = bstart[b] + (uint32_t)(((uint64_t)(k + 1) * cnt) / nch);
-  (void)elog;
-  // 29-bit-limb XYZZ accumulator (lazily reduced); table points are in the
-  // R = 2^261 domain
-  X29 acc = x29_inf();
-  for (uint32_t e = e0; e < e1; e++) {
-    const uint32_t ent = entries[e];
-    const G1Affine w = table[ent & 0x7fffffffu];
-    if (w.is_inf()) continue;
-    A29 a = a29_load(w);
-    if (ent >> 31) a.y = red2p29(sub29(Q29::zero(), a.y));
-    acc = x29_acc_madd(acc, a);
-  }
-  partial[t] = x29_store(x29_acc_finish(acc));
-  owner[t] = b;
+// Flat chunks: the bucket-sorted entries are cut into chunks of exactly L
+// entries regardless of bucket boundaries, one thread per chunk, so every lane
+// of a wave runs the same trip count.  A thread whose chunk crosses a bucket
+// boundary stores the finished bucket's partial sum and starts a new one.  The
+// partial of (thread t, bucket b) lives in slot t + b: unique, and the slots
+// of bucket b are the contiguous range [t_first(b) + b, t_last(b) + b] with
+// t_first(b) = bstart[b] / L, t_last(b) = (bstart[b + 1] - 1) / L.
+QG_DEV void msm_flush(G1Xyzz* partial, uint32_t* owner, uint32_t slot, uint32_t b, const X29& acc,
+                      bool inf) {
+  partial[slot] = x29_store(inf ? x29_inf() : x29_acc_finish(acc));
+  owner[slot] = b;
 }
 
-// Segmented pairwise tree over bucket partials: after the steps s = 1, 2, 4, ...
-// partial[tstart[j]] holds bucket j's sum.  Depth log2(max partials per bucket).
-__global__ void k_msm_tree_step(G1Xyzz* __restrict__ partial, const uint32_t* __restrict__ owner,
-                                const uint32_t* __restrict__ tstart, uint32_t nb, uint32_t s) {
+__global__ void __launch_bounds__(MSM_BLOCK)
+    k_msm_accumulate(const MsmPt* __restrict__ table, const uint32_t* __restrict__ entries,
+                     const uint32_t* __restrict__ bstart, uint32_t nb, uint32_t L,
+                     G1Xyzz* __restrict__ partial, uint32_t* __restrict__ owner) {
   const uint32_t t = blockIdx.x * blockDim.x + threadIdx.x;
-  if (t >= tstart[nb]) return;
-  const uint32_t b = owner[t];
-  const uint32_t off = t - tstart[b];
-  if ((off & (2 * s - 1)) == 0 && t + s < tstart[b + 1])
-    partial[t] = x29_store(x29_add(x29_load(partial[t]), x29_load(partial[t + s])));
+  const uint32_t total = bstart[nb];
+  const uint64_t e0w = (uint64_t)t * L;
+  if (e0w >= total) return;
+  const uint32_t e0 = (uint32_t)e0w;
+  const uint32_t e1 = total - e0 < L ? total : e0 + L;
+  // bucket of entry e0: the largest b with bstart[b] <= e0 (b < nb)
+  uint32_t lo = 0, hi = nb;
+  while (hi - lo > 1) {
+    const uint32_t mid = (lo + hi) >> 1;
+    if (bstart[mid] <= e0) lo = mid;
+    else hi = mid;
+  }
+  uint32_t b = lo;
+  uint32_t next = bstart[b + 1];
+  // 29-bit-limb XYZZ accumulator (lazily reduced, curve29.h x29_acc_madd_tp);
+  // rows are canonical in the R = 2^261 domain, the signed digit picks y or p - y
+  X29 acc;
+  bool inf = true;
+  uint32_t ent = entries[e0];
+  for (uint32_t e = e0; e < e1; e++) {
+    if (e == next) {  // bucket boundary (at most a few per thread)
+      msm_flush(partial, owner, t + b, b, acc, inf);
+      inf = true;
+      do {
+        b++;
+        next = bstart[b + 1];
+      } while (next <= e);
+    }
+    Q29 ax, ay;
+    const bool pinf = msm_pt_load(table, ent & 0x7fffffffu, (ent >> 31) != 0u, ax, ay);
+    if (e + 1 < e1) ent = entries[e + 1];  // next index in flight during the add
+    if (pinf) continue;
+    if (inf) {
+      acc.X = ax;
+      acc.Y = ay;
+      acc.ZZ = Q29::from_l9(F29P<FqP>::ONE);
+      acc.ZZZ = acc.ZZ;
+      inf = false;
+      continue;
+    }
+    if (!x29_acc_madd_tp(acc, ax, ay)) x29_acc_madd_exc(acc, ax, ay, &inf);
+  }
+  msm_flush(partial, owner, t + b, b, acc, inf);
+}
+
+// first / last partial slot of bucket b (nonempty)
+QG_DEV uint32_t msm_slot_first(const uint32_t* bstart, uint32_t b, uint32_t L) {
+  return bstart[b] / L + b;
+}
+QG_DEV uint32_t msm_slot_last(const uint32_t* bstart, uint32_t b, uint32_t L) {
+  return (bstart[b + 1] - 1) / L + b;
+}
+
+// Segmented pairwise tree over the partial slots: after the steps s = 1, 2,
+// 4, ... slot_first(b) holds bucket b's sum.  Slots no thread wrote carry
+// owner == ~0 and are skipped.
+__global__ void k_msm_tree_step(G1Xyzz* __restrict__ partial, const uint32_t* __restrict__ owner,
+                                const uint32_t* __restrict__ bstart, uint32_t L, uint32_t nslots,
+                                uint32_t s) {
+  const uint32_t i = blockIdx.x * blockDim.x + threadIdx.x;
+  if (i >= nslots) return;
+  const uint32_t b = owner[i];
+  if (b == 0xffffffffu) return;
+  const uint32_t f = msm_slot_first(bstart, b, L), l = msm_slot_last(bstart, b, L);
+  const uint32_t off = i - f;
+  if ((off & (2 * s - 1)) == 0 && i + s <= l)
+    partial[i] = x29_store(x29_add(x29_load(partial[i]), x29_load(partial[i + s])));
 }
 
 // ---- reduction ------------------------------------------------------------
@@ -505,23 +541,23 @@ __device__ void block_reduce_x29(X29 v, G1Xyzz* sh, G1Xyzz* out) {
   if (threadIdx.x == 0) *out = sh[0];
 }
 
-// B_j = sum of bucket j's group sums at offsets 0, step, 2 step, ... (empty
+// B_j = sum of bucket j's partial slots at offsets 0, step, 2 step, ... (empty
 // bucket -> infinity); at most MSM_COMBINE_SEQ of them
-__global__ void k_msm_combine(const G1Xyzz* __restrict__ partial, const uint32_t* __restrict__ tstart,
-                              uint32_t nb, uint32_t step, G1Xyzz* __restrict__ buckets) {
+__global__ void k_msm_combine(const G1Xyzz* __restrict__ partial, const uint32_t* __restrict__ bstart,
+                              uint32_t nb, uint32_t L, uint32_t step, G1Xyzz* __restrict__ buckets) {
   const uint32_t j = blockIdx.x * blockDim.x + threadIdx.x;
   if (j >= nb) return;
-  const uint32_t t0 = tstart[j], t1 = tstart[j + 1];
-  if (t0 == t1) {
+  if (bstart[j] == bstart[j + 1]) {
     buckets[j] = x29_store(x29_inf());
     return;
   }
-  if (t1 - t0 <= step) {
-    buckets[j] = partial[t0];
+  const uint32_t f = msm_slot_first(bstart, j, L), l = msm_slot_last(bstart, j, L);
+  if (l - f < step) {
+    buckets[j] = partial[f];
     return;
   }
-  X29 acc = x29_load(partial[t0]);
-  for (uint32_t t = t0 + step; t < t1; t += step) acc = x29_add(acc, x29_load(partial[t]));
+  X29 acc = x29_load(partial[f]);
+  for (uint32_t t = f + step; t <= l; t += step) acc = x29_add(acc, x29_load(partial[t]));
   buckets[j] = x29_store(acc);
 }
 
@@ -564,29 +600,44 @@ __global__ void k_msm_export(const G1Xyzz* __restrict__ in, G1Xyzz* __restrict__
   *out = {q29_export(p.X), q29_export(p.Y), q29_export(p.ZZ), q29_export(p.ZZZ)};
 }
 
-// table points R = 2^256 -> R = 2^261 domain (canonical), in place
-__global__ void k_srs_to261(G1Affine* __restrict__ pts, size_t n) {
+// arkworks affine points (R = 2^256 words, (0,0) = infinity) -> table rows
+// (R = 2^261 canonical 29-bit limbs, y and p - y)
+__global__ void k_srs_pack(const G1Affine* __restrict__ pts, size_t n, MsmPt* __restrict__ out) {
   const size_t i = (size_t)blockIdx.x * blockDim.x + threadIdx.x;
   if (i >= n) return;
   const G1Affine w = pts[i];
-  if (w.is_inf()) return;
-  pts[i] = {from29(q29_import(w.x)), from29(q29_import(w.y))};
+  out[i] = w.is_inf() ? msm_pt_pack(Q29::zero(), Q29::zero(), true)
+                      : msm_pt_pack(q29_import(w.x), q29_import(w.y), false);
 }
 
-__global__ void k_srs_shift(G1Affine* table, size_t N, int w, int c) {
+// table rows -> arkworks affine points (R = 2^256 words, canonical)
+__global__ void k_srs_unpack(const MsmPt* __restrict__ rows, size_t n, G1Affine* __restrict__ out) {
   const size_t i = (size_t)blockIdx.x * blockDim.x + threadIdx.x;
-  if (i >= N) return;
-  const G1Affine a = table[(size_t)(w - 1) * N + i];
-  if (a.is_inf()) {
-    table[(size_t)w * N + i] = a;
+  if (i >= n) return;
+  Q29 x, y;
+  if (msm_pt_unpack(rows[i], x, y)) {
+    out[i] = G1Affine::infinity();
     return;
   }
-  X29 p = x29_from_affine(a29_load(a));
+  out[i] = {q29_export(x), q29_export(y)};
+}
+
+// table[w] = 2^c table[w - 1] (c doublings, one inversion back to affine)
+__global__ void k_srs_shift(MsmPt* table, size_t N, int w, int c) {
+  const size_t i = (size_t)blockIdx.x * blockDim.x + threadIdx.x;
+  if (i >= N) return;
+  A29 a;
+  if (msm_pt_unpack(table[(size_t)(w - 1) * N + i], a.x, a.y)) {
+    table[(size_t)w * N + i] = msm_pt_pack(Q29::zero(), Q29::zero(), true);
+    return;
+  }
+  X29 p = x29_from_affine(a);
   for (int k = 0; k < c; k++) p = x29_dbl(p);
   // affine: x = X / ZZ, y = Y / ZZZ with one inversion
   const Q29 t = inv29(mul29(p.ZZ, p.ZZZ));
   const Q29 zzinv = mul29(t, p.ZZZ), zzzinv = mul29(t, p.ZZ);
-  table[(size_t)w * N + i] = {from29(canon29(mul29(p.X, zzinv))), from29(canon29(mul29(p.Y, zzzinv)))};
+  table[(size_t)w * N + i] = msm_pt_pack(canon29(mul29(p.X, zzinv)), canon29(mul29(p.Y, zzzinv)),
+                                         false);
 }
 
 __global__ void k_powers(Fr tau, uint64_t offset, size_t n, int K, Fr* out) {
@@ -647,12 +698,12 @@ __global__ void k_import_bases(const uint64_t* __restrict__ xy, const uint8_t* _
   out[i] = a;
 }
 
-// table 0 arrives in the arkworks R = 2^256 form; every table is kept in the
-// R = 2^261 domain of the 29-bit-limb accumulation (curve29.h)
-static void srs_build_shifts(qg_ctx* ctx, qg_srs* srs) {
+// table 0 arrives as arkworks affine points (R = 2^256) in `base`; every row
+// is kept in the R = 2^261 domain of the 29-bit-limb accumulation (curve29.h)
+static void srs_build_tables(qg_ctx* ctx, qg_srs* srs, const G1Affine* base) {
   QgTimed tm(ctx, "srs_shift");
-  hipLaunchKernelGGL(k_srs_to261, dim3(div_up(srs->n, 256)), dim3(256), 0, ctx->stream,
-                     srs->d_table, srs->n);
+  hipLaunchKernelGGL(k_srs_pack, dim3(div_up(srs->n, 256)), dim3(256), 0, ctx->stream, base,
+                     srs->n, srs->d_table);
   QG_LAUNCH_CHECK();
   for (int w = 1; w < srs->W; w++) {
     hipLaunchKernelGGL(k_srs_shift, dim3(div_up(srs->n, 256)), dim3(256), 0, ctx->stream,
@@ -672,7 +723,7 @@ static qg_srs* srs_alloc(qg_ctx* ctx, size_t n) {
   QG_CHECK(ct >= 4 && ct <= 26, QG_ERR_INVALID, "MSM window bits out of range");
   srs->W = (255 + ct - 1) / ct;
   srs->c = (255 + srs->W - 1) / srs->W;
-  hipError_t e = hipMalloc(&srs->d_table, (size_t)srs->W * n * sizeof(G1Affine));
+  hipError_t e = hipMalloc(&srs->d_table, (size_t)srs->W * n * sizeof(MsmPt));
   if (e != hipSuccess) {
     delete srs;
     throw Error(QG_ERR_OOM, "qg_srs: hipMalloc of the window tables failed");
@@ -715,20 +766,23 @@ G1Affine msm_device(qg_ctx* ctx, const qg_srs* srs, const Fr* d_scalars, size_t 
     uint32_t* entries = ctx->scratch_as<uint32_t>("msm_entries", max_entries + 1);
     const int ntiles = (int)div_up(nb, SCAN_TILE);
     uint2* tile_tot = ctx->scratch_as<uint2>("msm_tiles", ntiles);
-    // entries per accumulation thread: ~half the mean bucket load, so a bucket
-    // has ~2 partials on average while keeping >> 256 CUs of threads
-    int elog = 4;
-    while (elog < 7 && ((size_t)2 << (elog + 1)) * nb <= max_entries) elog++;
-    const size_t max_threads = (max_entries >> elog) + nb + 1;
-    G1Xyzz* partial = ctx->scratch_as<G1Xyzz>("msm_partial", max_threads);
-    uint32_t* owner = ctx->scratch_as<uint32_t>("msm_owner", max_threads);
+    // entries per accumulation thread (flat chunks, k_msm_accumulate): 64 at
+    // the headline sizes, fewer while that would leave < 8 waves of threads per
+    // resident slot (256 CUs x 12 waves)
+    int elog = 6;
+    while (elog > 2 && (max_entries >> elog) < (size_t)ctx->num_cus() * 12 * 64 * 8) elog--;
+    const uint32_t L = 1u << elog;
+    const size_t max_threads = div_up(max_entries, L);
+    const size_t nslots = max_threads + nb + 1;  // partial slot of (thread t, bucket b): t + b
+    G1Xyzz* partial = ctx->scratch_as<G1Xyzz>("msm_partial", nslots);
+    uint32_t* owner = ctx->scratch_as<uint32_t>("msm_owner", nslots);
     G1Xyzz* buckets = ctx->scratch_as<G1Xyzz>("msm_buckets", nb);
     const uint32_t nseg = div_up(nb, MSM_SEG);
     const uint32_t nred = div_up(nseg, MSM_BLOCK);
     G1Xyzz* red = ctx->scratch_as<G1Xyzz>("msm_red", nred + 2);
     QG_CHECK(ntiles <= 1024 * 64 && H <= 1024 && NL <= 4096, QG_ERR_UNSUPPORTED,
              "bucket count too large");
-    QG_CHECK(max_threads < 0xffffffffull && max_chunks < 0xffffffffull, QG_ERR_UNSUPPORTED,
+    QG_CHECK(nslots < 0xffffffffull && max_chunks < 0xffffffffull, QG_ERR_UNSUPPORTED,
              "MSM too large");
 
     {
@@ -792,11 +846,11 @@ G1Affine msm_device(qg_ctx* ctx, const qg_srs* srs, const Fr* d_scalars, size_t 
                          ctx->stream, tmp, gstart, cbase, cgroup, misc, NL, chist, coff, entries);
       QG_LAUNCH_CHECK();
     }
+    QG_HIP(hipMemsetAsync(owner, 0xff, nslots * sizeof(uint32_t), ctx->stream));
     {
       QgTimed tm(ctx, "msm_accumulate");
       hipLaunchKernelGGL(k_msm_accumulate, dim3(div_up(max_threads, MSM_BLOCK)), dim3(MSM_BLOCK),
-                         0, ctx->stream, srs->d_table, entries, bstart, tstart, nb, elog, partial,
-                         owner);
+                         0, ctx->stream, srs->d_table, entries, bstart, nb, L, partial, owner);
       QG_LAUNCH_CHECK();
     }
     uint32_t max_tpb = 0;
@@ -804,18 +858,20 @@ G1Affine msm_device(qg_ctx* ctx, const qg_srs* srs, const Fr* d_scalars, size_t 
     QG_HIP(hipStreamSynchronize(ctx->stream));
     {
       QgTimed tm(ctx, "msm_reduce");
-      // tree steps only until every bucket has <= MSM_COMBINE_SEQ group sums
+      // tree steps only until every bucket has <= MSM_COMBINE_SEQ partials
       // left; the combine kernel adds those sequentially (one launch instead
-      // of log2(max partials) full-grid steps for typical, unskewed scalars)
+      // of log2(max partials) full-grid steps for typical, unskewed scalars).
+      // A bucket of count c spans at most ceil(c / L) + 1 slots.
+      const uint32_t max_slots = max_tpb + 1;
       uint32_t st = 1;
-      while ((size_t)st * MSM_COMBINE_SEQ < max_tpb) {
-        hipLaunchKernelGGL(k_msm_tree_step, dim3(div_up(max_threads, MSM_BLOCK)), dim3(MSM_BLOCK),
-                           0, ctx->stream, partial, owner, tstart, nb, st);
+      while ((size_t)st * MSM_COMBINE_SEQ < max_slots) {
+        hipLaunchKernelGGL(k_msm_tree_step, dim3(div_up(nslots, MSM_BLOCK)), dim3(MSM_BLOCK), 0,
+                           ctx->stream, partial, owner, bstart, L, (uint32_t)nslots, st);
         QG_LAUNCH_CHECK();
         st <<= 1;
       }
       hipLaunchKernelGGL(k_msm_combine, dim3(div_up(nb, MSM_BLOCK)), dim3(MSM_BLOCK), 0,
-                         ctx->stream, partial, tstart, nb, st, buckets);
+                         ctx->stream, partial, bstart, nb, L, st, buckets);
       QG_LAUNCH_CHECK();
       hipLaunchKernelGGL(k_msm_reduce, dim3(nred), dim3(MSM_BLOCK), 0, ctx->stream, buckets, nb,
                          red);
@@ -908,10 +964,11 @@ int qg_srs_upload(qg_ctx* ctx, const uint64_t* affine_xy, const uint8_t* infinit
       d_inf = ctx->scratch_as<uint8_t>("srs_up_inf", n);
       QG_HIP(hipMemcpyAsync(d_inf, infinity, n, hipMemcpyHostToDevice, ctx->stream));
     }
+    G1Affine* d_base = ctx->scratch_as<G1Affine>("srs_base", n);
     hipLaunchKernelGGL(k_import_bases, dim3(div_up(n, 256)), dim3(256), 0, ctx->stream, d_xy,
-                       d_inf, n, srs->d_table);
+                       d_inf, n, d_base);
     QG_LAUNCH_CHECK();
-    srs_build_shifts(ctx, srs);
+    srs_build_tables(ctx, srs, d_base);
     ctx->sync();
   });
   if (rc != QG_OK) {
@@ -950,6 +1007,7 @@ int qg_srs_generate_range(qg_ctx* ctx, const uint64_t tau[4], const uint64_t* g_
     Fr* d_pow = ctx->scratch_as<Fr>("srs_pow", n);
     G1Xyzz* d_fbb = ctx->scratch_as<G1Xyzz>("srs_fbb", 32);
     G1Affine* d_fb = ctx->scratch_as<G1Affine>("srs_fb", 32 * 256);
+    G1Affine* d_base = ctx->scratch_as<G1Affine>("srs_base", n);
     {
       QgTimed tm(ctx, "srs_generate");
       const int K = 64;
@@ -961,10 +1019,10 @@ int qg_srs_generate_range(qg_ctx* ctx, const uint64_t tau[4], const uint64_t* g_
       hipLaunchKernelGGL(k_fb_table, dim3(32), dim3(256), 0, ctx->stream, d_fbb, d_fb);
       QG_LAUNCH_CHECK();
       hipLaunchKernelGGL(k_fb_mul, dim3(div_up(n, 256)), dim3(256), 0, ctx->stream, d_fb, d_pow,
-                         n, srs->d_table);
+                         n, d_base);
       QG_LAUNCH_CHECK();
     }
-    srs_build_shifts(ctx, srs);
+    srs_build_tables(ctx, srs, d_base);
     ctx->sync();
   });
   if (rc != QG_OK) {
@@ -999,18 +1057,16 @@ int qg_srs_download(const qg_srs* srs, size_t offset, size_t n, uint64_t* affine
   if (!srs || (!affine_xy && n) || offset + n > srs->n) return QG_ERR_INVALID;
   qg_ctx* ctx = srs->ctx;
   return qg_guard(ctx, [&] {
+    if (n == 0) return;
+    QG_HIP(hipSetDevice(ctx->device));
     std::vector<G1Affine> h(n);
-    QG_HIP(hipMemcpyAsync(h.data(), srs->d_table + offset, n * sizeof(G1Affine),
-                          hipMemcpyDeviceToHost, ctx->stream));
+    G1Affine* d = ctx->scratch_as<G1Affine>("srs_download", n);
+    hipLaunchKernelGGL(k_srs_unpack, dim3(div_up(n, 256)), dim3(256), 0, ctx->stream,
+                       srs->d_table + offset, n, d);
+    QG_LAUNCH_CHECK();
+    QG_HIP(hipMemcpyAsync(h.data(), d, n * sizeof(G1Affine), hipMemcpyDeviceToHost, ctx->stream));
     ctx->sync();
-    // R = 2^261 -> arkworks R = 2^256: Montgomery multiply by 2^251 (plain)
-    Fq c = Fq::zero();
-    c.v[7] = 0x08000000u;
-    for (size_t i = 0; i < n; i++) {
-      G1Affine a = h[i];
-      if (!a.is_inf()) a = {a.x * c, a.y * c};
-      g1_export(a, affine_xy + 8 * i, infinity ? infinity + i : nullptr);
-    }
+    for (size_t i = 0; i < n; i++) g1_export(h[i], affine_xy + 8 * i, infinity ? infinity + i : nullptr);
   });
 }
 

@@ -85,6 +85,50 @@ __device__ __forceinline__ F29 mul29s(const F29& a, const F29& b) {
   return r;
 }
 
+// one accumulation chain per column, kept by inline asm (the compiler cannot
+// re-associate it into split chains merged by 64-bit adds); p limbs in SGPRs
+__device__ __forceinline__ uint64_t mad_asm(uint32_t a, uint32_t b, uint64_t c) {
+  uint64_t r, cc;
+  asm("v_mad_u64_u32 %0, %1, %2, %3, %4" : "=v"(r), "=s"(cc) : "v"(a), "v"(b), "v"(c));
+  return r;
+}
+__device__ __forceinline__ uint64_t mad_asm_s(uint32_t a, uint32_t b, uint64_t c) {
+  uint64_t r, cc;
+  asm("v_mad_u64_u32 %0, %1, %2, %3, %4" : "=v"(r), "=s"(cc) : "v"(a), "s"(b), "v"(c));
+  return r;
+}
+__device__ __forceinline__ F29 mul29a(const F29& a, const F29& b) {
+  constexpr uint32_t P[9] = {0x187cfd47u, 0x10460b6u, 0x1c72a34fu, 0x2d522d0u, 0x1585d978u,
+                             0x2db40c0u,  0xa6e141u,  0xe5c2634u,  0x30644eu};
+  uint32_t m[9];
+  F29 r;
+  uint64_t acc = 0;
+#pragma unroll
+  for (int k = 0; k < 9; k++) {
+#pragma unroll
+    for (int j = 0; j < k; j++) {
+      acc = mad_asm(a.l[j], b.l[k - j], acc);
+      acc = mad_asm_s(m[j], P[k - j], acc);
+    }
+    acc = mad_asm(a.l[k], b.l[0], acc);
+    m[k] = ((uint32_t)acc * INV29) & M29;
+    acc = mad_asm_s(m[k], P[0], acc);
+    acc >>= 29;
+  }
+#pragma unroll
+  for (int k = 9; k < 17; k++) {
+#pragma unroll
+    for (int j = k - 8; j < 9; j++) {
+      acc = mad_asm(a.l[j], b.l[k - j], acc);
+      acc = mad_asm_s(m[j], P[k - j], acc);
+    }
+    r.l[k - 9] = (uint32_t)acc & M29;
+    acc >>= 29;
+  }
+  r.l[8] = (uint32_t)acc;
+  return r;
+}
+
 __device__ __forceinline__ F29 to29(const Fq& x) {
   F29 r;
 #pragma unroll
@@ -116,7 +160,8 @@ __device__ __forceinline__ void mulv(Fq& a, F29& a29, const Fq& b, const F29& b2
   if constexpr (V == 0) a = a * b;
   else if constexpr (V == 1) a29 = mul29(a29, b29);
   else if constexpr (V == 2) a29 = mul29s<2>(a29, b29);
-  else a29 = mul29s<4>(a29, b29);
+  else if constexpr (V == 3) a29 = mul29s<4>(a29, b29);
+  else a29 = mul29a(a29, b29);
 }
 
 template <int V>
@@ -164,8 +209,9 @@ __global__ void k_check(const Fq* x, const Fq* y, Fq* o29, Fq* oref, int n) {
   Fq z = from29(mul29(to29(x[i]), to29(y[i])));
   Fq z2 = from29(mul29s<2>(to29(x[i]), to29(y[i])));
   Fq z4 = from29(mul29s<4>(to29(x[i]), to29(y[i])));
+  Fq za = from29(mul29a(to29(x[i]), to29(y[i])));
   for (int l = 0; l < 8; l++)
-    if (z2.v[l] != z.v[l] || z4.v[l] != z.v[l]) z.v[0] ^= 1;  // poison -> mismatch
+    if (z2.v[l] != z.v[l] || z4.v[l] != z.v[l] || za.v[l] != z.v[l]) z.v[0] ^= 1;  // poison
   // z < 2p: reduce once
   uint32_t t[8];
   for (int l = 0; l < 8; l++) t[l] = z.v[l];
@@ -259,5 +305,6 @@ int main() {
   run<1>("mont29_9limb", io);
   run<2>("mont29_split2", io);
   run<3>("mont29_split4", io);
+  run<4>("mont29_asm_1chain", io);
   return bad ? 1 : 0;
 }
