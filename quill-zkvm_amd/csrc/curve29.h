@@ -110,7 +110,7 @@ __device__ __forceinline__ bool x29_acc_madd_tp(X29& p, const Q29& ax, const Q29
   p.Y = Y3;
   return true;
 }
-#else
+#elif defined(__HIP__)
 __device__ bool x29_acc_madd_tp(X29& p, const Q29& ax, const Q29& ay);
 #endif
 
@@ -187,10 +187,52 @@ __device__ __forceinline__ bool msm_pt_load(const MsmPt* __restrict__ table, uin
   y.l[8] = neg ? top.z : top.y;
   return (top.w & 1u) != 0u;
 }
-#else
+#elif defined(__HIP__)
 __device__ bool msm_pt_load(const MsmPt* __restrict__ table, uint32_t idx, bool neg, Q29& x,
                             Q29& y);
 #endif
+
+// XYZZ accumulator in its 29-bit limbs as stored by the bucket accumulation
+// (144 B, no reduction or re-limbing at the store); readers finish it with
+// x29_acc_finish
+struct X29Raw {
+  uint4 q[9];
+};
+
+QG_HD X29Raw x29_raw(const X29& p) {
+  uint32_t w[36];
+#pragma unroll
+  for (int i = 0; i < 9; i++) {
+    w[i] = p.X.l[i];
+    w[9 + i] = p.Y.l[i];
+    w[18 + i] = p.ZZ.l[i];
+    w[27 + i] = p.ZZZ.l[i];
+  }
+  X29Raw r;
+#pragma unroll
+  for (int k = 0; k < 9; k++) r.q[k] = make_uint4(w[4 * k], w[4 * k + 1], w[4 * k + 2], w[4 * k + 3]);
+  return r;
+}
+
+QG_HD X29 x29_unraw(const X29Raw& r) {
+  uint32_t w[36];
+#pragma unroll
+  for (int k = 0; k < 9; k++) {
+    w[4 * k] = r.q[k].x;
+    w[4 * k + 1] = r.q[k].y;
+    w[4 * k + 2] = r.q[k].z;
+    w[4 * k + 3] = r.q[k].w;
+  }
+  X29 p;
+#pragma unroll
+  for (int i = 0; i < 9; i++) {
+    p.X.l[i] = w[i];
+    p.Y.l[i] = w[9 + i];
+    p.ZZ.l[i] = w[18 + i];
+    p.ZZZ.l[i] = w[27 + i];
+  }
+  return p;
+}
 
 // lazily reduced accumulator -> every coordinate < 2p
 QG_HD X29 x29_acc_finish(const X29& p) {

@@ -402,7 +402,7 @@ __device__ __forceinline__ F29<C> mulsub29t(const F29<C>& a, const F29<C>& b, co
   r.l[8] = (uint32_t)(acc + F29P<C>::P4.v[8]);
   return r;
 }
-#else
+#elif defined(__HIP__)
 // host pass: declarations only (device code, never called from the host)
 template <class C>
 __device__ F29<C> mul29t(const F29<C>& a, const F29<C>& b);

@@ -28,8 +28,7 @@ using namespace qg;
 
 namespace qg {
 
-static constexpr int MSM_SEG = 8;       // buckets per reduction segment
-static constexpr int MSM_COMBINE_SEQ = 16;  // group sums a bucket's combine adds sequentially
+static constexpr int MSM_COMBINE_SEQ = 64;  // partials a bucket's combine adds sequentially
 static constexpr int MSM_BLOCK = 256;
 
 // window size for an SRS of n bases (tuned later)
@@ -42,32 +41,53 @@ static int msm_window_bits(size_t n) {
   return c;
 }
 
-QG_DEV uint32_t scalar_bits(const uint32_t s[8], int lo, int c) {
-  if (lo >= 256) return 0;
-  int li = lo >> 5, sh = lo & 31;
-  uint64_t w = s[li];
-  if (li + 1 < 8) w |= (uint64_t)s[li + 1] << 32;
-  return (uint32_t)(w >> sh) & ((1u << c) - 1u);
+// canonical words of a Montgomery-form scalar, x 2^-256 mod r: the 29-bit
+// Montgomery reduction (mul29 by the plain integer 2^5: 2^5 2^-261 = 2^-256),
+// no 32-bit carry chains
+QG_DEV Fr fr_canon29(const Fr& x) {
+  F29<FrP> k = F29<FrP>::zero();
+  k.l[0] = 32;
+  return from29(canon29(mul29(to29(x), k)));
 }
 
-// signed c-bit digit decomposition, emit(w, bucket, neg) for nonzero digits
+// signed c-bit digit decomposition of a CANONICAL scalar (8 words), emit(w,
+// bucket, neg) for nonzero digits.  The window walks the words by funnel
+// shifts (v_alignbit), all register-resident: no dynamically indexed array
+// (which would live in scratch memory).  c < 32.
 template <class Emit>
-QG_DEV void for_each_digit(const Fr& mont_scalar, int c, int W, Emit&& emit) {
-  Fr s = from_mont(mont_scalar);
+QG_DEV void for_each_digit(const Fr& canon, int c, int W, Emit&& emit) {
+  uint32_t v[8];
+#pragma unroll
+  for (int i = 0; i < 8; i++) v[i] = canon.v[i];
+  const uint32_t mask = (1u << c) - 1u;
   const uint32_t half = 1u << (c - 1);
   const uint32_t full = 1u << c;
   uint32_t carry = 0;
   for (int w = 0; w < W; w++) {
-    uint32_t d = scalar_bits(s.v, w * c, c) + carry;
+    const uint32_t d = (v[0] & mask) + carry;
     if (d > half) {
       carry = 1;
-      uint32_t mag = full - d;  // digit = d - 2^c < 0
+      const uint32_t mag = full - d;  // digit = d - 2^c < 0
       if (mag) emit(w, mag - 1, true);
     } else {
       carry = 0;
       if (d) emit(w, d - 1, false);
     }
+#pragma unroll
+    for (int i = 0; i < 7; i++) v[i] = __builtin_amdgcn_alignbit(v[i + 1], v[i], (uint32_t)c);
+    v[7] >>= c;
   }
+}
+
+// XCD-aware tile order: workgroup b runs on XCD b % 8 (placement is a speed
+// hint only, never assumed for correctness), so tile t = start(b % 8) + b / 8
+// gives every XCD one contiguous range of tiles.  The runs that neighbouring
+// tiles write into one group / bucket region are then adjacent in the same
+// L2, which merges their partial lines before write-back.  A bijection of
+// [0, G).
+QG_DEV uint32_t xcd_tile(uint32_t b, uint32_t G) {
+  const uint32_t x = b & 7u, q = G >> 3, r = G & 7u;
+  return x * q + (x < r ? x : r) + (b >> 3);
 }
 
 // ---- bucketing: two-pass LDS-histogram radix sort ------------------------
@@ -80,18 +100,40 @@ static constexpr int SORT_TILE_MAX = 1024;                  // scalars per block
 static constexpr size_t SORT_LDS_A = 72 * 1024;             // LDS budget for staged entries (2 blocks/CU)
 static constexpr int SORT_CHUNK = 8192;                     // entries per block (pass B)
 
+// Pass A histogram; also writes every scalar's canonical words (`canon`), so
+// the scatter pass reads them without a second Montgomery reduction.
 __global__ void __launch_bounds__(SORT_BLOCK)
     k_sortA_hist(const Fr* __restrict__ scalars, size_t n, int c, int W, int LO, int H,
-                 uint32_t nblk, uint32_t tile, uint32_t* __restrict__ ghist) {
+                 uint32_t nblk, uint32_t tile, uint32_t* __restrict__ hrow, Fr* __restrict__ canon) {
   extern __shared__ uint32_t hist[];
   for (int g = threadIdx.x; g < H; g += blockDim.x) hist[g] = 0;
   __syncthreads();
-  const size_t base = (size_t)blockIdx.x * tile;
+  const uint32_t tb = xcd_tile(blockIdx.x, nblk);
+  const size_t base = (size_t)tb * tile;
   const size_t end = base + tile < n ? base + tile : n;
-  for (size_t i = base + threadIdx.x; i < end; i += blockDim.x)
-    for_each_digit(scalars[i], c, W, [&](int, uint32_t b, bool) { atomicAdd(&hist[b >> LO], 1u); });
+  static_assert(SORT_TILE_MAX % SORT_BLOCK == 0, "pass-A tile must split evenly over the block");
+  for (size_t i = base + threadIdx.x; i < end; i += blockDim.x) {
+    const Fr s = fr_canon29(scalars[i]);
+    canon[i] = s;
+    for_each_digit(s, c, W, [&](int, uint32_t b, bool) { atomicAdd(&hist[b >> LO], 1u); });
+  }
   __syncthreads();
-  for (int g = threadIdx.x; g < H; g += blockDim.x) ghist[(size_t)g * nblk + blockIdx.x] = hist[g];
+  // row-major (tile, group): one contiguous row per block; transposed for the scan
+  for (int g = threadIdx.x; g < H; g += blockDim.x) hrow[(size_t)tb * H + g] = hist[g];
+}
+
+// out[c][r] = in[r][c] for a rows x cols u32 matrix (32 x 32 LDS tiles)
+__global__ void __launch_bounds__(256)
+    k_transpose32(const uint32_t* __restrict__ in, uint32_t rows, uint32_t cols,
+                  uint32_t* __restrict__ out) {
+  __shared__ uint32_t tile[32][33];
+  const uint32_t c0 = blockIdx.x * 32, r0 = blockIdx.y * 32;
+  const uint32_t tx = threadIdx.x & 31, ty = threadIdx.x >> 5;
+  for (uint32_t k = ty; k < 32; k += 8)
+    if (r0 + k < rows && c0 + tx < cols) tile[k][tx] = in[(size_t)(r0 + k) * cols + c0 + tx];
+  __syncthreads();
+  for (uint32_t k = ty; k < 32; k += 8)
+    if (c0 + k < cols && r0 + tx < rows) out[(size_t)(c0 + k) * rows + r0 + tx] = tile[tx][k];
 }
 
 // Block-local exclusive scan of n <= 4 * SORT_BLOCK counts in LDS (in place).
@@ -132,40 +174,77 @@ __device__ __forceinline__ int lds_upper(const uint32_t* off, int n, uint32_t p)
 }
 
 // Pass A scatter: digits of the block's tile are bucketed by group in LDS
-// (entry + its group id), then written out as contiguous per-group runs
+// (entry + its bucket), then written out as contiguous per-group runs
 // (coalesced stores) through a per-block base table, no per-element search.
+// The block's counts and global offsets are contiguous rows (hrow / orow).
+// Output per digit: the table entry (u32) and the bucket's low LO bits (u16).
 __global__ void __launch_bounds__(SORT_BLOCK)
-    k_sortA_scatter(const Fr* __restrict__ scalars, size_t n, size_t N, int c, int W, int LO, int H,
-                    uint32_t nblk, uint32_t tile, const uint32_t* __restrict__ ghist,
-                    const uint32_t* __restrict__ goff, unsigned long long* __restrict__ tmp) {
+    k_sortA_scatter(const Fr* __restrict__ canon, size_t n, size_t N, int c, int W, int LO, int H,
+                    uint32_t nblk, uint32_t tile, const uint32_t* __restrict__ hrow,
+                    const uint32_t* __restrict__ orow, uint32_t* __restrict__ tmp_e,
+                    uint16_t* __restrict__ tmp_l) {
   extern __shared__ __attribute__((aligned(16))) unsigned char smem[];
-  unsigned long long* ent = reinterpret_cast<unsigned long long*>(smem);
-  uint16_t* grp = reinterpret_cast<uint16_t*>(ent + (size_t)tile * W);
-  uint32_t* loff = reinterpret_cast<uint32_t*>(grp + (((size_t)tile * W + 1) & ~(size_t)1));
+  uint32_t* ent = reinterpret_cast<uint32_t*>(smem);
+  uint32_t* bkt = ent + (size_t)tile * W;
+  uint32_t* loff = bkt + (size_t)tile * W;
   uint32_t* cur = loff + H;
   uint32_t* gb = cur + H;
   uint32_t* scr = gb + H;
+  (void)scr;
+  const uint32_t tb = xcd_tile(blockIdx.x, nblk);
+  // rows prepared by k_sortA_rows: the tile's local run starts and global bases
   for (int g = threadIdx.x; g < H; g += blockDim.x) {
-    loff[g] = ghist[(size_t)g * nblk + blockIdx.x];
+    loff[g] = hrow[(size_t)tb * H + g];
+    gb[g] = orow[(size_t)tb * H + g];
     cur[g] = 0;
   }
   __syncthreads();
-  lds_exscan(loff, H, scr);
-  for (int g = threadIdx.x; g < H; g += blockDim.x)
-    gb[g] = goff[(size_t)g * nblk + blockIdx.x] - loff[g];
-  const size_t base = (size_t)blockIdx.x * tile;
+  const size_t base = (size_t)tb * tile;
   const size_t end = base + tile < n ? base + tile : n;
-  for (size_t i = base + threadIdx.x; i < end; i += blockDim.x)
-    for_each_digit(scalars[i], c, W, [&](int w, uint32_t b, bool neg) {
+  // the thread's scalars (tile <= SORT_TILE_MAX) are loaded before the digit loops
+  constexpr int PER = SORT_TILE_MAX / SORT_BLOCK;
+  Fr sv[PER];
+#pragma unroll
+  for (int j = 0; j < PER; j++) {
+    const size_t i = base + threadIdx.x + (size_t)j * SORT_BLOCK;
+    if (i < end) sv[j] = canon[i];
+  }
+#pragma unroll
+  for (int j = 0; j < PER; j++) {
+    const size_t i = base + threadIdx.x + (size_t)j * SORT_BLOCK;
+    if (i >= end) break;
+    for_each_digit(sv[j], c, W, [&](int w, uint32_t b, bool neg) {
       const uint32_t g = b >> LO;
       const uint32_t slot = loff[g] + atomicAdd(&cur[g], 1u);
-      const uint32_t e = (uint32_t)((size_t)w * N + i) | (neg ? 0x80000000u : 0u);
-      ent[slot] = ((unsigned long long)b << 32) | e;
-      grp[slot] = (uint16_t)g;
+      ent[slot] = (uint32_t)((size_t)w * N + i) | (neg ? 0x80000000u : 0u);
+      bkt[slot] = b;
     });
+  }
   __syncthreads();
   const uint32_t total = loff[H - 1] + cur[H - 1];
-  for (uint32_t p = threadIdx.x; p < total; p += blockDim.x) tmp[gb[grp[p]] + p] = ent[p];
+  const uint32_t lmask = (1u << LO) - 1u;
+  for (uint32_t p = threadIdx.x; p < total; p += blockDim.x) {
+    const uint32_t b = bkt[p];
+    const uint32_t dst = gb[b >> LO] + p;
+    tmp_e[dst] = ent[p];
+    tmp_l[dst] = (uint16_t)(b & lmask);
+  }
+}
+
+// per tile row (one block each): hrow <- exclusive scan of the tile's group
+// counts (its local run starts), orow <- global offset - local start (the base
+// that the scatter adds to an LDS position)
+__global__ void __launch_bounds__(SORT_BLOCK)
+    k_sortA_rows(uint32_t* __restrict__ hrow, uint32_t* __restrict__ orow, int H) {
+  __shared__ uint32_t a[4 * SORT_BLOCK], scr[SORT_BLOCK];
+  const size_t r = (size_t)blockIdx.x * H;
+  for (int g = threadIdx.x; g < H; g += blockDim.x) a[g] = hrow[r + g];
+  __syncthreads();
+  lds_exscan(a, H, scr);
+  for (int g = threadIdx.x; g < H; g += blockDim.x) {
+    hrow[r + g] = a[g];
+    orow[r + g] -= a[g];
+  }
 }
 
 // groups -> chunks (single block): gstart[g] = goff[g*nblk], chunk bases, chunk->group map
@@ -204,19 +283,28 @@ __global__ void __launch_bounds__(1024)
 }
 
 __global__ void __launch_bounds__(SORT_BLOCK)
-    k_sortB_hist(const unsigned long long* __restrict__ tmp, const uint32_t* __restrict__ gstart,
+    k_sortB_hist(const uint16_t* __restrict__ tmp_l, const uint32_t* __restrict__ gstart,
                  const uint32_t* __restrict__ cbase, const uint32_t* __restrict__ chunk_group,
                  const uint32_t* __restrict__ nchunks, int NL, uint32_t* __restrict__ chist) {
   extern __shared__ uint32_t hist[];
-  const uint32_t k = blockIdx.x;
-  if (k >= *nchunks) return;
+  const uint32_t nch = *nchunks;
+  if (blockIdx.x >= nch) return;
+  const uint32_t k = xcd_tile(blockIdx.x, nch);
   const uint32_t g = chunk_group[k];
   const uint32_t s = gstart[g] + (k - cbase[g]) * SORT_CHUNK;
   const uint32_t e = min(s + SORT_CHUNK, gstart[g + 1]);
   for (int l = threadIdx.x; l < NL; l += blockDim.x) hist[l] = 0;
   __syncthreads();
-  for (uint32_t p = s + threadIdx.x; p < e; p += blockDim.x)
-    atomicAdd(&hist[(uint32_t)(tmp[p] >> 32) & (NL - 1)], 1u);
+  constexpr int PER = SORT_CHUNK / SORT_BLOCK;
+  uint32_t lv[PER];
+#pragma unroll
+  for (int j = 0; j < PER; j++) {
+    const uint32_t p = s + threadIdx.x + j * SORT_BLOCK;
+    lv[j] = p < e ? (uint32_t)tmp_l[p] : 0xffffffffu;
+  }
+#pragma unroll
+  for (int j = 0; j < PER; j++)
+    if (lv[j] != 0xffffffffu) atomicAdd(&hist[lv[j]], 1u);
   __syncthreads();
   for (int l = threadIdx.x; l < NL; l += blockDim.x) chist[(size_t)k * NL + l] = hist[l];
 }
@@ -228,6 +316,7 @@ __global__ void k_sort_bucket_count(const uint32_t* __restrict__ cbase, const ui
   if (b >= nb) return;
   const uint32_t g = b >> LO, l = b & ((1u << LO) - 1);
   uint32_t c = 0;
+#pragma unroll 8
   for (uint32_t k = cbase[g]; k < cbase[g + 1]; k++) c += chist[((size_t)k << LO) + l];
   counts[b] = c;
 }
@@ -240,6 +329,7 @@ __global__ void k_sort_chunk_offsets(const uint32_t* __restrict__ cbase,
   if (b >= nb) return;
   const uint32_t g = b >> LO, l = b & ((1u << LO) - 1);
   uint32_t run = bstart[b];
+#pragma unroll 8
   for (uint32_t k = cbase[g]; k < cbase[g + 1]; k++) {
     const size_t idx = ((size_t)k << LO) + l;
     coff[idx] = run;  // chunk k's output offset for bucket b
@@ -249,8 +339,10 @@ __global__ void k_sort_chunk_offsets(const uint32_t* __restrict__ cbase,
 
 // Pass B scatter: the chunk is counting-sorted by the low bucket bits in LDS,
 // then each bucket run is written contiguously at its chunk offset.
+static_assert(SORT_CHUNK % SORT_BLOCK == 0, "pass-B chunk must split evenly over the block");
 __global__ void __launch_bounds__(SORT_BLOCK)
-    k_sortB_scatter(const unsigned long long* __restrict__ tmp, const uint32_t* __restrict__ gstart,
+    k_sortB_scatter(const uint32_t* __restrict__ tmp_e, const uint16_t* __restrict__ tmp_l,
+                    const uint32_t* __restrict__ gstart,
                     const uint32_t* __restrict__ cbase, const uint32_t* __restrict__ chunk_group,
                     const uint32_t* __restrict__ nchunks, int NL, const uint32_t* __restrict__ chist,
                     const uint32_t* __restrict__ coff, uint32_t* __restrict__ entries) {
@@ -261,12 +353,13 @@ __global__ void __launch_bounds__(SORT_BLOCK)
   uint32_t* cur = loff + NL;
   uint32_t* cb = cur + NL;
   uint32_t* scr = cb + NL;
-  const uint32_t k = blockIdx.x;
-  if (k >= *nchunks) return;
+  const uint32_t nch = *nchunks;
+  if (blockIdx.x >= nch) return;
+  const uint32_t k = xcd_tile(blockIdx.x, nch);
   const uint32_t g = chunk_group[k];
   const uint32_t s = gstart[g] + (k - cbase[g]) * SORT_CHUNK;
   const uint32_t e = min(s + SORT_CHUNK, gstart[g + 1]);
-  // the chunk's histogram was computed by k_sortB_hist (chist), so tmp is read once here
+  // the chunk's histogram was computed by k_sortB_hist (chist)
   for (int l = threadIdx.x; l < NL; l += blockDim.x) {
     loff[l] = chist[(size_t)k * NL + l];
     cur[l] = 0;
@@ -274,11 +367,22 @@ __global__ void __launch_bounds__(SORT_BLOCK)
   __syncthreads();
   lds_exscan(loff, NL, scr);
   for (int l = threadIdx.x; l < NL; l += blockDim.x) cb[l] = coff[(size_t)k * NL + l] - loff[l];
-  for (uint32_t p = s + threadIdx.x; p < e; p += blockDim.x) {
-    const unsigned long long v = tmp[p];
-    const uint32_t l = (uint32_t)(v >> 32) & (NL - 1);
+  // all of the thread's entries are loaded before the first LDS atomic, so the
+  // global loads overlap instead of one round trip per entry
+  constexpr int PER = SORT_CHUNK / SORT_BLOCK;
+  uint32_t ev[PER], lv[PER];
+#pragma unroll
+  for (int j = 0; j < PER; j++) {
+    const uint32_t p = s + threadIdx.x + j * SORT_BLOCK;
+    lv[j] = p < e ? (uint32_t)tmp_l[p] : 0xffffffffu;
+    ev[j] = p < e ? tmp_e[p] : 0u;
+  }
+#pragma unroll
+  for (int j = 0; j < PER; j++) {
+    if (lv[j] == 0xffffffffu) continue;
+    const uint32_t l = lv[j];
     const uint32_t slot = loff[l] + atomicAdd(&cur[l], 1u);
-    e32[slot] = (uint32_t)v;
+    e32[slot] = ev[j];
     bins[slot] = (uint16_t)l;
   }
   __syncthreads();
@@ -449,16 +553,20 @@ __global__ void k_scan_add(const uint2* __restrict__ tile_off, size_t nb, uint32
 // partial of (thread t, bucket b) lives in slot t + b: unique, and the slots
 // of bucket b are the contiguous range [t_first(b) + b, t_last(b) + b] with
 // t_first(b) = bstart[b] / L, t_last(b) = (bstart[b + 1] - 1) / L.
-QG_DEV void msm_flush(G1Xyzz* partial, uint32_t* owner, uint32_t slot, uint32_t b, const X29& acc,
+QG_DEV void msm_flush(X29Raw* partial, uint32_t* owner, uint32_t slot, uint32_t b, const X29& acc,
                       bool inf) {
-  partial[slot] = x29_store(inf ? x29_inf() : x29_acc_finish(acc));
+  partial[slot] = x29_raw(inf ? x29_inf() : acc);  // finished by the reader
   owner[slot] = b;
+}
+
+QG_DEV X29 msm_partial(const X29Raw* partial, uint32_t slot) {
+  return x29_acc_finish(x29_unraw(partial[slot]));
 }
 
 __global__ void __launch_bounds__(MSM_BLOCK)
     k_msm_accumulate(const MsmPt* __restrict__ table, const uint32_t* __restrict__ entries,
                      const uint32_t* __restrict__ bstart, uint32_t nb, uint32_t L,
-                     G1Xyzz* __restrict__ partial, uint32_t* __restrict__ owner) {
+                     X29Raw* __restrict__ partial, uint32_t* __restrict__ owner) {
   const uint32_t t = blockIdx.x * blockDim.x + threadIdx.x;
   const uint32_t total = bstart[nb];
   const uint64_t e0w = (uint64_t)t * L;
@@ -516,7 +624,8 @@ QG_DEV uint32_t msm_slot_last(const uint32_t* bstart, uint32_t b, uint32_t L) {
 // Segmented pairwise tree over the partial slots: after the steps s = 1, 2,
 // 4, ... slot_first(b) holds bucket b's sum.  Slots no thread wrote carry
 // owner == ~0 and are skipped.
-__global__ void k_msm_tree_step(G1Xyzz* __restrict__ partial, const uint32_t* __restrict__ owner,
+__global__ void __launch_bounds__(MSM_BLOCK)
+    k_msm_tree_step(X29Raw* __restrict__ partial, const uint32_t* __restrict__ owner,
                                 const uint32_t* __restrict__ bstart, uint32_t L, uint32_t nslots,
                                 uint32_t s) {
   const uint32_t i = blockIdx.x * blockDim.x + threadIdx.x;
@@ -526,24 +635,14 @@ __global__ void k_msm_tree_step(G1Xyzz* __restrict__ partial, const uint32_t* __
   const uint32_t f = msm_slot_first(bstart, b, L), l = msm_slot_last(bstart, b, L);
   const uint32_t off = i - f;
   if ((off & (2 * s - 1)) == 0 && i + s <= l)
-    partial[i] = x29_store(x29_add(x29_load(partial[i]), x29_load(partial[i + s])));
+    partial[i] = x29_raw(x29_add(msm_partial(partial, i), msm_partial(partial, i + s)));
 }
 
 // ---- reduction ------------------------------------------------------------
-__device__ void block_reduce_x29(X29 v, G1Xyzz* sh, G1Xyzz* out) {
-  sh[threadIdx.x] = x29_store(v);
-  __syncthreads();
-  for (unsigned s = blockDim.x / 2; s > 0; s >>= 1) {
-    if (threadIdx.x < s)
-      sh[threadIdx.x] = x29_store(x29_add(x29_load(sh[threadIdx.x]), x29_load(sh[threadIdx.x + s])));
-    __syncthreads();
-  }
-  if (threadIdx.x == 0) *out = sh[0];
-}
-
 // B_j = sum of bucket j's partial slots at offsets 0, step, 2 step, ... (empty
 // bucket -> infinity); at most MSM_COMBINE_SEQ of them
-__global__ void k_msm_combine(const G1Xyzz* __restrict__ partial, const uint32_t* __restrict__ bstart,
+__global__ void __launch_bounds__(MSM_BLOCK)
+    k_msm_combine(const X29Raw* __restrict__ partial, const uint32_t* __restrict__ bstart,
                               uint32_t nb, uint32_t L, uint32_t step, G1Xyzz* __restrict__ buckets) {
   const uint32_t j = blockIdx.x * blockDim.x + threadIdx.x;
   if (j >= nb) return;
@@ -553,41 +652,75 @@ __global__ void k_msm_combine(const G1Xyzz* __restrict__ partial, const uint32_t
   }
   const uint32_t f = msm_slot_first(bstart, j, L), l = msm_slot_last(bstart, j, L);
   if (l - f < step) {
-    buckets[j] = partial[f];
+    buckets[j] = x29_store(msm_partial(partial, f));
     return;
   }
-  X29 acc = x29_load(partial[f]);
-  for (uint32_t t = f + step; t <= l; t += step) acc = x29_add(acc, x29_load(partial[t]));
+  X29 acc = msm_partial(partial, f);
+  for (uint32_t t = f + step; t <= l; t += step) acc = x29_add(acc, msm_partial(partial, t));
   buckets[j] = x29_store(acc);
 }
 
-// Segment s of MSM_SEG buckets: V_s = sum_i (lo+i+1) B_{lo+i}
-//   = [sum_i (i+1) B_{lo+i}]  (running sums from the top)  +  lo * [sum_i B_{lo+i}]
-// then a block tree reduction.
-__global__ void __launch_bounds__(MSM_BLOCK)
-    k_msm_reduce(const G1Xyzz* __restrict__ buckets, uint32_t nb, G1Xyzz* __restrict__ block_out) {
-  __shared__ G1Xyzz sh[MSM_BLOCK];
-  const uint32_t seg = blockIdx.x * blockDim.x + threadIdx.x;
-  const uint32_t lo = seg * MSM_SEG;
-  X29 v = x29_inf();
-  if (lo < nb) {
-    const uint32_t hi = lo + MSM_SEG < nb ? lo + MSM_SEG : nb;
-    X29 run = x29_load(buckets[hi - 1]), acc = run;
-    for (uint32_t j = hi - 1; j-- > lo;) {
-      run = x29_add(run, x29_load(buckets[j]));
-      acc = x29_add(acc, run);
-    }
-    v = x29_add(acc, x29_mul_small(run, lo));
-  }
-  block_reduce_x29(v, sh, &block_out[blockIdx.x]);
+// k doublings (k < 32)
+QG_DEV X29 x29_dbl_k(X29 p, int k) {
+  for (int i = 0; i < k; i++) p = x29_dbl(p);
+  return p;
 }
 
+// One level of the bucket reduction  sum_i Q_i + i P_i  over i in [0, m)
+// (Q = P when Q is null).  Thread t of block b folds its S = 2^slog consecutive
+// elements from the top (run = sum P, wsum = sum (i - lo) P: one running-sum
+// chain, no scalar multiplications); the block then needs
+//   A_b = sum_t [acc_t + t S run_t],  sum_t t run_t = sum_{k>=1} Suf_k
+// with Suf_k = sum_{t>=k} run_t: an LDS suffix scan and a tree sum.  Output
+//   A_b = sum_{i in block b} Q_i + (i - base_b) P_i,   R_b = 2^rlog sum_{i in b} P_i
+// with rlog = log2(T S), so sum_i Q_i + i P_i = sum_b A_b + b R_b: the same form
+// one level up (P' = R, Q' = A).  A single block's A_0 is the total.
+// Level 1 runs on the buckets with P = Q = B: sum_j (j + 1) B_j.
 __global__ void __launch_bounds__(MSM_BLOCK)
-    k_msm_final(const G1Xyzz* __restrict__ in, uint32_t m, G1Xyzz* __restrict__ out) {
-  __shared__ G1Xyzz sh[MSM_BLOCK];
-  X29 v = x29_inf();
-  for (uint32_t i = threadIdx.x; i < m; i += blockDim.x) v = x29_add(v, x29_load(in[i]));
-  block_reduce_x29(v, sh, out);
+    k_msm_wsum(const G1Xyzz* __restrict__ P, const G1Xyzz* __restrict__ Q, uint32_t m, int slog,
+               int rlog, G1Xyzz* __restrict__ A_out, G1Xyzz* __restrict__ R_out) {
+  __shared__ G1Xyzz sh_r[MSM_BLOCK], sh_a[MSM_BLOCK];
+  const uint32_t t = threadIdx.x, T = blockDim.x;
+  const uint64_t lo = ((uint64_t)blockIdx.x * T + t) << slog;
+  X29 run = x29_inf(), acc = x29_inf();
+  if (lo < m) {
+    const uint32_t l = (uint32_t)lo;
+    const uint32_t hi = m - l < (1u << slog) ? m : l + (1u << slog);
+    X29 wsum = x29_inf(), qsum = x29_inf();
+    for (uint32_t i = hi - 1; i > l; i--) {
+      run = x29_add(run, x29_load(P[i]));
+      wsum = x29_add(wsum, run);
+      if (Q) qsum = x29_add(qsum, x29_load(Q[i]));
+    }
+    run = x29_add(run, x29_load(P[l]));
+    if (Q) qsum = x29_add(qsum, x29_load(Q[l]));
+    acc = x29_add(wsum, Q ? qsum : run);
+  }
+  // inclusive suffix scan of run over the block (Hillis-Steele, double sync)
+  sh_r[t] = x29_store(run);
+  __syncthreads();
+  for (uint32_t off = 1; off < T; off <<= 1) {
+    X29 v = run;
+    if (t + off < T) v = x29_add(run, x29_load(sh_r[t + off]));
+    __syncthreads();
+    sh_r[t] = x29_store(v);
+    run = v;
+    __syncthreads();
+  }
+  const X29 total_run = x29_load(sh_r[0]);
+  // one tree sum of y_t = acc_t + S Suf_t (t >= 1), acc_0
+  const X29 y = t ? x29_add(acc, x29_dbl_k(run, slog)) : acc;
+  __syncthreads();
+  sh_a[t] = x29_store(y);
+  __syncthreads();
+  for (uint32_t s = T / 2; s > 0; s >>= 1) {
+    if (t < s) sh_a[t] = x29_store(x29_add(x29_load(sh_a[t]), x29_load(sh_a[t + s])));
+    __syncthreads();
+  }
+  if (t == 0) {
+    A_out[blockIdx.x] = sh_a[0];
+    if (R_out) R_out[blockIdx.x] = x29_store(x29_dbl_k(total_run, rlog));
+  }
 }
 
 // R = 2^261 XYZZ words -> R = 2^256 Montgomery XYZZ (canonical) for the host
@@ -745,7 +878,10 @@ G1Affine msm_device(qg_ctx* ctx, const qg_srs* srs, const Fr* d_scalars, size_t 
     const int H = 1 << HI, NL = 1 << LO;
     // pass-A tile: as many scalars as fit their W digits (8 B each) in LDS
     uint32_t tile = SORT_TILE_MAX;
-    while (tile > 64 && (size_t)tile * W * 10 > SORT_LDS_A) tile >>= 1;
+    while (tile > 64 && (size_t)tile * W * 8 > SORT_LDS_A) tile >>= 1;
+    if (const char* ov = getenv("QG_SORT_TILE")) tile = (uint32_t)atoi(ov);  // tuning experiments
+    QG_CHECK(tile >= 64 && tile <= SORT_TILE_MAX && (tile & (tile - 1)) == 0, QG_ERR_INVALID,
+             "QG_SORT_TILE must be a power of two in [64, 1024]");
     const uint32_t nblk = div_up(n, tile);
     const size_t nghist = (size_t)H * nblk;
     const size_t max_chunks = max_entries / SORT_CHUNK + H + 1;
@@ -758,7 +894,11 @@ G1Affine msm_device(qg_ctx* ctx, const qg_srs* srs, const Fr* d_scalars, size_t 
     uint32_t* misc = ctx->scratch_as<uint32_t>("msm_misc", 4);  // [0] nchunks, [1] max tpb
     uint32_t* chist = ctx->scratch_as<uint32_t>("msm_chist", max_chunks * NL);
     uint32_t* coff = ctx->scratch_as<uint32_t>("msm_coff", max_chunks * NL);
-    unsigned long long* tmp = ctx->scratch_as<unsigned long long>("msm_tmp", max_entries + 1);
+    uint32_t* tmp_e = ctx->scratch_as<uint32_t>("msm_tmp_e", max_entries + 1);
+    uint16_t* tmp_l = ctx->scratch_as<uint16_t>("msm_tmp_l", max_entries + 1);
+    uint32_t* hrow = ctx->scratch_as<uint32_t>("msm_hrow", nghist + 1);
+    uint32_t* orow = ctx->scratch_as<uint32_t>("msm_orow", nghist + 1);
+    Fr* canon = ctx->scratch_as<Fr>("msm_canon", n);
     uint32_t* counts = ctx->scratch_as<uint32_t>("msm_counts", nb);
     uint32_t* bstart = ctx->scratch_as<uint32_t>("msm_bstart", nb + 1);
     uint32_t* tstart = ctx->scratch_as<uint32_t>("msm_tstart", nb + 1);
@@ -770,16 +910,22 @@ G1Affine msm_device(qg_ctx* ctx, const qg_srs* srs, const Fr* d_scalars, size_t 
     // the headline sizes, fewer while that would leave < 8 waves of threads per
     // resident slot (256 CUs x 12 waves)
     int elog = 6;
-    while (elog > 2 && (max_entries >> elog) < (size_t)ctx->num_cus() * 12 * 64 * 8) elog--;
+    while (elog > 2 && (max_entries >> elog) < (size_t)ctx->num_cus() * 16 * 64 * 3) elog--;
+    if (const char* ov = getenv("QG_MSM_ELOG")) elog = atoi(ov);  // tuning experiments
+    QG_CHECK(elog >= 0 && elog <= 12, QG_ERR_INVALID, "QG_MSM_ELOG out of range");
     const uint32_t L = 1u << elog;
     const size_t max_threads = div_up(max_entries, L);
     const size_t nslots = max_threads + nb + 1;  // partial slot of (thread t, bucket b): t + b
-    G1Xyzz* partial = ctx->scratch_as<G1Xyzz>("msm_partial", nslots);
+    X29Raw* partial = ctx->scratch_as<X29Raw>("msm_partial", nslots);
     uint32_t* owner = ctx->scratch_as<uint32_t>("msm_owner", nslots);
     G1Xyzz* buckets = ctx->scratch_as<G1Xyzz>("msm_buckets", nb);
-    const uint32_t nseg = div_up(nb, MSM_SEG);
-    const uint32_t nred = div_up(nseg, MSM_BLOCK);
-    G1Xyzz* red = ctx->scratch_as<G1Xyzz>("msm_red", nred + 2);
+    // bucket reduction: level 1 over the buckets (8 per thread), level 2 in one block
+    const int slog1 = nb >= 8u * MSM_BLOCK ? 3 : 0;
+    const uint32_t nred = div_up(nb, (size_t)MSM_BLOCK << slog1);
+    int slog2 = 0;
+    while (((size_t)MSM_BLOCK << slog2) < nred) slog2++;
+    QG_CHECK(slog2 <= 12, QG_ERR_UNSUPPORTED, "bucket count too large");
+    G1Xyzz* red = ctx->scratch_as<G1Xyzz>("msm_red", 2 * nred + 3);
     QG_CHECK(ntiles <= 1024 * 64 && H <= 1024 && NL <= 4096, QG_ERR_UNSUPPORTED,
              "bucket count too large");
     QG_CHECK(nslots < 0xffffffffull && max_chunks < 0xffffffffull, QG_ERR_UNSUPPORTED,
@@ -789,7 +935,10 @@ G1Affine msm_device(qg_ctx* ctx, const qg_srs* srs, const Fr* d_scalars, size_t 
       QgTimed tm(ctx, "msm_bucketing");
       // pass A: partition digits by the high bucket bits
       hipLaunchKernelGGL(k_sortA_hist, dim3(nblk), dim3(SORT_BLOCK), H * sizeof(uint32_t),
-                         ctx->stream, d_scalars, n, c, W, LO, H, nblk, tile, ghist);
+                         ctx->stream, d_scalars, n, c, W, LO, H, nblk, tile, hrow, canon);
+      QG_LAUNCH_CHECK();
+      hipLaunchKernelGGL(k_transpose32, dim3(div_up(H, 32), div_up(nblk, 32)), dim3(256), 0,
+                         ctx->stream, hrow, nblk, (uint32_t)H, ghist);
       QG_LAUNCH_CHECK();
       const unsigned gt = div_up(nghist, 2048);
       QG_CHECK(gt <= 1024u * 1024u, QG_ERR_UNSUPPORTED, "histogram too large");
@@ -802,8 +951,12 @@ G1Affine msm_device(qg_ctx* ctx, const qg_srs* srs, const Fr* d_scalars, size_t 
       hipLaunchKernelGGL(k_scan32_add, dim3(div_up(nghist, 256)), dim3(256), 0, ctx->stream, gtiles,
                          nghist, goff);
       QG_LAUNCH_CHECK();
-      const size_t smemA = (size_t)tile * W * 8 + (((size_t)tile * W + 1) & ~(size_t)1) * 2 +
-                           (3 * (size_t)H + SORT_BLOCK) * 4;
+      hipLaunchKernelGGL(k_transpose32, dim3(div_up(nblk, 32), div_up(H, 32)), dim3(256), 0,
+                         ctx->stream, goff, (uint32_t)H, nblk, orow);
+      QG_LAUNCH_CHECK();
+      hipLaunchKernelGGL(k_sortA_rows, dim3(nblk), dim3(SORT_BLOCK), 0, ctx->stream, hrow, orow, H);
+      QG_LAUNCH_CHECK();
+      const size_t smemA = (size_t)tile * W * 8 + (3 * (size_t)H + SORT_BLOCK) * 4;
       QG_CHECK(smemA <= 160 * 1024, QG_ERR_UNSUPPORTED, "pass-A tile exceeds LDS");
       // the >64 KiB dynamic-LDS attribute, once per context (= per device and
       // per calling thread: a context is used by one thread at a time)
@@ -815,7 +968,7 @@ G1Affine msm_device(qg_ctx* ctx, const qg_srs* srs, const Fr* d_scalars, size_t 
         ctx->memo["msm_lds_attr"] = "1";
       }
       hipLaunchKernelGGL(k_sortA_scatter, dim3(nblk), dim3(SORT_BLOCK), smemA, ctx->stream,
-                         d_scalars, n, srs->n, c, W, LO, H, nblk, tile, ghist, goff, tmp);
+                         canon, n, srs->n, c, W, LO, H, nblk, tile, hrow, orow, tmp_e, tmp_l);
       QG_LAUNCH_CHECK();
       // pass B: sort every group by the low bits, in chunks
       QG_HIP(hipMemsetAsync(misc, 0, 4 * sizeof(uint32_t), ctx->stream));
@@ -823,7 +976,7 @@ G1Affine msm_device(qg_ctx* ctx, const qg_srs* srs, const Fr* d_scalars, size_t 
                          gstart, cbase, cgroup, misc);
       QG_LAUNCH_CHECK();
       hipLaunchKernelGGL(k_sortB_hist, dim3((unsigned)max_chunks), dim3(SORT_BLOCK),
-                         NL * sizeof(uint32_t), ctx->stream, tmp, gstart, cbase, cgroup, misc, NL,
+                         NL * sizeof(uint32_t), ctx->stream, tmp_l, gstart, cbase, cgroup, misc, NL,
                          chist);
       QG_LAUNCH_CHECK();
       hipLaunchKernelGGL(k_sort_bucket_count, dim3(div_up(nb, 256)), dim3(256), 0, ctx->stream,
@@ -843,7 +996,8 @@ G1Affine msm_device(qg_ctx* ctx, const qg_srs* srs, const Fr* d_scalars, size_t 
       QG_LAUNCH_CHECK();
       const size_t smemB = (size_t)SORT_CHUNK * 6 + (3 * (size_t)NL + SORT_BLOCK) * 4;
       hipLaunchKernelGGL(k_sortB_scatter, dim3((unsigned)max_chunks), dim3(SORT_BLOCK), smemB,
-                         ctx->stream, tmp, gstart, cbase, cgroup, misc, NL, chist, coff, entries);
+                         ctx->stream, tmp_e, tmp_l, gstart, cbase, cgroup, misc, NL, chist, coff,
+                         entries);
       QG_LAUNCH_CHECK();
     }
     QG_HIP(hipMemsetAsync(owner, 0xff, nslots * sizeof(uint32_t), ctx->stream));
@@ -873,16 +1027,19 @@ G1Affine msm_device(qg_ctx* ctx, const qg_srs* srs, const Fr* d_scalars, size_t 
       hipLaunchKernelGGL(k_msm_combine, dim3(div_up(nb, MSM_BLOCK)), dim3(MSM_BLOCK), 0,
                          ctx->stream, partial, bstart, nb, L, st, buckets);
       QG_LAUNCH_CHECK();
-      hipLaunchKernelGGL(k_msm_reduce, dim3(nred), dim3(MSM_BLOCK), 0, ctx->stream, buckets, nb,
-                         red);
+      // level 1: A = red[0, nred), R = red[nred, 2 nred); level 2: red[2 nred]
+      hipLaunchKernelGGL(k_msm_wsum, dim3(nred), dim3(MSM_BLOCK), 0, ctx->stream, buckets,
+                         (const G1Xyzz*)nullptr, nb, slog1, 8 + slog1, red, red + nred);
       QG_LAUNCH_CHECK();
-      hipLaunchKernelGGL(k_msm_final, dim3(1), dim3(MSM_BLOCK), 0, ctx->stream, red, nred,
-                         red + nred);
+      const uint32_t t2 = div_up(nred, (size_t)1 << slog2);
+      hipLaunchKernelGGL(k_msm_wsum, dim3(1), dim3(t2 < 64 ? 64 : t2), 0, ctx->stream,
+                         red + nred, red, nred, slog2, 0, red + 2 * nred, (G1Xyzz*)nullptr);
       QG_LAUNCH_CHECK();
     }
-    hipLaunchKernelGGL(k_msm_export, dim3(1), dim3(1), 0, ctx->stream, red + nred, red + nred + 1);
+    hipLaunchKernelGGL(k_msm_export, dim3(1), dim3(1), 0, ctx->stream, red + 2 * nred,
+                       red + 2 * nred + 1);
     QG_LAUNCH_CHECK();
-    QG_HIP(hipMemcpyAsync(&local, red + nred + 1, sizeof(G1Xyzz), hipMemcpyDeviceToHost,
+    QG_HIP(hipMemcpyAsync(&local, red + 2 * nred + 1, sizeof(G1Xyzz), hipMemcpyDeviceToHost,
                           ctx->stream));
     ctx->sync();
   }
