@@ -186,6 +186,7 @@ int qg_ctx_destroy(qg_ctx* ctx) {
   if (ctx->stream) (void)hipStreamSynchronize(ctx->stream);
   comm_release(ctx);
   for (auto& kv : ctx->scratch) (void)hipFree(kv.second.first);
+  for (auto& kv : ctx->pinned) (void)hipHostFree(kv.second.first);
   for (auto& kv : ctx->pending) {
     (void)hipEventDestroy(kv.second.a);
     (void)hipEventDestroy(kv.second.b);

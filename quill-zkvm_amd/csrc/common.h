@@ -87,6 +87,21 @@ struct qg_ctx {
   T* scratch_as(const std::string& slot, size_t count) {
     return reinterpret_cast<T*>(scratch_get(slot, count * sizeof(T)));
   }
+  // grow-only pinned host staging (small per-call transfers: no pageable bounce)
+  std::map<std::string, std::pair<void*, size_t>> pinned;
+  void* pinned_get(const std::string& slot, size_t bytes) {
+    auto it = pinned.find(slot);
+    if (it != pinned.end() && it->second.second >= bytes) return it->second.first;
+    if (it != pinned.end()) {
+      QG_HIP(hipHostFree(it->second.first));
+      pinned.erase(it);
+    }
+    void* p = nullptr;
+    size_t b = bytes ? bytes : 16;
+    QG_HIP(hipHostMalloc(&p, b, hipHostMallocDefault));
+    pinned[slot] = {p, b};
+    return p;
+  }
 
   hipEvent_t ev_get() {
     if (!event_pool.empty()) {

@@ -73,7 +73,13 @@ static unsigned sc_round_blocks(qg_ctx* ctx, size_t npairs) {
   cap = std::min<size_t>(cap, SC_MAX_BLOCKS);
   return (unsigned)std::max<size_t>(1, std::min<size_t>(cap, div_up(npairs, SC_BLOCK)));
 }
-static constexpr int TAIL_BLOCK = 512;  // persistent-kernel block
+// QG_SC_STAGED=1 selects the LDS-staged round kernels + persistent tail (k_sc_round,
+// k_sc_persist) on one GPU, for A/B runs
+static bool sc_use_staged() {
+  static const bool v = getenv("QG_SC_STAGED") != nullptr;
+  return v;
+}
+static constexpr int TAIL_BLOCK = 256;  // persistent-kernel block (one wave per SIMD: latency-bound rounds)
 static constexpr int PERS_LOG = 16;     // tables of <= 2^16 entries: rounds run in one persistent launch
 
 // device-side program image.  The header and byte arrays are copied into LDS
@@ -106,8 +112,11 @@ static_assert(offsetof(SopDev, c29) == SOP_HDR_WORDS * 4, "SopDev layout");
 
 // program header passed by value (no dependent loads before the LDS copy)
 struct SopHdr {
-  uint32_t nmono, nslots, np, pad;
+  uint32_t nmono, nslots, np, pad;  // pad: SOP_* flags
 };
+// the expression is the product of every used slot once, in slot order, with
+// coefficient 1 (h = g1 g2 ... gk): evaluated without slot picks
+static constexpr uint32_t SOP_PURE = 1;
 
 using R29 = F29<FrP>;
 
@@ -298,22 +307,83 @@ QG_DEV void round_sweep(RoundLds<K, NP, BLOCK>& L, const SopLds<NP>& sp, const S
   }
 }
 
-// Sum of acc over the threads of each point t (t = tid % NP) -> res[t] (LDS,
-// canonical 32-bit words at scale S), visible to all threads on return.
-// red: (BLOCK / 64) * NP LDS scratch.
+// lazy value < 128p (limbs < 2^32) -> normalized, < 2p
+QG_DEV R29 red128p(const R29& a) {
+  R29 x = normfull29<FrP>(a);
+  x = condsub29<FrP>(x, l9_mul_small(F29P<FrP>::P, 64));
+  x = condsub29<FrP>(x, l9_mul_small(F29P<FrP>::P, 32));
+  x = condsub29<FrP>(x, F29P<FrP>::KP20.k[16]);
+  x = condsub29<FrP>(x, F29P<FrP>::P8);
+  x = condsub29<FrP>(x, F29P<FrP>::P4);
+  return condsub29<FrP>(x, F29P<FrP>::P2);
+}
+
+// Block sums of NP per-thread values acc[t] (each < 2p, normalized) -> res[t]
+// (LDS, canonical words), visible to all threads on return.  All points move
+// together (independent chains); additions are lazy, one parallel carry pass
+// per shuffle step, one reduction per point at the wave and block levels.
+// red: (blockDim / 64) * NP LDS scratch.
 template <int NP>
-QG_DEV void block_reduce_pts(R29 acc, uint32_t np, R29* red, Fr* res) {
+QG_DEV void block_sums29(R29 (&acc)[NP], uint32_t np, R29* red, R29* res) {
+  const uint32_t lane = threadIdx.x & 63, wid = threadIdx.x >> 6, nw = blockDim.x >> 6;
+  // one point at a time (register pressure of the sweep kernel stays low)
 #pragma unroll
-  for (int m = 32; m >= NP; m >>= 1) acc = red6p(add29(acc, shfl_xor29(acc, m)));
+  for (int t = 0; t < NP; t++) {
+    R29 a = acc[t];
+#pragma unroll
+    for (int m = 32; m >= 1; m >>= 1) a = norm29(add29(a, shfl_xor29(a, m)));  // < 128p
+    if (lane == 0 && (uint32_t)t < np) red[wid * NP + t] = red128p(a);
+  }
+  __syncthreads();
+  if (threadIdx.x < np) {
+    R29 a = red[threadIdx.x];
+    for (uint32_t w = 1; w < nw; w++) a = add29(a, red[w * NP + threadIdx.x]);  // nw <= 8: < 16p
+    res[threadIdx.x] = red16p29<FrP>(a);
+  }
+  __syncthreads();
+}
+
+// Sum of acc (< 2p, normalized) over the threads of each point t (t = tid %
+// NP) -> res[t] (LDS, < 2p normalized), visible to all threads on return.
+// Lazy: the shuffle steps and the cross-wave sum only add (with parallel
+// carry passes); one reduction per point at the end.  red: (blockDim / 64) *
+// NP LDS scratch.
+template <int NP>
+QG_DEV void block_reduce_pts(R29 acc, uint32_t np, R29* red, R29* res) {
+#pragma unroll
+  for (int m = 32; m >= NP; m >>= 1) acc = norm29(add29(acc, shfl_xor29(acc, m)));  // < 128p / NP
   const uint32_t lane = threadIdx.x & 63, wid = threadIdx.x >> 6, nw = blockDim.x >> 6;
   if (lane < NP) red[wid * NP + lane] = acc;
   __syncthreads();
   if (threadIdx.x < np) {
+    // NP >= 4: a wave's value is < 32p; up to 4 of them (< 128p) between reductions
     R29 a = red[threadIdx.x];
-    for (uint32_t w = 1; w < nw; w++) a = red6p(add29(a, red[w * NP + threadIdx.x]));
-    res[threadIdx.x] = from29(canon29(a));
+    for (uint32_t w = 1; w < nw; w++) {
+      if ((w & 3) == 0) a = red128p(a);
+      a = norm29(add29(a, red[w * NP + threadIdx.x]));
+    }
+    res[threadIdx.x] = red128p(a);
   }
   __syncthreads();
+}
+
+// Sum of nrows rows of NP canonical values (row b at rows[b * NP]) -> res[t]
+// (whole block; thread = (row group, point), lazy sums)
+template <int NP>
+QG_DEV void sum_rows29(const Fr* rows, uint32_t nrows, uint32_t np, R29* red, R29* res) {
+  const uint32_t t = threadIdx.x % NP;
+  R29 a = R29::zero();
+  uint32_t c = 0;
+  if (t < np)
+    for (uint32_t b = threadIdx.x / NP; b < nrows; b += blockDim.x / NP) {
+      a = add29(a, to29(rows[(size_t)b * NP + t]));  // canonical: < p
+      if (++c == 6) {  // limbs: 7 normalized terms stay below 2^32
+        a = red16p29<FrP>(a);
+        c = 0;
+      }
+    }
+  a = red16p29<FrP>(a);
+  block_reduce_pts<NP>(a, np, red, res);
 }
 
 // Round bookkeeping.  The transcript state, the deferred absorb, the current
@@ -354,30 +424,26 @@ struct FinSmem {
 // lanes (r * 2^261 for the fold and r * 2^256 for the output, each lo + hi).
 // Absorbing the 48 challenge bytes is deferred when pend_out != nullptr.
 template <int NP>
-QG_DEV void finish_core(const SopLds<NP>& sp, uint32_t np, const Fr* ev, const RoundOut& ro,
+QG_DEV void finish_core(const SopLds<NP>& sp, uint32_t np, const R29* ev, const RoundOut& ro,
                         uint32_t j, FinSmem& fs, const uint32_t* state_in, uint32_t* pend_out,
                         uint32_t* state_out, uint32_t tr = 4096, bool writer = true) {
   constexpr uint32_t U = NP <= 8 ? NP : 4;  // lanes per coefficient
   const uint32_t tid = threadIdx.x;
   const bool w0 = tid < 64;
   const uint32_t ct = tid / U, cu = tid % U;
-  R29 cm = R29::zero(), cc = R29::zero();
+  // canonical coefficients (transcript bytes) first; the Montgomery ones (proof
+  // output) after the challenge.  Lazy sums: <= 4 terms < 2p per lane, U <= 8
+  // lanes: < 64p before the one reduction.
+  R29 cc = R29::zero();
   if (w0 && ct < np) {
-    for (uint32_t u = cu; u < np; u += U) {
-      const R29 e = to29(ev[u]);
-      cm = red6p(add29(cm, mul29(sp.vm[ct * NP + u], e)));
-      cc = red6p(add29(cc, mul29(sp.vc[ct * NP + u], e)));
-    }
+    for (uint32_t u = cu; u < np; u += U) cc = add29(cc, mul29(sp.vc[ct * NP + u], ev[u]));
   }
+  cc = norm29(cc);
 #pragma unroll
-  for (uint32_t m = 1; m < U; m <<= 1) {
-    cm = red6p(add29(cm, shfl_xor29(cm, m)));
-    cc = red6p(add29(cc, shfl_xor29(cc, m)));
-  }
-  const Fr cmw = from29(canon29(cm)), ccw = from29(canon29(cc));
+  for (uint32_t m = 1; m < U; m <<= 1) cc = norm29(add29(cc, shfl_xor29(cc, m)));
+  const Fr ccw = from29(canon29(red128p(cc)));
   const bool lead = w0 && cu == 0 && ct < np;
   if (writer) {
-    if (lead) ro.coeffs[(size_t)j * ro.width + ct] = cmw;
     for (uint32_t i = np + tid; i < ro.width; i += blockDim.x)
       ro.coeffs[(size_t)j * ro.width + i] = Fr::zero();
   }
@@ -434,6 +500,17 @@ QG_DEV void finish_core(const SopLds<NP>& sp, uint32_t np, const Fr* ev, const R
   __syncthreads();
   SC_TR(tr + 6);
   if (!pend_out && w0) b3_hash_quad(fs.ab, 80, state_out, 8);
+  if (writer) {
+    // Montgomery coefficients for the proof output (off the challenge path)
+    R29 cm = R29::zero();
+    if (w0 && ct < np) {
+      for (uint32_t u = cu; u < np; u += U) cm = add29(cm, mul29(sp.vm[ct * NP + u], ev[u]));
+    }
+    cm = norm29(cm);
+#pragma unroll
+    for (uint32_t m = 1; m < U; m <<= 1) cm = norm29(add29(cm, shfl_xor29(cm, m)));
+    if (lead) ro.coeffs[(size_t)j * ro.width + ct] = from29(canon29(red128p(cm)));
+  }
 }
 
 // round kernel: fused fold(r_{j-1}) + evaluate at t = 0..np-1, per-block
@@ -447,7 +524,7 @@ __global__ void __launch_bounds__(SC_BLOCK)
   __shared__ SopLds<NP> sp;
   __shared__ RoundLds<K, NP, SC_BLOCK> L;
   __shared__ R29 red[(SC_BLOCK / 64) * NP];
-  __shared__ Fr res[NP];
+  __shared__ R29 res[NP];
   __shared__ FinSmem fs;
   __shared__ uint32_t last;
   const uint32_t tid = threadIdx.x;
@@ -481,7 +558,7 @@ __global__ void __launch_bounds__(SC_BLOCK)
                                (size_t)gridDim.x * PB, acc);
   if (blockIdx.x == 0) SC_TR(tr + 1);
   block_reduce_pts<NP>(acc, h.np, red, res);
-  if (tid < h.np) partial[(size_t)blockIdx.x * NP + tid] = res[tid];
+  if (tid < h.np) partial[(size_t)blockIdx.x * NP + tid] = from29(canon29(res[tid]));
   __syncthreads();
   if (tid == 0) {
     __builtin_amdgcn_fence(__ATOMIC_RELEASE, "agent");
@@ -503,10 +580,250 @@ __global__ void __launch_bounds__(SC_BLOCK)
   block_reduce_pts<NP>(acc, h.np, red, res);
   if (tid == 0) ro.st->ticket = 0;
   if (loc) {
-    if (tid < NP) loc[tid] = tid < h.np ? res[tid] : Fr::zero();
+    if (tid < NP) loc[tid] = tid < h.np ? from29(canon29(res[tid])) : Fr::zero();
     return;
   }
   finish_core<NP>(sp, h.np, res, ro, j, fs, ro.st->state, ro.st->pend, nullptr, tr);
+  if (tid < 9) ro.st->r29[tid] = fs.r.l[tid];
+  SC_TR(tr + 7);
+}
+
+// ---------------------------------------------------------------------------
+// Throughput form of a large round for product expressions (SOP_PURE, e.g.
+// the h = g1 g2 g3 of config 3): one thread per pair (grid-stride), no LDS
+// staging and no per-step barriers.  Slot by slot the thread folds its 4
+// entries by r_{j-1} (2 throughput multiplies; the folded pair is written back
+// < 2p) and multiplies lo + t (hi - lo) into the running product of every
+// point t = 0..np-1; the points accumulate lazily.  Other expressions use the
+// LDS-staged k_sc_round.
+// ---------------------------------------------------------------------------
+
+// ---------------------------------------------------------------------------
+// Large rounds, thread per pair (k_sc_big).
+//  * Sweep: one thread per pair, grid-stride.  Slot by slot the thread folds
+//    its 4 entries by r_{j-1} (throughput multiplies; the folded pair is
+//    written back < 2p) and evaluates at t = 0..np-1: product expressions
+//    (SOP_PURE) multiply lo + t (hi - lo) into a running product per point,
+//    the next slot's entries in flight during the current slot's arithmetic;
+//    other expressions (K <= 4) keep every slot's lo / hi and run the
+//    compiled monomials with uniform-index selects.  The points accumulate
+//    lazily (three additions per reduction).
+//  * Round end: per-block partial rows; the last block to publish (ticket)
+//    sums them and runs the transcript step.
+// ---------------------------------------------------------------------------
+// lo + t (hi - lo + 4p) for point t (d = norm29(hi - lo + 4p) < 6p)
+template <int NP>
+QG_DEV R29 at_point(const R29& lo, const R29& d, int t, const SopLds<NP>& sp) {
+  if constexpr (NP <= 4) {
+    R29 v = lo;  // lazy, < 20p, then one carry pass
+    if (t & 1) v = add29(v, d);
+    if (t & 2) v = add29(v, add29(d, d));
+    return norm29(v);
+  } else {
+    return norm29(add29(lo, mul29t(d, sp.t29[t])));  // < 4p
+  }
+}
+
+// fold x0..x3 -> (lo, hi) < 2p and store them (round j >= 1), or take x0, x1
+QG_DEV void fold_pair(const Fr (&w)[4], bool fold, const R29& r, Fr* dst, R29& lo, R29& hi) {
+  if (fold) {
+    const R29 x0 = to29(w[0]), x1 = to29(w[1]), x2 = to29(w[2]), x3 = to29(w[3]);
+    lo = red6p(add29(x0, mul29t(sub29(x1, x0), r)));
+    hi = red6p(add29(x2, mul29t(sub29(x3, x2), r)));
+    dst[0] = from29(lo);
+    dst[1] = from29(hi);
+  } else {
+    lo = to29(w[0]);
+    hi = to29(w[1]);
+  }
+}
+
+QG_DEV void load_pair(const Fr* src, bool fold, Fr (&w)[4]) {
+  w[0] = src[0];
+  w[1] = src[1];
+  if (fold) {
+    w[2] = src[2];
+    w[3] = src[3];
+  }
+}
+
+template <int K>
+QG_DEV R29 pick29(const R29 (&v)[K], uint32_t i) {
+  // select chain on a uniform index (v_cndmask): a switch of loads would be
+  // merged into one dynamically indexed load and demote v[] to scratch
+  i = __builtin_amdgcn_readfirstlane(i);
+  R29 r = v[0];
+#pragma unroll
+  for (int k = 1; k < K; k++)
+    if (i == (uint32_t)k) r = v[k];
+  return r;
+}
+
+// source / destination tables of round j of k_sc_big: round 0 reads the
+// input tables; round j >= 1 folds into X (j odd, N/2 per slot) or Y (j even,
+// N/4 per slot) and reads round j - 1's output
+struct AllBufs {
+  TablePtrs in;  // src[] = input tables
+  Fr* X;
+  Fr* Y;
+  size_t capX, capY;
+  QG_DEV const Fr* src(uint32_t j, uint32_t s) const {
+    if (j <= 1) return in.src[s];
+    return (j & 1) ? Y + capY * s : X + capX * s;
+  }
+  QG_DEV Fr* dst(uint32_t j, uint32_t s) const { return (j & 1) ? X + capX * s : Y + capY * s; }
+};
+
+template <int K, int NP, bool PURE, bool PF>
+QG_DEV void sweep_pairs(const AllBufs& tb, uint32_t j, bool fold, const R29& r, size_t npairs,
+                        size_t p0, size_t stride, const SopLds<NP>& sp, const SopHdr& h,
+                        R29 (&acc)[NP]) {
+  const uint32_t nslots = h.nslots, np = h.np;
+  uint32_t cnt = 0;
+  for (size_t p = p0; p < npairs; p += stride) {
+    R29 prod[NP];
+    if constexpr (PURE) {
+      Fr w[4], wn[4];
+      if constexpr (PF) load_pair(tb.src(j, 0) + (fold ? 4 : 2) * p, fold, w);
+      for (uint32_t s = 0; s < nslots; s++) {
+        if constexpr (PF) {
+          if (s + 1 < nslots) load_pair(tb.src(j, s + 1) + (fold ? 4 : 2) * p, fold, wn);
+        } else {
+          load_pair(tb.src(j, s) + (fold ? 4 : 2) * p, fold, w);
+        }
+        R29 lo, hi;
+        fold_pair(w, fold, r, tb.dst(j, s) + 2 * p, lo, hi);
+        const R29 d = norm29(sub29(hi, lo));
+#pragma unroll
+        for (int t = 0; t < NP; t++) {
+          const R29 v = at_point<NP>(lo, d, t, sp);
+          prod[t] = s == 0 ? v : mul29t(prod[t], v);
+        }
+        if constexpr (PF) {
+#pragma unroll
+          for (int i = 0; i < 4; i++) w[i] = wn[i];
+        }
+      }
+      // products of >= 2 factors are < 4p: three lazy additions stay below 16p
+#pragma unroll
+      for (int t = 0; t < NP; t++)
+        if ((uint32_t)t < np) acc[t] = add29(acc[t], prod[t]);
+      if (++cnt == 3) {
+#pragma unroll
+        for (int t = 0; t < NP; t++) acc[t] = red16p29<FrP>(acc[t]);
+        cnt = 0;
+      }
+    } else {
+      static_assert(PURE || K <= 4, "generic sweep keeps <= 4 slots in registers");
+      R29 lo[K], hi[K], dd[K];
+#pragma unroll
+      for (int s = 0; s < K; s++) {
+        lo[s] = hi[s] = dd[s] = R29::zero();
+        if ((uint32_t)s < nslots) {
+          Fr w[4];
+          load_pair(tb.src(j, s) + (fold ? 4 : 2) * p, fold, w);
+          fold_pair(w, fold, r, tb.dst(j, s) + 2 * p, lo[s], hi[s]);
+          dd[s] = norm29(sub29(hi[s], lo[s]));
+        }
+      }
+      uint32_t f = 0;
+      for (uint32_t m = 0; m < h.nmono; m++) {
+        const uint32_t len = sp.mono_len(m);
+        if (len == 0) {
+#pragma unroll
+          for (int t = 0; t < NP; t++) prod[t] = sp.c29[m];
+        } else {
+          for (uint32_t q = 0; q < len; q++) {
+            const uint32_t s = sp.fac(f + q);
+            const R29 a = pick29<K>(lo, s), d = pick29<K>(dd, s);
+#pragma unroll
+            for (int t = 0; t < NP; t++) {
+              const R29 v = at_point<NP>(a, d, t, sp);
+              prod[t] = q == 0 ? v : mul29t(prod[t], v);
+            }
+          }
+          if (!sp.skip(m) || len == 1) {
+#pragma unroll
+            for (int t = 0; t < NP; t++) prod[t] = mul29t(prod[t], sp.c29[m]);
+          }
+        }
+        f += len;
+        // every monomial value is < 4p (a single factor is scaled by its
+        // multiplier): three lazy additions stay below 16p
+#pragma unroll
+        for (int t = 0; t < NP; t++)
+          if ((uint32_t)t < np) acc[t] = add29(acc[t], prod[t]);
+        if (++cnt == 3) {
+#pragma unroll
+          for (int t = 0; t < NP; t++) acc[t] = red16p29<FrP>(acc[t]);
+          cnt = 0;
+        }
+      }
+    }
+  }
+#pragma unroll
+  for (int t = 0; t < NP; t++) acc[t] = red16p29<FrP>(acc[t]);
+}
+
+// One large round (tables > 2^PERS_LOG) in one launch: thread-per-pair sweep
+// (sweep_pairs), per-block partial rows, and the last block to publish
+// (ticket election) sums the rows and runs the transcript step (or, sharded,
+// writes this rank's local sums).
+template <int K, int NP, bool PURE, bool PF>
+__global__ void __launch_bounds__(SC_BLOCK)
+    k_sc_big(AllBufs tb, uint32_t j, const SopDev* __restrict__ spg, SopHdr h, size_t npairs,
+             RoundOut ro, int pending, Fr* __restrict__ partial, Fr* __restrict__ loc) {
+  __shared__ SopLds<NP> sp;
+  __shared__ R29 red[(SC_BLOCK / 64) * NP];
+  __shared__ R29 res[NP];
+  __shared__ FinSmem fs;
+  __shared__ uint32_t last;
+  const uint32_t tid = threadIdx.x;
+  const uint32_t tr = 1024 + 16 * j;
+  const bool fold = j > 0;
+  if (blockIdx.x == 0) SC_TR(tr + 0);
+  sop_load<NP>(sp, spg, h, loc == nullptr);
+  R29 r = R29::zero();
+  if (fold) {
+#pragma unroll
+    for (int i = 0; i < 9; i++) r.l[i] = ro.st->r29[i];
+  }
+  if (pending && blockIdx.x == 0 && tid >= 64 && tid < 128) {
+    // deferred absorb of round j-1's challenge bytes (wave 1 of block 0)
+    if (tid - 64 < 32) fs.ab[tid - 64] = tid - 64 < 20 ? ro.st->pend[tid - 64] : 0u;
+    __builtin_amdgcn_s_waitcnt(0);
+    __builtin_amdgcn_wave_barrier();
+    b3_hash_quad(fs.ab, 80, ro.st->state, 8);
+    __builtin_amdgcn_fence(__ATOMIC_RELEASE, "agent");
+  }
+  __syncthreads();
+  const uint32_t np = h.np;
+  R29 acc[NP];
+#pragma unroll
+  for (int t = 0; t < NP; t++) acc[t] = R29::zero();
+  sweep_pairs<K, NP, PURE, PF>(tb, j, fold, r, npairs, (size_t)blockIdx.x * SC_BLOCK + tid,
+                           (size_t)gridDim.x * SC_BLOCK, sp, h, acc);
+  if (blockIdx.x == 0) SC_TR(tr + 1);
+  block_sums29<NP>(acc, np, red, res);
+  if (tid < np) partial[(size_t)blockIdx.x * NP + tid] = from29(canon29(res[tid]));
+  __syncthreads();
+  if (tid == 0) {
+    __builtin_amdgcn_fence(__ATOMIC_RELEASE, "agent");
+    const uint32_t old =
+        __hip_atomic_fetch_add(&ro.st->ticket, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+    last = old + 1 == gridDim.x;
+    if (last) __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "agent");
+  }
+  __syncthreads();
+  if (!last) return;
+  SC_TR(tr + 2);
+  sum_rows29<NP>(partial, gridDim.x, np, red, res);
+  if (tid == 0) ro.st->ticket = 0;
+  if (loc) {
+    if (tid < NP) loc[tid] = tid < np ? from29(canon29(res[tid])) : Fr::zero();
+    return;
+  }
+  finish_core<NP>(sp, np, res, ro, j, fs, ro.st->state, ro.st->pend, nullptr, tr);
   if (tid < 9) ro.st->r29[tid] = fs.r.l[tid];
   SC_TR(tr + 7);
 }
@@ -518,7 +835,7 @@ __global__ void __launch_bounds__(SC_BLOCK)
                 uint32_t nrows, RoundOut ro, uint32_t j) {
   __shared__ SopLds<NP> sp;
   __shared__ R29 red[(SC_BLOCK / 64) * NP];
-  __shared__ Fr res[NP];
+  __shared__ R29 res[NP];
   __shared__ FinSmem fs;
   __shared__ uint32_t st[8];
   const uint32_t tid = threadIdx.x;
@@ -581,7 +898,7 @@ __global__ void __launch_bounds__(TAIL_BLOCK)
   __shared__ SopLds<NP> sp;
   __shared__ RoundLds<K, NP, TAIL_BLOCK> L;
   __shared__ R29 red[(TAIL_BLOCK / 64) * NP];
-  __shared__ Fr res[NP];
+  __shared__ R29 res[NP];
   __shared__ FinSmem fs;
   __shared__ uint32_t st[8];
   __shared__ uint32_t pend[32];
@@ -617,10 +934,12 @@ __global__ void __launch_bounds__(TAIL_BLOCK)
                                    (size_t)nb * PB, acc);
     if (writer) SC_TR(16 * j + 1);
     block_reduce_pts<NP>(acc, np, red, res);
+    if (writer) SC_TR(16 * j + 7);
     if (nb > 1) {
       Fr* part = partial + (size_t)(j & 1) * gridDim.x * NP;
-      if (tid < np) part[(size_t)blk * NP + tid] = res[tid];
+      if (tid < np) part[(size_t)blk * NP + tid] = from29(canon29(res[tid]));
       grid_barrier(bar + j, nb, &ro.st->err);
+      if (writer) SC_TR(16 * j + 8);
       acc = R29::zero();
       const uint32_t t = tid % NP;
       if (t < np)
@@ -830,7 +1149,10 @@ static std::shared_ptr<const ScProgram> get_program(const qg_expr_op* prog, size
   d.cr29[1] = l9_of(pow2_mod_plain<FrP>(778));
   d.cr29[2] = l9_of(pow2_mod_plain<FrP>(517));
   d.cr29[3] = l9_of(pow2_mod_plain<FrP>(773));
-  p->hdr = {d.nmono, d.nslots, np, 0};
+  bool pure = d.nmono == 1 && sp.is_one[0] && sp.mono_len[0] == d.nslots && d.nslots >= 2 &&
+              d.nslots == sp.degree;
+  for (uint32_t f = 0; pure && f < d.nfac; f++) pure = sp.fac[f] == f;
+  p->hdr = {d.nmono, d.nslots, np, pure ? SOP_PURE : 0u};
   p->used = sp.used;
   p->nused = (uint32_t)sp.used.size();
   std::lock_guard<std::mutex> lk(g_prog_mu);
@@ -862,10 +1184,52 @@ static unsigned persist_grid_cap(qg_ctx* ctx, size_t cus) {
   return (unsigned)std::max<size_t>(1, cus);
 }
 
+// thread-per-pair round kernel (k_sc_big) for product expressions and for
+// expressions of <= 4 slots at degree <= 3; false: use the staged k_sc_round
+static unsigned sc_big_blocks(qg_ctx* ctx, size_t npairs) {
+  static int ov = [] {
+    const char* e = getenv("QG_SC_BIG_BLOCKS");
+    return e ? atoi(e) : 0;
+  }();
+  size_t cap = ov > 0 ? (size_t)ov : (size_t)4 * ctx->num_cus();
+  cap = std::min<size_t>(cap, SC_MAX_BLOCKS);
+  return (unsigned)std::max<size_t>(1, std::min<size_t>(cap, div_up(npairs, SC_BLOCK)));
+}
+
+template <int K, int NP>
+static bool launch_big(qg_ctx* ctx, const std::vector<const Fr*>& src, Fr* X, Fr* Y, size_t N,
+                       uint32_t j, const SopDev* d_sp, SopHdr h, size_t npairs, RoundOut ro,
+                       int pending, Fr* partial, Fr* loc) {
+  if (sc_use_staged() || NP > 4) return false;
+  const bool pure = (h.pad & SOP_PURE) != 0;
+  if (!pure && K > 4) return false;
+  AllBufs tb{};
+  for (uint32_t i = 0; i < 8; i++) tb.in.src[i] = i < src.size() ? src[i] : nullptr;
+  tb.X = X;
+  tb.Y = Y;
+  tb.capX = N / 2;
+  tb.capY = std::max<size_t>(1, N / 4);
+  const unsigned blocks = sc_big_blocks(ctx, npairs);
+  // QG_SC_PF=1: next slot's entries prefetched during the current slot (tuning)
+  static const bool pf = getenv("QG_SC_PF") != nullptr;
+  if (pure && pf)
+    hipLaunchKernelGGL((k_sc_big<K, 4, true, true>), dim3(blocks), dim3(SC_BLOCK), 0, ctx->stream,
+                       tb, j, d_sp, h, npairs, ro, pending, partial, loc);
+  else if (pure)
+    hipLaunchKernelGGL((k_sc_big<K, 4, true, false>), dim3(blocks), dim3(SC_BLOCK), 0, ctx->stream,
+                       tb, j, d_sp, h, npairs, ro, pending, partial, loc);
+  else
+    hipLaunchKernelGGL((k_sc_big<4, 4, false, false>), dim3(blocks), dim3(SC_BLOCK), 0, ctx->stream,
+                       tb, j, d_sp, h, npairs, ro, pending, partial, loc);
+  QG_LAUNCH_CHECK();
+  return true;
+}
+
 template <int K, int NP>
 static void run_rounds(qg_ctx* ctx, uint32_t nvars, const std::vector<const Fr*>& src,
                        const SopDev* d_sp, SopHdr h, RoundOut ro, uint32_t* bar, Fr* d_final,
                        Fr* d_eval) {
+
   const uint32_t nslots = h.nslots;
   const size_t N = (size_t)1 << nvars;
   // ping-pong scratch: X holds N/2 per slot, Y holds N/4 per slot
@@ -889,14 +1253,15 @@ static void run_rounds(qg_ctx* ctx, uint32_t nvars, const std::vector<const Fr*>
       const size_t table = N >> j;  // entries per table evaluated in round j
       if (table <= ((size_t)1 << PERS_LOG)) break;
       const size_t npairs = table / 2;
-      const unsigned blocks = sc_round_blocks(ctx, npairs);
       TablePtrs tp = cur;
       if (fold) {
         const TablePtrs& d = parity ? tY : tX;
         for (int i = 0; i < 8; i++) tp.dst[i] = d.dst[i];
       }
-      hipLaunchKernelGGL((k_sc_round<K, NP>), dim3(blocks), dim3(SC_BLOCK), 0, ctx->stream, tp,
-                         d_sp, h, npairs, fold, ro, j, pending, partial, (Fr*)nullptr);
+      if (!launch_big<K, NP>(ctx, src, X, Y, N, j, d_sp, h, npairs, ro, pending, partial, nullptr))
+        hipLaunchKernelGGL((k_sc_round<K, NP>), dim3(sc_round_blocks(ctx, npairs)), dim3(SC_BLOCK),
+                           0, ctx->stream, tp, d_sp, h, npairs, fold, ro, j, pending, partial,
+                           (Fr*)nullptr);
       QG_LAUNCH_CHECK();
       if (fold) {
         for (int i = 0; i < 8; i++) cur.src[i] = tp.dst[i];
@@ -994,14 +1359,14 @@ static void run_rounds_dist(qg_ctx* ctx, uint32_t nvars, const std::vector<const
     QgTimed tm(ctx, "sumcheck_round");
     for (uint32_t j = 0; j < js; j++) {
       const size_t npairs = (NL >> j) / 2;
-      const unsigned blocks = sc_round_blocks(ctx, npairs);
       TablePtrs tp = cur;
       if (fold) {
         const TablePtrs& d = parity ? tY : tX;
         for (int i = 0; i < 8; i++) tp.dst[i] = d.dst[i];
       }
-      hipLaunchKernelGGL((k_sc_round<K, NP>), dim3(blocks), dim3(SC_BLOCK), 0, ctx->stream, tp,
-                         d_sp, h, npairs, fold, ro, j, 0, partial, loc);
+      if (!launch_big<K, NP>(ctx, src, X, Y, NL, j, d_sp, h, npairs, ro, 0, partial, loc))
+        hipLaunchKernelGGL((k_sc_round<K, NP>), dim3(sc_round_blocks(ctx, npairs)), dim3(SC_BLOCK),
+                           0, ctx->stream, tp, d_sp, h, npairs, fold, ro, j, 0, partial, loc);
       QG_LAUNCH_CHECK();
       comm_allgather_bytes(ctx, loc, all, sizeof(Fr) * NP);
       hipLaunchKernelGGL((k_sc_finish<NP>), dim3(1), dim3(SC_BLOCK), 0, ctx->stream, d_sp, h, all,
@@ -1101,7 +1466,7 @@ static void sumcheck_run(qg_ctx* ctx, uint32_t nvars, uint32_t ntables,
   // one device region: ScState | barrier counters | chal | coeffs | final (8 slots +
   // evaluation) | lens.  ScState and the counters are (re)initialised per call.
   const size_t o_bar = sizeof(ScState);
-  const size_t o_chal = o_bar + sizeof(uint32_t) * ((nvars + 7) & ~7u);
+  const size_t o_chal = o_bar + sizeof(uint32_t) * ((nvars + 2 + 7) & ~7u);
   const size_t o_coeffs = o_chal + sizeof(Fr) * nvars;
   const size_t o_final = o_coeffs + sizeof(Fr) * (size_t)nvars * width;
   const size_t o_lens = o_final + sizeof(Fr) * 9;
@@ -1113,9 +1478,10 @@ static void sumcheck_run(qg_ctx* ctx, uint32_t nvars, uint32_t ntables,
     QG_HIP(hipMemcpyAsync(d_sp, &P->img, sizeof(SopDev), hipMemcpyHostToDevice, ctx->stream));
     ctx->memo["sc_prog"] = memo;
   }
-  std::vector<uint8_t> hin(o_chal, 0);
-  memcpy(hin.data(), &hs, sizeof hs);
-  QG_HIP(hipMemcpyAsync(io, hin.data(), o_chal, hipMemcpyHostToDevice, ctx->stream));
+  uint8_t* hio = reinterpret_cast<uint8_t*>(ctx->pinned_get("sc_io", io_bytes));
+  memset(hio, 0, o_chal);
+  memcpy(hio, &hs, sizeof hs);
+  QG_HIP(hipMemcpyAsync(io, hio, o_chal, hipMemcpyHostToDevice, ctx->stream));
   uint32_t* bar = reinterpret_cast<uint32_t*>(io + o_bar);
 
   std::vector<const Fr*> src;
@@ -1138,9 +1504,9 @@ static void sumcheck_run(qg_ctx* ctx, uint32_t nvars, uint32_t ntables,
     run_rounds_any<8, 16>(ctx, nvars, src, d_sp, P->hdr, ro, bar, d_final, d_eval);
   }
 
-  std::vector<uint8_t> h(io_bytes);
-  QG_HIP(hipMemcpyAsync(h.data(), io, io_bytes, hipMemcpyDeviceToHost, ctx->stream));
+  QG_HIP(hipMemcpyAsync(hio, io, io_bytes, hipMemcpyDeviceToHost, ctx->stream));
   ctx->sync();
+  const std::vector<uint8_t> h(hio, hio + io_bytes);
   QG_CHECK(reinterpret_cast<const ScState*>(h.data())->err == 0, QG_ERR_DEVICE,
            "sumcheck: grid barrier timed out (persistent blocks not co-resident)");
   memcpy(state, h.data(), 32);

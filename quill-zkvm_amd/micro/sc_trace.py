@@ -34,11 +34,12 @@ for j in range(nv):
     t0 = buf[b]
     print(j, " ".join(f"{names_r[k]}={(buf[b + k] - t0) * tick:.2f}" for k in range(1, 8)
                       if buf[b + k]))
-names_t = ["start", "evaluated", "reduced", "interp", "hash1", "hash2", "chal"]
+names_t = ["start", "evaluated", "reduced", "interp", "hash1", "hash2", "chal", "blockred", "barrier"]
 print("tail rounds, us relative to round start")
 for j in range(nv):
     b = 16 * j
     if buf[b] == 0 or buf[b + 6] == 0:
         continue
     t0 = buf[b]
-    print(j, " ".join(f"{names_t[k]}={(buf[b + k] - t0) * tick:.2f}" for k in range(1, 7)))
+    print(j, " ".join(f"{names_t[k]}={(buf[b + k] - t0) * tick:.2f}" for k in (1, 7, 8, 2, 3, 4, 5, 6)
+                      if buf[b + k] >= t0))
