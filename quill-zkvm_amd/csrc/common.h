@@ -200,6 +200,10 @@ static int qg_guard(qg_ctx* ctx, F&& f) {
 namespace qg {
 // MSM over device scalars; result (XYZZ, summed over RCCL ranks if attached)
 G1Affine msm_device(qg_ctx* ctx, const qg_srs* srs, const Fr* d_scalars, size_t n);
+// k MSMs over one SRS with shared reduction launches (null scalars allowed when n = 0)
+std::vector<G1Affine> msm_device_batch(qg_ctx* ctx, const qg_srs* srs,
+                                       const std::vector<const Fr*>& scalars,
+                                       const std::vector<size_t>& ns);
 void fr_upload(qg_ctx* ctx, Fr* d, const uint64_t* h, size_t n);
 void fr_download(qg_ctx* ctx, uint64_t* h, const Fr* d, size_t n);
 // affine G1 -> ABI (xy Montgomery limbs + inf flag)

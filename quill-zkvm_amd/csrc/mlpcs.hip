@@ -442,6 +442,33 @@ static size_t trimmed_len(qg_ctx* ctx, const Fr* a, size_t n) {
   return (size_t)h;
 }
 
+// KZG::open quotient on a device polynomial: x, y into `out`, the quotient
+// coefficients q_i = s_{i+1} (i < Lt - 1) in scratch slot `slot`; returns the
+// quotient pointer and its length for the (batched) commitment
+static std::pair<const Fr*, size_t> kzg_quotient_device(qg_ctx* ctx, const qg_srs* srs,
+                                                        const Fr* c, size_t L, const Fr& x,
+                                                        qg_kzg_opening* out, int slot) {
+  fr_export(x, out->x);
+  size_t Lt = trimmed_len(ctx, c, L);  // DensePolynomial::from_coefficients_slice trims
+  Fr y = Fr::zero();
+  const Fr* q = nullptr;
+  size_t qn = 0;
+  if (Lt > 0) {
+    Fr* s = ctx->scratch_as<Fr>("open_s#" + std::to_string(slot), Lt);
+    {
+      QgTimed tm(ctx, "kzg_division");
+      suffix_horner(ctx, c, Lt, x, s);
+    }
+    QG_HIP(hipMemcpyAsync(&y, s, sizeof(Fr), hipMemcpyDeviceToHost, ctx->stream));
+    ctx->sync();
+    QG_CHECK(Lt - 1 <= srs->n, QG_ERR_INVALID, "Polynomial degree exceeds max degree");
+    q = s + 1;
+    qn = Lt - 1;
+  }
+  fr_export(y, out->y);
+  return {q, qn};
+}
+
 // KZG::open on a device polynomial; fills x, y, proof
 static void kzg_open_device(qg_ctx* ctx, const qg_srs* srs, const Fr* c, size_t L, const Fr& x,
                             qg_kzg_opening* out) {
@@ -638,11 +665,22 @@ static void mle_open_device(qg_ctx* ctx, const qg_srs* srs, const Fr* dpoly, siz
   Fr r_inv = finv(r);
   fr_export(evaluation, out->evaluation);
   g1_export(s_comm, out->s_comm_xy, &out->s_comm_inf);
-  // four KZG openings (mlpcs.rs:108-113)
-  kzg_open_device(ctx, srs, dpoly, n, r, &out->poly_opening);
-  kzg_open_device(ctx, srs, dpoly, n, r_inv, &out->poly_opening_inv);
-  kzg_open_device(ctx, srs, dS, Slen, r, &out->s_opening);
-  kzg_open_device(ctx, srs, dS, Slen, r_inv, &out->s_opening_inv);
+  // four KZG openings (mlpcs.rs:108-113): the four quotients first, then their
+  // commitments as one MSM batch (shared reduction launches)
+  qg_kzg_opening* outs[4] = {&out->poly_opening, &out->poly_opening_inv, &out->s_opening,
+                             &out->s_opening_inv};
+  const Fr* polys[4] = {dpoly, dpoly, dS, dS};
+  const size_t lens[4] = {n, n, Slen, Slen};
+  const Fr xs[4] = {r, r_inv, r, r_inv};
+  std::vector<const Fr*> qs;
+  std::vector<size_t> qns;
+  for (int i = 0; i < 4; i++) {
+    auto q = kzg_quotient_device(ctx, srs, polys[i], lens[i], xs[i], outs[i], i);
+    qs.push_back(q.first);
+    qns.push_back(q.second);
+  }
+  const std::vector<G1Affine> pis = msm_device_batch(ctx, srs, qs, qns);
+  for (int i = 0; i < 4; i++) g1_export(pis[i], outs[i]->proof_xy, &outs[i]->proof_inf);
 }
 
 }  // namespace qg

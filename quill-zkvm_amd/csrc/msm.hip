@@ -31,14 +31,26 @@ namespace qg {
 static constexpr int MSM_COMBINE_SEQ = 64;  // partials a bucket's combine adds sequentially
 static constexpr int MSM_BLOCK = 256;
 
-// window size for an SRS of n bases (tuned later)
+// Window size for an SRS of n bases.  Cost model in bucket-addition units:
+// n * ceil(255 / c) accumulations + ~12 per bucket for bucketing and the
+// reduction (fitted to MI355X runs: 2^24 c = 20 vs 22, 2^22 c = 20 vs 17 / 19).
+// Windows whose top digit covers few bits (k = 254 - c (W - 1), scalars <
+// 2^254) send n / 2^k entries to each of 2^k buckets (skewed combine):
+// excluded when that exceeds 4096.  Gives c = 17 at 2^20, 20 at 2^21..2^24.
 static int msm_window_bits(size_t n) {
-  int lg = 0;
-  while (((size_t)1 << lg) < n) lg++;
-  int c = lg - 3;
-  if (c < 4) c = 4;
-  if (c > 21) c = 21;
-  return c;
+  int best = 4;
+  double best_cost = 1e300;
+  for (int c = 4; c <= 22; c++) {
+    const int W = (255 + c - 1) / c;
+    const int k = 254 - c * (W - 1);
+    if (k < 30 && (n >> k) > 4096) continue;
+    const double cost = (double)n * W + 12.0 * (double)((size_t)1 << (c - 1));
+    if (cost < best_cost) {
+      best_cost = cost;
+      best = c;
+    }
+  }
+  return best;
 }
 
 // canonical words of a Montgomery-form scalar, x 2^-256 mod r: the 29-bit
@@ -639,25 +651,34 @@ __global__ void __launch_bounds__(MSM_BLOCK)
 }
 
 // ---- reduction ------------------------------------------------------------
+// per-MSM inputs of the batched reduction kernels (blockIdx.y = MSM)
+struct MsmRed {
+  const X29Raw* partial;
+  const uint32_t* bstart;
+  uint32_t L, step;
+};
+
 // B_j = sum of bucket j's partial slots at offsets 0, step, 2 step, ... (empty
-// bucket -> infinity); at most MSM_COMBINE_SEQ of them
+// bucket -> infinity); at most MSM_COMBINE_SEQ of them.  buckets: nb per MSM.
 __global__ void __launch_bounds__(MSM_BLOCK)
-    k_msm_combine(const X29Raw* __restrict__ partial, const uint32_t* __restrict__ bstart,
-                              uint32_t nb, uint32_t L, uint32_t step, G1Xyzz* __restrict__ buckets) {
+    k_msm_combine(const MsmRed* __restrict__ runs, uint32_t nb, G1Xyzz* __restrict__ buckets) {
   const uint32_t j = blockIdx.x * blockDim.x + threadIdx.x;
   if (j >= nb) return;
-  if (bstart[j] == bstart[j + 1]) {
-    buckets[j] = x29_store(x29_inf());
+  const MsmRed rr = runs[blockIdx.y];
+  G1Xyzz* out = buckets + (size_t)blockIdx.y * nb;
+  const X29Raw* partial = rr.partial;
+  if (rr.bstart[j] == rr.bstart[j + 1]) {
+    out[j] = x29_store(x29_inf());
     return;
   }
-  const uint32_t f = msm_slot_first(bstart, j, L), l = msm_slot_last(bstart, j, L);
-  if (l - f < step) {
-    buckets[j] = x29_store(msm_partial(partial, f));
+  const uint32_t f = msm_slot_first(rr.bstart, j, rr.L), l = msm_slot_last(rr.bstart, j, rr.L);
+  if (l - f < rr.step) {
+    out[j] = x29_store(msm_partial(partial, f));
     return;
   }
   X29 acc = msm_partial(partial, f);
-  for (uint32_t t = f + step; t <= l; t += step) acc = x29_add(acc, msm_partial(partial, t));
-  buckets[j] = x29_store(acc);
+  for (uint32_t t = f + rr.step; t <= l; t += rr.step) acc = x29_add(acc, msm_partial(partial, t));
+  out[j] = x29_store(acc);
 }
 
 // k doublings (k < 32)
@@ -678,9 +699,15 @@ QG_DEV X29 x29_dbl_k(X29 p, int k) {
 // Level 1 runs on the buckets with P = Q = B: sum_j (j + 1) B_j.
 __global__ void __launch_bounds__(MSM_BLOCK)
     k_msm_wsum(const G1Xyzz* __restrict__ P, const G1Xyzz* __restrict__ Q, uint32_t m, int slog,
-               int rlog, G1Xyzz* __restrict__ A_out, G1Xyzz* __restrict__ R_out) {
+               int rlog, G1Xyzz* __restrict__ A_out, G1Xyzz* __restrict__ R_out, size_t stride_in,
+               size_t stride_out) {
   __shared__ G1Xyzz sh_r[MSM_BLOCK], sh_a[MSM_BLOCK];
   const uint32_t t = threadIdx.x, T = blockDim.x;
+  // MSM blockIdx.y of a batch: inputs stride_in apart, outputs stride_out apart
+  P += blockIdx.y * stride_in;
+  if (Q) Q += blockIdx.y * stride_in;
+  A_out += blockIdx.y * stride_out;
+  if (R_out) R_out += blockIdx.y * stride_out;
   const uint64_t lo = ((uint64_t)blockIdx.x * T + t) << slog;
   X29 run = x29_inf(), acc = x29_inf();
   if (lo < m) {
@@ -724,13 +751,16 @@ __global__ void __launch_bounds__(MSM_BLOCK)
 }
 
 // R = 2^261 XYZZ words -> R = 2^256 Montgomery XYZZ (canonical) for the host
-__global__ void k_msm_export(const G1Xyzz* __restrict__ in, G1Xyzz* __restrict__ out) {
-  const X29 p = x29_load(*in);
+__global__ void k_msm_export(const G1Xyzz* __restrict__ in, size_t stride, uint32_t k,
+                             G1Xyzz* __restrict__ out) {
+  const uint32_t i = threadIdx.x;
+  if (i >= k) return;
+  const X29 p = x29_load(in[i * stride]);
   if (x29_is_inf(p)) {
-    *out = G1Xyzz::infinity();
+    out[i] = G1Xyzz::infinity();
     return;
   }
-  *out = {q29_export(p.X), q29_export(p.Y), q29_export(p.ZZ), q29_export(p.ZZZ)};
+  out[i] = {q29_export(p.X), q29_export(p.Y), q29_export(p.ZZ), q29_export(p.ZZZ)};
 }
 
 // arkworks affine points (R = 2^256 words, (0,0) = infinity) -> table rows
@@ -864,9 +894,24 @@ static qg_srs* srs_alloc(qg_ctx* ctx, size_t n) {
   return srs;
 }
 
-G1Affine msm_device(qg_ctx* ctx, const qg_srs* srs, const Fr* d_scalars, size_t n) {
+// One MSM of a batch after bucketing + accumulation: its partial slots and
+// bucket offsets (per-slot scratch, so a batch's reductions run together).
+struct MsmRun {
+  bool empty = true;
+  uint32_t L = 1;
+  size_t nslots = 0;
+  X29Raw* partial = nullptr;
+  uint32_t* owner = nullptr;
+  uint32_t* bstart = nullptr;
+  uint32_t* misc = nullptr;  // [0] nchunks, [1] max accumulation threads per bucket
+};
+
+// bucketing (two-pass radix sort) + bucket accumulation of MSM `slot` of a batch
+static MsmRun msm_accumulate_phase(qg_ctx* ctx, const qg_srs* srs, const Fr* d_scalars, size_t n,
+                                   int slot) {
   QG_CHECK(n <= srs->n, QG_ERR_INVALID, "MSM length exceeds the SRS");
-  G1Xyzz local = G1Xyzz::infinity();
+  MsmRun run;
+  const std::string sfx = "#" + std::to_string(slot);
   if (n > 0) {
     const int c = srs->c, W = srs->W;
     const uint32_t nb = 1u << (c - 1);
@@ -891,7 +936,7 @@ G1Affine msm_device(qg_ctx* ctx, const qg_srs* srs, const Fr* d_scalars, size_t 
     uint32_t* gstart = ctx->scratch_as<uint32_t>("msm_gstart", H + 1);
     uint32_t* cbase = ctx->scratch_as<uint32_t>("msm_cbase", H + 1);
     uint32_t* cgroup = ctx->scratch_as<uint32_t>("msm_cgroup", max_chunks);
-    uint32_t* misc = ctx->scratch_as<uint32_t>("msm_misc", 4);  // [0] nchunks, [1] max tpb
+    uint32_t* misc = ctx->scratch_as<uint32_t>("msm_misc" + sfx, 4);  // [0] nchunks, [1] max tpb
     uint32_t* chist = ctx->scratch_as<uint32_t>("msm_chist", max_chunks * NL);
     uint32_t* coff = ctx->scratch_as<uint32_t>("msm_coff", max_chunks * NL);
     uint32_t* tmp_e = ctx->scratch_as<uint32_t>("msm_tmp_e", max_entries + 1);
@@ -900,7 +945,7 @@ G1Affine msm_device(qg_ctx* ctx, const qg_srs* srs, const Fr* d_scalars, size_t 
     uint32_t* orow = ctx->scratch_as<uint32_t>("msm_orow", nghist + 1);
     Fr* canon = ctx->scratch_as<Fr>("msm_canon", n);
     uint32_t* counts = ctx->scratch_as<uint32_t>("msm_counts", nb);
-    uint32_t* bstart = ctx->scratch_as<uint32_t>("msm_bstart", nb + 1);
+    uint32_t* bstart = ctx->scratch_as<uint32_t>("msm_bstart" + sfx, nb + 1);
     uint32_t* tstart = ctx->scratch_as<uint32_t>("msm_tstart", nb + 1);
     uint32_t* cursor = ctx->scratch_as<uint32_t>("msm_cursor", nb);
     uint32_t* entries = ctx->scratch_as<uint32_t>("msm_entries", max_entries + 1);
@@ -916,16 +961,8 @@ G1Affine msm_device(qg_ctx* ctx, const qg_srs* srs, const Fr* d_scalars, size_t 
     const uint32_t L = 1u << elog;
     const size_t max_threads = div_up(max_entries, L);
     const size_t nslots = max_threads + nb + 1;  // partial slot of (thread t, bucket b): t + b
-    X29Raw* partial = ctx->scratch_as<X29Raw>("msm_partial", nslots);
-    uint32_t* owner = ctx->scratch_as<uint32_t>("msm_owner", nslots);
-    G1Xyzz* buckets = ctx->scratch_as<G1Xyzz>("msm_buckets", nb);
-    // bucket reduction: level 1 over the buckets (8 per thread), level 2 in one block
-    const int slog1 = nb >= 8u * MSM_BLOCK ? 3 : 0;
-    const uint32_t nred = div_up(nb, (size_t)MSM_BLOCK << slog1);
-    int slog2 = 0;
-    while (((size_t)MSM_BLOCK << slog2) < nred) slog2++;
-    QG_CHECK(slog2 <= 12, QG_ERR_UNSUPPORTED, "bucket count too large");
-    G1Xyzz* red = ctx->scratch_as<G1Xyzz>("msm_red", 2 * nred + 3);
+    X29Raw* partial = ctx->scratch_as<X29Raw>("msm_partial" + sfx, nslots);
+    uint32_t* owner = ctx->scratch_as<uint32_t>("msm_owner" + sfx, nslots);
     QG_CHECK(ntiles <= 1024 * 64 && H <= 1024 && NL <= 4096, QG_ERR_UNSUPPORTED,
              "bucket count too large");
     QG_CHECK(nslots < 0xffffffffull && max_chunks < 0xffffffffull, QG_ERR_UNSUPPORTED,
@@ -1007,56 +1044,129 @@ G1Affine msm_device(qg_ctx* ctx, const qg_srs* srs, const Fr* d_scalars, size_t 
                          0, ctx->stream, srs->d_table, entries, bstart, nb, L, partial, owner);
       QG_LAUNCH_CHECK();
     }
-    uint32_t max_tpb = 0;
-    QG_HIP(hipMemcpyAsync(&max_tpb, misc + 1, sizeof(uint32_t), hipMemcpyDeviceToHost, ctx->stream));
-    QG_HIP(hipStreamSynchronize(ctx->stream));
-    {
-      QgTimed tm(ctx, "msm_reduce");
-      // tree steps only until every bucket has <= MSM_COMBINE_SEQ partials
-      // left; the combine kernel adds those sequentially (one launch instead
-      // of log2(max partials) full-grid steps for typical, unskewed scalars).
-      // A bucket of count c spans at most ceil(c / L) + 1 slots.
-      const uint32_t max_slots = max_tpb + 1;
+    run.empty = n == 0;
+    run.L = L;
+    run.nslots = nslots;
+    run.partial = partial;
+    run.owner = owner;
+    run.bstart = bstart;
+    run.misc = misc;
+  }
+  return run;
+}
+
+// Bucket reduction of a batch of accumulated MSMs (same SRS): tree steps for
+// skewed buckets (per MSM, rare), then ONE launch each of the bucket combine,
+// the two weighted-sum levels and the export for the whole batch — the
+// latency-bound tail of the MSM is paid once per batch.  out: XYZZ (R = 2^256)
+// per MSM, not yet summed over ranks.
+static void msm_reduce_phase(qg_ctx* ctx, const qg_srs* srs, const std::vector<MsmRun>& runs,
+                             std::vector<G1Xyzz>& out) {
+  const uint32_t k = (uint32_t)runs.size();
+  out.assign(k, G1Xyzz::infinity());
+  std::vector<uint32_t> live;
+  for (uint32_t i = 0; i < k; i++)
+    if (!runs[i].empty) live.push_back(i);
+  if (live.empty()) return;
+  QG_CHECK(live.size() <= 1024, QG_ERR_UNSUPPORTED, "MSM batch too large");
+  const uint32_t kl = (uint32_t)live.size();
+  const uint32_t nb = 1u << (srs->c - 1);
+  // max accumulation threads per bucket of every MSM (one transfer)
+  uint32_t* d_mx = ctx->scratch_as<uint32_t>("msm_maxtpb", kl);
+  for (uint32_t q = 0; q < kl; q++)
+    QG_HIP(hipMemcpyAsync(d_mx + q, runs[live[q]].misc + 1, sizeof(uint32_t),
+                          hipMemcpyDeviceToDevice, ctx->stream));
+  std::vector<uint32_t> mx(kl);
+  QG_HIP(hipMemcpyAsync(mx.data(), d_mx, kl * sizeof(uint32_t), hipMemcpyDeviceToHost,
+                        ctx->stream));
+  QG_HIP(hipStreamSynchronize(ctx->stream));
+  const int slog1 = nb >= 8u * MSM_BLOCK ? 3 : 0;
+  const uint32_t nred = div_up(nb, (size_t)MSM_BLOCK << slog1);
+  int slog2 = 0;
+  while (((size_t)MSM_BLOCK << slog2) < nred) slog2++;
+  QG_CHECK(slog2 <= 12, QG_ERR_UNSUPPORTED, "bucket count too large");
+  G1Xyzz* buckets = ctx->scratch_as<G1Xyzz>("msm_buckets", (size_t)kl * nb);
+  const size_t rstride = 2 * (size_t)nred + 1;  // per MSM: A[nred] | R[nred] | total
+  G1Xyzz* red = ctx->scratch_as<G1Xyzz>("msm_red", (size_t)kl * rstride);
+  G1Xyzz* d_out = ctx->scratch_as<G1Xyzz>("msm_out", kl);
+  MsmRed* d_runs = ctx->scratch_as<MsmRed>("msm_runs", kl);
+  std::vector<MsmRed> h_runs(kl);
+  {
+    QgTimed tm(ctx, "msm_reduce");
+    // tree steps only until every bucket has <= MSM_COMBINE_SEQ partials left;
+    // the combine adds those sequentially.  A bucket of count c spans at most
+    // ceil(c / L) + 1 slots.
+    for (uint32_t q = 0; q < kl; q++) {
+      const MsmRun& r = runs[live[q]];
+      const uint32_t max_slots = mx[q] + 1;
       uint32_t st = 1;
       while ((size_t)st * MSM_COMBINE_SEQ < max_slots) {
-        hipLaunchKernelGGL(k_msm_tree_step, dim3(div_up(nslots, MSM_BLOCK)), dim3(MSM_BLOCK), 0,
-                           ctx->stream, partial, owner, bstart, L, (uint32_t)nslots, st);
+        hipLaunchKernelGGL(k_msm_tree_step, dim3(div_up(r.nslots, MSM_BLOCK)), dim3(MSM_BLOCK), 0,
+                           ctx->stream, r.partial, r.owner, r.bstart, r.L, (uint32_t)r.nslots, st);
         QG_LAUNCH_CHECK();
         st <<= 1;
       }
-      hipLaunchKernelGGL(k_msm_combine, dim3(div_up(nb, MSM_BLOCK)), dim3(MSM_BLOCK), 0,
-                         ctx->stream, partial, bstart, nb, L, st, buckets);
-      QG_LAUNCH_CHECK();
-      // level 1: A = red[0, nred), R = red[nred, 2 nred); level 2: red[2 nred]
-      hipLaunchKernelGGL(k_msm_wsum, dim3(nred), dim3(MSM_BLOCK), 0, ctx->stream, buckets,
-                         (const G1Xyzz*)nullptr, nb, slog1, 8 + slog1, red, red + nred);
-      QG_LAUNCH_CHECK();
-      const uint32_t t2 = div_up(nred, (size_t)1 << slog2);
-      hipLaunchKernelGGL(k_msm_wsum, dim3(1), dim3(t2 < 64 ? 64 : t2), 0, ctx->stream,
-                         red + nred, red, nred, slog2, 0, red + 2 * nred, (G1Xyzz*)nullptr);
-      QG_LAUNCH_CHECK();
+      h_runs[q] = {r.partial, r.bstart, r.L, st};
     }
-    hipLaunchKernelGGL(k_msm_export, dim3(1), dim3(1), 0, ctx->stream, red + 2 * nred,
-                       red + 2 * nred + 1);
+    QG_HIP(hipMemcpyAsync(d_runs, h_runs.data(), kl * sizeof(MsmRed), hipMemcpyHostToDevice,
+                          ctx->stream));
+    hipLaunchKernelGGL(k_msm_combine, dim3(div_up(nb, MSM_BLOCK), kl), dim3(MSM_BLOCK), 0,
+                       ctx->stream, d_runs, nb, buckets);
     QG_LAUNCH_CHECK();
-    QG_HIP(hipMemcpyAsync(&local, red + 2 * nred + 1, sizeof(G1Xyzz), hipMemcpyDeviceToHost,
-                          ctx->stream));
-    ctx->sync();
+    // level 1: A = red[0, nred), R = red[nred, 2 nred); level 2: red[2 nred]
+    hipLaunchKernelGGL(k_msm_wsum, dim3(nred, kl), dim3(MSM_BLOCK), 0, ctx->stream, buckets,
+                       (const G1Xyzz*)nullptr, nb, slog1, 8 + slog1, red, red + nred, (size_t)nb,
+                       rstride);
+    QG_LAUNCH_CHECK();
+    const uint32_t t2 = div_up(nred, (size_t)1 << slog2);
+    hipLaunchKernelGGL(k_msm_wsum, dim3(1, kl), dim3(t2 < 64 ? 64 : t2), 0, ctx->stream,
+                       red + nred, red, nred, slog2, 0, red + 2 * nred, (G1Xyzz*)nullptr, rstride,
+                       rstride);
+    QG_LAUNCH_CHECK();
   }
-  if (ctx->world > 1) {
-    // sum of the per-rank partial MSMs (allgather + host EC adds; RCCL cannot add points)
-    G1Xyzz* d_send = ctx->scratch_as<G1Xyzz>("msm_comm_send", 1);
-    G1Xyzz* d_recv = ctx->scratch_as<G1Xyzz>("msm_comm_recv", ctx->world);
-    QG_HIP(hipMemcpyAsync(d_send, &local, sizeof(G1Xyzz), hipMemcpyHostToDevice, ctx->stream));
-    comm_allgather_bytes(ctx, d_send, d_recv, sizeof(G1Xyzz));
-    std::vector<G1Xyzz> all(ctx->world);
-    QG_HIP(hipMemcpyAsync(all.data(), d_recv, sizeof(G1Xyzz) * ctx->world, hipMemcpyDeviceToHost,
-                          ctx->stream));
-    ctx->sync();
-    local = G1Xyzz::infinity();
-    for (int r = 0; r < ctx->world; r++) local = xyzz_add(local, all[r]);
+  hipLaunchKernelGGL(k_msm_export, dim3(1), dim3(1024), 0, ctx->stream, red + 2 * nred, rstride, kl,
+                     d_out);
+  QG_LAUNCH_CHECK();
+  std::vector<G1Xyzz> h(kl);
+  QG_HIP(hipMemcpyAsync(h.data(), d_out, kl * sizeof(G1Xyzz), hipMemcpyDeviceToHost, ctx->stream));
+  ctx->sync();
+  for (uint32_t q = 0; q < kl; q++) out[live[q]] = h[q];
+}
+
+// k MSMs over the same SRS (KZG openings of one proof); results per MSM,
+// summed over the RCCL ranks when a communicator is attached
+std::vector<G1Affine> msm_device_batch(qg_ctx* ctx, const qg_srs* srs,
+                                       const std::vector<const Fr*>& scalars,
+                                       const std::vector<size_t>& ns) {
+  QG_CHECK(scalars.size() == ns.size(), QG_ERR_INVALID, "MSM batch shape");
+  std::vector<MsmRun> runs;
+  for (size_t i = 0; i < scalars.size(); i++)
+    runs.push_back(msm_accumulate_phase(ctx, srs, scalars[i], ns[i], (int)i));
+  std::vector<G1Xyzz> local;
+  msm_reduce_phase(ctx, srs, runs, local);
+  std::vector<G1Affine> res(local.size());
+  for (size_t i = 0; i < local.size(); i++) {
+    G1Xyzz acc = local[i];
+    if (ctx->world > 1) {
+      // sum of the per-rank partial MSMs (allgather + host EC adds; RCCL cannot add points)
+      G1Xyzz* d_send = ctx->scratch_as<G1Xyzz>("msm_comm_send", 1);
+      G1Xyzz* d_recv = ctx->scratch_as<G1Xyzz>("msm_comm_recv", ctx->world);
+      QG_HIP(hipMemcpyAsync(d_send, &acc, sizeof(G1Xyzz), hipMemcpyHostToDevice, ctx->stream));
+      comm_allgather_bytes(ctx, d_send, d_recv, sizeof(G1Xyzz));
+      std::vector<G1Xyzz> all(ctx->world);
+      QG_HIP(hipMemcpyAsync(all.data(), d_recv, sizeof(G1Xyzz) * ctx->world,
+                            hipMemcpyDeviceToHost, ctx->stream));
+      ctx->sync();
+      acc = G1Xyzz::infinity();
+      for (int r = 0; r < ctx->world; r++) acc = xyzz_add(acc, all[r]);
+    }
+    res[i] = xyzz_to_affine(acc);
   }
-  return xyzz_to_affine(local);
+  return res;
+}
+
+G1Affine msm_device(qg_ctx* ctx, const qg_srs* srs, const Fr* d_scalars, size_t n) {
+  return msm_device_batch(ctx, srs, {d_scalars}, {n})[0];
 }
 
 // dependent Fq multiply chains: 8 independent chains per thread, ITER steps
