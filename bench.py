@@ -29,6 +29,11 @@ ROOT = os.path.dirname(os.path.abspath(__file__))
 sys.path.insert(0, os.path.join(ROOT, "quill-zkvm_amd"))
 
 HBM_PEAK_GBPS = 8000.0  # MI355X_MICROARCH.md: HBM3E 8.0 TB/s spec
+# hardware issue bound of the 29-bit Fq multiply: v_mad_u64_u32 lane-ops/s
+# measured on MI355X (profiles/r01_isa_rates.json, every CU issuing) / the 162
+# partial products of one 9 x 9-limb Montgomery product (81 a*b + 81 m*p)
+VMAD_LANE_OPS_PER_S = 3.1186e13
+MADS_PER_FQ_MUL = 162
 LOGUP_BYTES_PER_ROW = 128  # 3 x 32 B table reads + 32 B column write
 MSM_BYTES_PER_SCALAR = 96  # 32 B scalar + 64 B affine base
 MSM_FQMUL_PER_SCALAR = 176  # 16 signed windows x 11 Fq mults
@@ -54,12 +59,14 @@ def parse():
                     help="log2 size of the CPU-baseline MSM sample (a prefix of the workload)")
     ap.add_argument("--no-traffic", action="store_true",
                     help="skip the two rocprofv3 PMC passes that measure HBM traffic")
+    ap.add_argument("--no-scaling-modes", action="store_true",
+                    help="skip the strong-scaling MSM (fixed 2^log-msm total) and weak-scaling "
+                         "sumcheck (2^log-sumcheck per GPU) legs")
     ap.add_argument("--traffic-probe", action="store_true", help=argparse.SUPPRESS)
     return ap.parse_args()
 
 
-SC_KERNELS = ("k_sc_round", "k_sc_finish", "k_sc_tail", "k_sc_local_sum", "k_sc_fold_last",
-              "k_sc_transpose")
+SC_KERNELS = ("k_sc_big", "k_sc_round", "k_sc_persist", "k_sc_finish")
 
 
 def traffic_probe(args):
@@ -89,13 +96,25 @@ def traffic_probe(args):
                             LOGUP_BETA, out, E.Input(2))
         for t in tabs + [out]:
             t.close()
+    if args.log_mle > 0:
+        # ML-PCS commit + open (S-polynomial NTT passes, suffix-Horner, MSMs)
+        from quill_amd import KZG, Transcript
+        n = 1 << args.log_mle
+        kzg = KZG(dev, q.Srs.generate(dev, TAU, n), n - 1)
+        poly = q.DeviceVec(dev, n).fill_random(0x5155494C4C + 4)
+        C = kzg.srs.msm_dev(poly)
+        t = Transcript(b"MLPCS bench")
+        t.append_g1(C)
+        kzg.open_dev(poly, n, [t.draw_field_element() for _ in range(args.log_mle)], t)
+        poly.close()
+        kzg.srs.close()
     dev.close()
 
 
 def measure_traffic(args):
     import pmc_traffic
     probe = ["--log-msm", str(args.log_msm), "--log-sumcheck", str(args.log_sumcheck),
-             "--log-logup", str(args.log_logup)]
+             "--log-logup", str(args.log_logup), "--log-mle", str(args.log_mle)]
     if args.no_sumcheck:
         probe.append("--no-sumcheck")
     try:
@@ -196,7 +215,7 @@ def main():
                    "log_msm": args.log_msm, "parallelism": f"msm-shard-by-base-index x{world}"},
         "roofline": {"bound": "hbm", "kernel": "msm_accumulate", "achieved": achieved,
                      "peak": HBM_PEAK_GBPS, "unit": "GB/s", "frac": achieved / HBM_PEAK_GBPS,
-                     "traffic": _kernel_traffic(traffic, "k_msm_accumulate"),
+                     "traffic": _headline_traffic(traffic),
                      "algorithmic_bytes": MSM_BYTES_PER_SCALAR * n,
                      "note": "MSM is integer-VALU bound (no MFMA form): see compute"},
         "compute": {"fq_mul_per_s_peak_microbench": fq_peak,
@@ -206,7 +225,14 @@ def main():
                     "accumulate_fq_mul_per_s": exec_mults / (acc_ms * 1e-3),
                     "frac": exec_mults / (acc_ms * 1e-3) / fq_peak,
                     "frac_note": "msm_accumulate's executed Fq mults (10 per digit x W digits "
-                                 "per scalar) / microbenchmarked Fq-mul peak"},
+                                 "per scalar) / microbenchmarked Fq-mul peak",
+                    "issue_bound_fq_mul_per_s": VMAD_LANE_OPS_PER_S / MADS_PER_FQ_MUL,
+                    "frac_issue_bound": exec_mults / (acc_ms * 1e-3)
+                    / (VMAD_LANE_OPS_PER_S / MADS_PER_FQ_MUL),
+                    "issue_bound_note": "v_mad_u64_u32 lane-ops/s measured with every CU "
+                                        "issuing (profiles/r01_isa_rates.json) / 162 partial "
+                                        "products per 29-bit Montgomery multiply: a hardware "
+                                        "bound, independent of the microbenchmark"},
         "kernels_ms": kern,
         "setup_s": setup_s,
         "commitment_x_low64": hex(0 if res is None else res[0] & ((1 << 64) - 1)),
@@ -222,6 +248,13 @@ def main():
             tot = sum((traffic[k]["read_bytes_per_launch"] + traffic[k]["write_bytes_per_launch"])
                       * traffic[k]["launches"] for k in SC_KERNELS if k in traffic)
             out["sumcheck"]["roofline"]["traffic"] = tot
+    if not args.no_scaling_modes:
+        out["msm_strong_scaling"] = bench_msm_strong(q, dev, args, barrier_sync, max_over_ranks,
+                                                     rank, world, srs if world == 1 else None,
+                                                     scalars if world == 1 else None)
+        if not args.no_sumcheck:
+            out["sumcheck_weak_scaling"] = bench_sumcheck(q, dev, args, barrier_sync,
+                                                          max_over_ranks, rank, weak=True)
     if args.log_mle > 0:
         out["mle_open"] = bench_mle(q, dev, args, barrier_sync, max_over_ranks, rank, world)
     if args.log_logup > 0:
@@ -243,10 +276,40 @@ def main():
         dist.destroy_process_group()
 
 
-def bench_sumcheck(q, dev, args, barrier_sync, max_over_ranks, rank):
+def bench_msm_strong(q, dev, args, barrier_sync, max_over_ranks, rank, world, srs=None,
+                     scalars=None):
+    """Strong-scaling MSM: ONE commitment to a degree 2^log-msm polynomial split
+    over the ranks (rank r owns bases/scalars [r n/N, (r+1) n/N)); value = n /
+    max-over-ranks time.  At N = 1 it reuses the headline SRS and scalars."""
+    n = 1 << args.log_msm
+    L = n // world
+    own = srs is None
+    if own:
+        srs = q.Srs.generate(dev, TAU, L, offset=rank * L)
+        scalars = q.DeviceVec(dev, L).fill_random(0x5155494C4C + 6 + rank)
+    steps = max(1, min(args.steps, 3))
+    srs.msm_dev(scalars, L)
+    barrier_sync()
+    t0 = time.perf_counter()
+    for _ in range(steps):
+        srs.msm_dev(scalars, L)
+    barrier_sync()
+    dt = max_over_ranks(time.perf_counter() - t0)
+    if own:
+        srs.close()
+        scalars.close()
+    return {"metric": f"G1 MSM scalars/s, one 2^{args.log_msm} commitment split over the GPUs",
+            "value": n * steps / dt, "unit": "scalars/s", "ms_per_step": dt / steps * 1e3,
+            "steps": steps, "scaling": "strong", "per_rank_scalars": L}
+
+
+def bench_sumcheck(q, dev, args, barrier_sync, max_over_ranks, rank, weak=False):
     from quill_amd.hyperplonk import VirtualPolyExpr as E, sumcheck_prove_device
-    nv = args.log_sumcheck
     world = dev.world
+    lw = max(world.bit_length() - 1, 0)
+    # strong: one 2^n prove sharded by the high index bits; weak: 2^n entries per
+    # GPU (a 2^(n + log2 N)-variable prove)
+    nv = args.log_sumcheck + (lw if weak else 0)
     N = (1 << nv) // world  # this rank's block of every table (sharded by the high bits)
     tabs = [q.DeviceVec(dev, N).fill_random(0x5155494C4C + 3 + 7 * i + 100 * rank) for i in range(3)]
     expr = E.Input(0) * E.Input(1) * E.Input(2)
@@ -278,7 +341,9 @@ def bench_sumcheck(q, dev, args, barrier_sync, max_over_ranks, rank):
                          "achieved": per_call_gbps, "peak": HBM_PEAK_GBPS, "unit": "GB/s",
                          "frac": per_call_gbps / HBM_PEAK_GBPS, "traffic": None,
                          "algorithmic_bytes": total_bytes},
-            "parallelism": f"sharded x{world} (strong scaling)" if world > 1 else "single GPU",
+            "parallelism": (f"sharded x{world} ({'weak' if weak else 'strong'} scaling)"
+                            if world > 1 else "single GPU"),
+            "scaling": "weak" if weak else "strong",
             "round_kernels_ms_per_call": rk_ms / max(args.steps, 1),
             "tail_kernel_ms_per_call": tl_ms / max(args.steps, 1)}
 
@@ -494,11 +559,26 @@ def cpu_baseline_logup(args, tabs, out):
             "matches_gpu_column_of_sample": bool(np.array_equal(ref, out.to_numpy(ns)))}
 
 
-def _kernel_traffic(traffic, kernel):
-    """HBM bytes per launch (PMC, corrected) or None"""
-    if not traffic or "error" in traffic or kernel not in traffic:
+def _kernel_traffic(traffic, kernel, grid=None):
+    """HBM bytes per launch (PMC, corrected) or None; with `grid`, of the launches
+    of that shape (kernel@grid work-items) only"""
+    key = kernel if grid is None else f"{kernel}@{grid}"
+    if not traffic or "error" in traffic or key not in traffic:
         return None
-    d = traffic[kernel]
+    d = traffic[key]
+    return d["read_bytes_per_launch"] + d["write_bytes_per_launch"]
+
+
+def _headline_traffic(traffic):
+    """PMC bytes per launch of the headline MSM's accumulate: the probe's FIRST
+    k_msm_accumulate launch shape (the 2^log-msm MSM runs first)"""
+    if not traffic or "error" in traffic:
+        return None
+    shapes = [k for k in traffic if k.startswith("k_msm_accumulate@")]
+    if not shapes:
+        return _kernel_traffic(traffic, "k_msm_accumulate")
+    big = max(shapes, key=lambda k: int(k.split("@")[1]))  # largest grid = 2^log-msm
+    d = traffic[big]
     return d["read_bytes_per_launch"] + d["write_bytes_per_launch"]
 
 
@@ -546,9 +626,17 @@ def cpu_baseline(args, srs, scalars):
     xy, inf = srs.download_raw(0, ns)
     sc = scalars.to_numpy(ns)
     tm, tc, (cxy, cinf) = oc.bench_msm_arrays(xy, inf, sc)
+    nth = oc.usable_cores()
+    tmt, (mxy, minf) = oc.bench_msm_arrays_mt(xy, inf, sc, nth)
     from quill_amd.field import g1_from_abi
     gpu = srs.msm_dev(scalars, ns)
+    all_cores = {"value": ns / tmt, "unit": "scalars/s", "cores": nth, "kind": "port",
+                 "sample": f"same 2^{args.cpu_sample_log} sample, ark-ec's parallel window "
+                           f"split on {nth} threads ({tmt:.2f} s); the reference builds "
+                           "without rayon, so this is an all-cores port",
+                 "seconds": tmt, "matches_gpu_msm_of_sample": g1_from_abi(mxy, minf) == gpu}
     return {"value": ns / tm, "unit": "scalars/s", "cores": 1, "kind": "port",
+            "all_cores": all_cores,
             "sample": f"the first 2^{args.cpu_sample_log} bases and scalars of the timed "
                       f"workload, one msm_unchecked ({tm:.2f} s, single thread like the "
                       f"reference); KZG::commit as written (+ into_affine of every SRS point) "
@@ -559,11 +647,29 @@ def cpu_baseline(args, srs, scalars):
 
 
 def cpu_baseline_sumcheck(args):
+    """Evaluation-form C prover at the bench size (1 thread, a lower bound on the
+    reference), the reference-structured C prover (per-pair DensePolynomials,
+    FFT products, clones: sumcheck.rs:28-114, virtual_polynomial.rs:300-320) on
+    a bounded 2^(n-2) sample with the linear extrapolation to 2^n, and the
+    evaluation form on all usable cores at 2^n."""
     try:
         oc = _oracle_c()
     except Exception as e:
         return {"ms": None, "error": f"oracle C library unavailable: {e}"}
-    return oc.bench_sumcheck_baseline(args.log_sumcheck)
+    out = oc.bench_sumcheck_baseline(args.log_sumcheck)
+    ls = max(args.log_sumcheck - 2, 1)
+    t_ref = oc.bench_sumcheck_ref(ls)
+    out["reference_structured"] = {
+        "ms_sample": t_ref * 1e3, "sample_log_vars": ls,
+        "ms_extrapolated": t_ref * 1e3 * (1 << (args.log_sumcheck - ls)), "cores": 1,
+        "kind": "port",
+        "note": f"the reference's data flow restated in C at 2^{ls} vars; work is linear in "
+                f"2^n, so x{1 << (args.log_sumcheck - ls)} gives the 2^{args.log_sumcheck} "
+                "estimate"}
+    nth = oc.usable_cores()
+    out["all_cores"] = {"ms": oc.bench_sumcheck_mt(args.log_sumcheck, nth) * 1e3, "cores": nth,
+                        "kind": "port", "sample": f"evaluation form, 2^{args.log_sumcheck} vars"}
+    return out
 
 
 if __name__ == "__main__":

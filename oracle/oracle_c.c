@@ -826,3 +826,500 @@ int oc_g1_mul(const uint64_t base_xy[8], uint8_t base_inf, const uint64_t s_mont
   *out_inf = (uint8_t)r.inf;
   return 0;
 }
+
+/* ================================================================ all-cores
+ * Multi-threaded variants for the all-cores CPU baseline:
+ * ark-ec's msm_bigint_wnaf with its `parallel` feature splits the windows
+ * across threads (each window's bucket sum independent, the window combination
+ * serial); the evaluation-form sumcheck splits each round's pairs.  The
+ * reference itself builds without rayon, so these are labelled "all-cores
+ * port", not the reference. */
+#include <pthread.h>
+
+typedef struct {
+  const g1a* bases;
+  const int64_t* dig;
+  size_t n;
+  int c, digits, w0, wstep;
+  g1j* win;
+} msm_task;
+
+static void* msm_window_worker(void* arg) {
+  msm_task* t = (msm_task*)arg;
+  const size_t nbk = (size_t)1 << t->c;
+  g1j* buckets = (g1j*)malloc(sizeof(g1j) * nbk);
+  for (int w = t->w0; w < t->digits; w += t->wstep) {
+    for (size_t b = 0; b < nbk; b++) buckets[b] = j_zero();
+    for (size_t i = 0; i < t->n; i++) {
+      int64_t d = t->dig[i * t->digits + w];
+      if (d > 0) {
+        j_add_affine(&buckets[d - 1], &t->bases[i]);
+      } else if (d < 0) {
+        g1a nb = t->bases[i];
+        if (!nb.inf) nb.y = f_sub(&FQ, (fp){{0, 0, 0, 0}}, nb.y);
+        j_add_affine(&buckets[-d - 1], &nb);
+      }
+    }
+    g1j run = j_zero(), res = j_zero();
+    for (size_t b = nbk; b-- > 0;) {
+      j_add(&run, &buckets[b]);
+      j_add(&res, &run);
+    }
+    t->win[w] = res;
+  }
+  free(buckets);
+  return NULL;
+}
+
+static g1j msm_ark_mt(const g1a* bases, const fp* scalars, size_t n, int nthreads) {
+  const int c = n < 32 ? 3 : (int)ln_without_floats(n) + 2;
+  const int num_bits = 254;
+  const int digits = (num_bits + c - 1) / c;
+  int64_t* dig = (int64_t*)malloc(sizeof(int64_t) * digits * (n ? n : 1));
+  for (size_t i = 0; i < n; i++) {
+    fp cs = f_from_mont(&FR, scalars[i]);
+    make_digits(cs.v, c, num_bits, dig + i * digits);
+  }
+  g1j* win = (g1j*)malloc(sizeof(g1j) * digits);
+  if (nthreads > digits) nthreads = digits;
+  if (nthreads < 1) nthreads = 1;
+  pthread_t* th = (pthread_t*)malloc(sizeof(pthread_t) * nthreads);
+  msm_task* tk = (msm_task*)malloc(sizeof(msm_task) * nthreads);
+  for (int t = 0; t < nthreads; t++) {
+    tk[t] = (msm_task){bases, dig, n, c, digits, t, nthreads, win};
+    pthread_create(&th[t], NULL, msm_window_worker, &tk[t]);
+  }
+  for (int t = 0; t < nthreads; t++) pthread_join(th[t], NULL);
+  g1j total = j_zero();
+  for (int w = digits - 1; w >= 1; w--) {
+    j_add(&total, &win[w]);
+    for (int k = 0; k < c; k++) j_double(&total);
+  }
+  j_add(&total, &win[0]);
+  free(dig);
+  free(win);
+  free(th);
+  free(tk);
+  return total;
+}
+
+/* all-cores MSM on caller arrays (same inputs as oc_bench_msm_arrays) */
+int oc_bench_msm_arrays_mt(const uint64_t* bases_xy, const uint8_t* inf, const uint64_t* scalars,
+                           size_t n, int nthreads, double* t_msm, uint64_t out_xy[8],
+                           uint8_t* out_inf) {
+  g1a* b = (g1a*)malloc(sizeof(g1a) * (n ? n : 1));
+  for (size_t i = 0; i < n; i++) {
+    memcpy(b[i].x.v, bases_xy + 8 * i, 32);
+    memcpy(b[i].y.v, bases_xy + 8 * i + 4, 32);
+    b[i].inf = inf ? inf[i] : 0;
+  }
+  double a = now_s();
+  g1j r = msm_ark_mt(b, (const fp*)scalars, n, nthreads);
+  *t_msm = now_s() - a;
+  g1a ra = j_to_affine(&r);
+  memcpy(out_xy, ra.x.v, 32);
+  memcpy(out_xy + 4, ra.y.v, 32);
+  *out_inf = (uint8_t)ra.inf;
+  free(b);
+  return 0;
+}
+
+/* ------------------------------------------------ all-cores sumcheck (eval form) */
+typedef struct {
+  fp* g;        /* k tables of stride N (current round) */
+  fp* fold_out; /* k tables of stride N (next round) */
+  size_t N, p0, p1;
+  int k, np;
+  fp sums[16];
+  fp r;
+  int phase; /* 0: evaluate, 1: fold */
+} sc_task;
+
+static void* sc_worker(void* arg) {
+  sc_task* t = (sc_task*)arg;
+  if (t->phase == 0) {
+    for (int u = 0; u < t->np; u++) t->sums[u] = (fp){{0, 0, 0, 0}};
+    for (size_t p = t->p0; p < t->p1; p++) {
+      fp lo[8], df[8];
+      for (int i = 0; i < t->k; i++) {
+        lo[i] = t->g[i * t->N + 2 * p];
+        df[i] = f_sub(&FR, t->g[i * t->N + 2 * p + 1], lo[i]);
+      }
+      for (int u = 0; u < t->np; u++) {
+        if (u) for (int i = 0; i < t->k; i++) lo[i] = f_add(&FR, lo[i], df[i]);
+        fp prod = lo[0];
+        for (int i = 1; i < t->k; i++) prod = f_mul(&FR, prod, lo[i]);
+        t->sums[u] = f_add(&FR, t->sums[u], prod);
+      }
+    }
+  } else {
+    /* out of place (ping-pong): thread slices would race in place */
+    for (int i = 0; i < t->k; i++)
+      for (size_t p = t->p0; p < t->p1; p++) {
+        fp a = t->g[i * t->N + 2 * p], b = t->g[i * t->N + 2 * p + 1];
+        t->fold_out[i * t->N + p] = f_add(&FR, a, f_mul(&FR, t->r, f_sub(&FR, b, a)));
+      }
+  }
+  return NULL;
+}
+
+/* inverse Vandermonde on the nodes 0..np-1 (as in oc_sumcheck_prod) */
+static void sc_vandermonde(int np, fp V[16][16]) {
+  for (int j = 0; j < np; j++) {
+    fp poly[17] = {{{0}}};
+    poly[0] = f_one(&FR);
+    int deg = 0;
+    fp den = f_one(&FR);
+    for (int mm = 0; mm < np; mm++) {
+      if (mm == j) continue;
+      fp nm = {{(uint64_t)mm, 0, 0, 0}};
+      nm = f_sub(&FR, (fp){{0, 0, 0, 0}}, f_to_mont(&FR, nm));
+      fp np2[17] = {{{0}}};
+      for (int t = 0; t <= deg; t++) {
+        np2[t] = f_add(&FR, np2[t], f_mul(&FR, poly[t], nm));
+        np2[t + 1] = f_add(&FR, np2[t + 1], poly[t]);
+      }
+      deg++;
+      memcpy(poly, np2, sizeof poly);
+      int64_t d = j - mm;
+      fp dd = {{(uint64_t)(d < 0 ? -d : d), 0, 0, 0}};
+      dd = f_to_mont(&FR, dd);
+      if (d < 0) dd = f_sub(&FR, (fp){{0, 0, 0, 0}}, dd);
+      den = f_mul(&FR, den, dd);
+    }
+    fp di = f_inv(&FR, den);
+    for (int t = 0; t < np; t++) V[t][j] = f_mul(&FR, poly[t], di);
+  }
+}
+
+/* round message from the np evaluations: coefficients, trim, absorb, draw r */
+static fp sc_round_message(int np, fp V[16][16], const fp* sums, uint8_t state[32],
+                           uint64_t* coeff_row, uint32_t* len_out) {
+  fp co[16];
+  uint32_t len = 0;
+  for (int t = 0; t < np; t++) {
+    fp acc = {{0, 0, 0, 0}};
+    for (int u = 0; u < np; u++) acc = f_add(&FR, acc, f_mul(&FR, V[t][u], sums[u]));
+    co[t] = acc;
+    if (!f_is_zero(acc)) len = t + 1;
+  }
+  uint8_t msg[8 + 16 * 32];
+  for (int i = 0; i < 8; i++) msg[i] = (uint8_t)((uint64_t)len >> (8 * i));
+  for (uint32_t t = 0; t < len; t++) fr_bytes(co[t], msg + 8 + 32 * t);
+  tr_append(state, msg, 8 + 32 * len);
+  fp r = tr_draw_fr(state);
+  for (int t = 0; t < np; t++)
+    memcpy(coeff_row + 4 * t, (t < (int)len ? co[t] : (fp){{0, 0, 0, 0}}).v, 32);
+  *len_out = len;
+  return r;
+}
+
+/* evaluation-form sumcheck for h = prod of k tables on nthreads threads; same
+ * transcript and outputs as oc_sumcheck_prod */
+int oc_sumcheck_prod_mt(int nvars, int k, const uint64_t* tables, const uint64_t claimed[4],
+                        uint8_t state[32], uint64_t* coeffs, uint32_t* lens, uint64_t* point,
+                        uint64_t evaluation[4], int nthreads) {
+  size_t N = (size_t)1 << nvars;
+  fp* g = (fp*)malloc(sizeof(fp) * N * k);
+  fp* g2 = (fp*)malloc(sizeof(fp) * N * k);
+  memcpy(g, tables, sizeof(fp) * N * k);
+  uint8_t m8[8];
+  for (int i = 0; i < 8; i++) m8[i] = (uint8_t)((uint64_t)nvars >> (8 * i));
+  tr_append(state, m8, 8);
+  uint8_t b32[32];
+  fp cs;
+  memcpy(cs.v, claimed, 32);
+  fr_bytes(cs, b32);
+  tr_append(state, b32, 32);
+  const int np = k + 1;
+  fp V[16][16];
+  sc_vandermonde(np, V);
+  if (nthreads < 1) nthreads = 1;
+  pthread_t* th = (pthread_t*)malloc(sizeof(pthread_t) * nthreads);
+  sc_task* tk = (sc_task*)malloc(sizeof(sc_task) * nthreads);
+  size_t half = N;
+  for (int j = 0; j < nvars; j++) {
+    half >>= 1;
+    const int nt = half < (size_t)nthreads * 64 ? 1 : nthreads;
+    for (int t = 0; t < nt; t++) {
+      tk[t] = (sc_task){g, g2, N, half * t / nt, half * (t + 1) / nt, k, np, {{{0}}}, {{0}}, 0};
+      pthread_create(&th[t], NULL, sc_worker, &tk[t]);
+    }
+    for (int t = 0; t < nt; t++) pthread_join(th[t], NULL);
+    fp sums[16];
+    for (int u = 0; u < np; u++) {
+      sums[u] = (fp){{0, 0, 0, 0}};
+      for (int t = 0; t < nt; t++) sums[u] = f_add(&FR, sums[u], tk[t].sums[u]);
+    }
+    fp r = sc_round_message(np, V, sums, state, coeffs + 4 * (size_t)j * np, &lens[j]);
+    memcpy(point + 4 * j, r.v, 32);
+    for (int t = 0; t < nt; t++) {
+      tk[t].phase = 1;
+      tk[t].r = r;
+      pthread_create(&th[t], NULL, sc_worker, &tk[t]);
+    }
+    for (int t = 0; t < nt; t++) pthread_join(th[t], NULL);
+    fp* tmp = g;
+    g = g2;
+    g2 = tmp;
+  }
+  fp e = g[0];
+  for (int i = 1; i < k; i++) e = f_mul(&FR, e, g[i * N]);
+  memcpy(evaluation, e.v, 32);
+  free(g);
+  free(g2);
+  free(th);
+  free(tk);
+  return 0;
+}
+
+/* ======================================================= reference structure
+ * The reference's prover data flow (sumcheck.rs:28-114) restated with its
+ * costs: every store table cloned (:44-49); per round a Vec<Vec<Dense-
+ * Polynomial>> of 2^i x k heap polynomials lo + X (hi - lo) (:52-63); per pair
+ * evaluate_poly's recursive expression walk (virtual_polynomial.rs:300-320):
+ * Input clones its polynomial, Mul is ark-poly's &a * &b — a
+ * GeneralEvaluationDomain of the product length (its generator by powering
+ * the 2^28 root, size_inv by a field inversion), FFT of both operands,
+ * pointwise product, IFFT, trim — and the per-pair results are summed with
+ * DensePolynomial + (a fresh trimmed vector per addition); the fold evaluates
+ * every pair polynomial at r (poly.evaluate, :81-90).  For h = g0 g1 ... (a
+ * left-deep Mul tree).  Same transcript and outputs as oc_sumcheck_prod. */
+typedef struct { fp* c; int n; } dpoly;
+
+static void dp_trim(dpoly* a) {
+  while (a->n > 0 && f_is_zero(a->c[a->n - 1])) a->n--;
+}
+static dpoly dp_new(int n) {
+  dpoly r = {(fp*)calloc(n ? n : 1, sizeof(fp)), n};
+  return r;
+}
+static dpoly dp_clone(const dpoly* a) {
+  dpoly r = dp_new(a->n);
+  memcpy(r.c, a->c, sizeof(fp) * a->n);
+  return r;
+}
+static void dp_free(dpoly* a) {
+  free(a->c);
+  a->c = NULL;
+  a->n = 0;
+}
+
+/* radix-2 domain of size 2^lg: generator = (2^28-th root)^(2^(28 - lg)), its
+ * inverse and size_inv by inversions (ark-poly Radix2EvaluationDomain::new) */
+typedef struct { int lg; fp g, gi, size_inv; } dom;
+static fp fr_root28(void) {
+  /* 5^((r - 1) / 2^28) (the two-adic root of ark-bn254 Fr), cached */
+  static int done = 0;
+  static fp w;
+  if (!done) {
+    uint64_t e[4];
+    memcpy(e, FR.p, 32);
+    e[0] -= 1;
+    for (int k = 0; k < 28; k++)
+      for (int i = 0; i < 4; i++) e[i] = (e[i] >> 1) | (i < 3 ? (e[i + 1] << 63) : 0);
+    fp five = f_to_mont(&FR, (fp){{5, 0, 0, 0}});
+    w = f_one(&FR);
+    for (int i = 3; i >= 0; i--)
+      for (int b = 63; b >= 0; b--) {
+        w = f_mul(&FR, w, w);
+        if ((e[i] >> b) & 1) w = f_mul(&FR, w, five);
+      }
+    done = 1;
+  }
+  return w;
+}
+static dom dom_new(int n) {
+  dom d;
+  d.lg = 0;
+  while ((1 << d.lg) < n) d.lg++;
+  fp g = fr_root28();
+  for (int i = d.lg; i < 28; i++) g = f_mul(&FR, g, g);
+  d.g = g;
+  d.gi = f_inv(&FR, g);
+  d.size_inv = f_inv(&FR, f_to_mont(&FR, (fp){{(uint64_t)1 << d.lg, 0, 0, 0}}));
+  return d;
+}
+static void fft_inplace(fp* a, int lg, fp w) {
+  const int n = 1 << lg;
+  for (int i = 1, j = 0; i < n; i++) {
+    int bit = n >> 1;
+    for (; j & bit; bit >>= 1) j ^= bit;
+    j ^= bit;
+    if (i < j) {
+      fp t = a[i];
+      a[i] = a[j];
+      a[j] = t;
+    }
+  }
+  for (int len = 2; len <= n; len <<= 1) {
+    fp wl = w;
+    for (int k = len; k < n; k <<= 1) wl = f_mul(&FR, wl, wl);
+    for (int i = 0; i < n; i += len) {
+      fp x = f_one(&FR);
+      for (int j = 0; j < len / 2; j++) {
+        fp u = a[i + j], v = f_mul(&FR, a[i + j + len / 2], x);
+        a[i + j] = f_add(&FR, u, v);
+        a[i + j + len / 2] = f_sub(&FR, u, v);
+        x = f_mul(&FR, x, wl);
+      }
+    }
+  }
+}
+/* ark-poly &a * &b (both nonzero) */
+static dpoly dp_mul(const dpoly* a, const dpoly* b) {
+  if (a->n == 0 || b->n == 0) return dp_new(0);
+  dom d = dom_new(a->n + b->n - 1);
+  const int n = 1 << d.lg;
+  fp* x = (fp*)calloc(n, sizeof(fp));
+  fp* y = (fp*)calloc(n, sizeof(fp));
+  memcpy(x, a->c, sizeof(fp) * a->n);
+  memcpy(y, b->c, sizeof(fp) * b->n);
+  fft_inplace(x, d.lg, d.g);
+  fft_inplace(y, d.lg, d.g);
+  for (int i = 0; i < n; i++) x[i] = f_mul(&FR, x[i], y[i]);
+  fft_inplace(x, d.lg, d.gi);
+  dpoly r = dp_new(n);
+  for (int i = 0; i < n; i++) r.c[i] = f_mul(&FR, x[i], d.size_inv);
+  free(x);
+  free(y);
+  dp_trim(&r);
+  return r;
+}
+static dpoly dp_add(const dpoly* a, const dpoly* b) {
+  const int n = a->n > b->n ? a->n : b->n;
+  dpoly r = dp_new(n);
+  for (int i = 0; i < n; i++) {
+    fp u = i < a->n ? a->c[i] : (fp){{0, 0, 0, 0}};
+    fp v = i < b->n ? b->c[i] : (fp){{0, 0, 0, 0}};
+    r.c[i] = f_add(&FR, u, v);
+  }
+  dp_trim(&r);
+  return r;
+}
+
+int oc_sumcheck_ref_prod(int nvars, int k, const uint64_t* tables, const uint64_t claimed[4],
+                         uint8_t state[32], uint64_t* coeffs, uint32_t* lens, uint64_t* point,
+                         uint64_t evaluation[4]) {
+  size_t N = (size_t)1 << nvars;
+  /* gs_local: a clone of every table */
+  fp** gs = (fp**)malloc(sizeof(fp*) * k);
+  for (int i = 0; i < k; i++) {
+    gs[i] = (fp*)malloc(sizeof(fp) * N);
+    memcpy(gs[i], tables + 4 * N * i, sizeof(fp) * N);
+  }
+  uint8_t m8[8];
+  for (int i = 0; i < 8; i++) m8[i] = (uint8_t)((uint64_t)nvars >> (8 * i));
+  tr_append(state, m8, 8);
+  uint8_t b32[32];
+  fp cs;
+  memcpy(cs.v, claimed, 32);
+  fr_bytes(cs, b32);
+  tr_append(state, b32, 32);
+  const int np = k + 1;
+  for (int j = 0; j < nvars; j++) {
+    const size_t half = N >> (j + 1);
+    /* r_polys: 2^i x k polynomials low + X (high - low) */
+    dpoly* rp = (dpoly*)malloc(sizeof(dpoly) * half * k);
+    for (size_t p = 0; p < half; p++)
+      for (int i = 0; i < k; i++) {
+        dpoly q = dp_new(2);
+        q.c[0] = gs[i][2 * p];
+        q.c[1] = f_sub(&FR, gs[i][2 * p + 1], q.c[0]);
+        dp_trim(&q); /* DensePolynomial::from_coefficients_vec trims */
+        rp[p * k + i] = q;
+      }
+    /* next_message = sum over pairs of evaluate_poly (left-deep product) */
+    dpoly msg = dp_new(0);
+    for (size_t p = 0; p < half; p++) {
+      dpoly acc = dp_clone(&rp[p * k]); /* Input(0) clones */
+      for (int i = 1; i < k; i++) {
+        dpoly in = dp_clone(&rp[p * k + i]);
+        dpoly prod = dp_mul(&acc, &in);
+        dp_free(&acc);
+        dp_free(&in);
+        acc = prod;
+      }
+      dpoly sum = dp_add(&msg, &acc);
+      dp_free(&msg);
+      dp_free(&acc);
+      msg = sum;
+    }
+    /* append the DensePolynomial (u64 length + coefficients), draw r */
+    uint8_t* mb = (uint8_t*)malloc(8 + 32 * (size_t)(msg.n ? msg.n : 1));
+    for (int i = 0; i < 8; i++) mb[i] = (uint8_t)((uint64_t)msg.n >> (8 * i));
+    for (int t = 0; t < msg.n; t++) fr_bytes(msg.c[t], mb + 8 + 32 * t);
+    tr_append(state, mb, 8 + 32 * (size_t)msg.n);
+    free(mb);
+    fp r = tr_draw_fr(state);
+    for (int t = 0; t < np; t++)
+      memcpy(coeffs + 4 * ((size_t)j * np + t), (t < msg.n ? msg.c[t] : (fp){{0, 0, 0, 0}}).v, 32);
+    lens[j] = (uint32_t)msg.n;
+    memcpy(point + 4 * j, r.v, 32);
+    dp_free(&msg);
+    /* new gs_local: every pair polynomial evaluated at r (Horner) */
+    for (int i = 0; i < k; i++) {
+      fp* ng = (fp*)malloc(sizeof(fp) * (half ? half : 1));
+      for (size_t p = 0; p < half; p++) {
+        const dpoly* q = &rp[p * k + i];
+        fp e = {{0, 0, 0, 0}};
+        for (int t = q->n; t-- > 0;) e = f_add(&FR, f_mul(&FR, e, r), q->c[t]);
+        ng[p] = e;
+      }
+      free(gs[i]);
+      gs[i] = ng;
+    }
+    for (size_t p = 0; p < half * k; p++) dp_free(&rp[p]);
+    free(rp);
+  }
+  fp e = gs[0][0];
+  for (int i = 1; i < k; i++) e = f_mul(&FR, e, gs[i][0]);
+  memcpy(evaluation, e.v, 32);
+  for (int i = 0; i < k; i++) free(gs[i]);
+  free(gs);
+  return 0;
+}
+
+/* timed baselines on 2^log_n, k = 3 random tables (same generator as
+ * oc_bench_sumcheck): reference-structured single thread, eval form all cores */
+int oc_bench_sumcheck_ref(int log_n, uint64_t seed, double* seconds) {
+  size_t N = (size_t)1 << log_n;
+  sm_state = seed;
+  fp* t = (fp*)malloc(sizeof(fp) * N * 3);
+  for (size_t i = 0; i < 3 * N; i++) t[i] = rand_fr();
+  uint8_t st[32] = {0};
+  uint64_t cl[4] = {0, 0, 0, 0};
+  uint64_t* co = (uint64_t*)malloc(sizeof(uint64_t) * 4 * 4 * log_n);
+  uint32_t* lens = (uint32_t*)malloc(sizeof(uint32_t) * log_n);
+  uint64_t* pt = (uint64_t*)malloc(sizeof(uint64_t) * 4 * log_n);
+  uint64_t ev[4];
+  double a = now_s();
+  oc_sumcheck_ref_prod(log_n, 3, (const uint64_t*)t, cl, st, co, lens, pt, ev);
+  *seconds = now_s() - a;
+  free(t);
+  free(co);
+  free(lens);
+  free(pt);
+  return 0;
+}
+
+int oc_bench_sumcheck_mt(int log_n, uint64_t seed, int nthreads, double* seconds) {
+  size_t N = (size_t)1 << log_n;
+  sm_state = seed;
+  fp* t = (fp*)malloc(sizeof(fp) * N * 3);
+  for (size_t i = 0; i < 3 * N; i++) t[i] = rand_fr();
+  uint8_t st[32] = {0};
+  uint64_t cl[4] = {0, 0, 0, 0};
+  uint64_t* co = (uint64_t*)malloc(sizeof(uint64_t) * 4 * 4 * log_n);
+  uint32_t* lens = (uint32_t*)malloc(sizeof(uint32_t) * log_n);
+  uint64_t* pt = (uint64_t*)malloc(sizeof(uint64_t) * 4 * log_n);
+  uint64_t ev[4];
+  double a = now_s();
+  oc_sumcheck_prod_mt(log_n, 3, (const uint64_t*)t, cl, st, co, lens, pt, ev, nthreads);
+  *seconds = now_s() - a;
+  free(t);
+  free(co);
+  free(lens);
+  free(pt);
+  return 0;
+}

@@ -41,6 +41,15 @@ def lib():
         L.oc_fr_mle_eval.argtypes = [U64P, C.c_int, U64P, U64P]
         L.oc_fr_sum_prod.argtypes = [C.POINTER(U64P), C.c_int, C.c_size_t, U64P]
         L.oc_g1_mul.argtypes = [U64P, C.c_uint8, U64P, U64P, C.POINTER(C.c_uint8)]
+        L.oc_bench_msm_arrays_mt.argtypes = [U64P, C.POINTER(C.c_uint8), U64P, C.c_size_t,
+                                             C.c_int, C.POINTER(C.c_double), U64P,
+                                             C.POINTER(C.c_uint8)]
+        L.oc_sumcheck_prod_mt.argtypes = [C.c_int, C.c_int, U64P, U64P, C.POINTER(C.c_uint8),
+                                          U64P, C.POINTER(C.c_uint32), U64P, U64P, C.c_int]
+        L.oc_sumcheck_ref_prod.argtypes = [C.c_int, C.c_int, U64P, U64P, C.POINTER(C.c_uint8),
+                                           U64P, C.POINTER(C.c_uint32), U64P, U64P]
+        L.oc_bench_sumcheck_ref.argtypes = [C.c_int, C.c_uint64, C.POINTER(C.c_double)]
+        L.oc_bench_sumcheck_mt.argtypes = [C.c_int, C.c_uint64, C.c_int, C.POINTER(C.c_double)]
         _lib = L
     return _lib
 
@@ -78,8 +87,10 @@ def msm(bases, scalars):
     return (_unmont(out[:4], P_MOD), _unmont(out[4:8], P_MOD))
 
 
-def sumcheck_prod(nvars, tables, claimed, state: bytes):
-    """h = prod tables; returns (r_polys, point, evaluation, new_state)."""
+def sumcheck_prod(nvars, tables, claimed, state: bytes, variant="eval", nthreads=4):
+    """h = prod tables; returns (r_polys, point, evaluation, new_state).
+    variant: "eval" (evaluation form, 1 thread), "mt" (evaluation form,
+    nthreads), "ref" (the reference's DensePolynomial / FFT-product structure)."""
     k = len(tables)
     N = 1 << nvars
     t = (C.c_uint64 * (4 * N * k))()
@@ -93,7 +104,12 @@ def sumcheck_prod(nvars, tables, claimed, state: bytes):
     pt = (C.c_uint64 * (4 * nvars))()
     ev = (C.c_uint64 * 4)()
     cl = (C.c_uint64 * 4)(*_mont(claimed, R_MOD))
-    lib().oc_sumcheck_prod(nvars, k, t, cl, st, co, lens, pt, ev)
+    if variant == "mt":
+        lib().oc_sumcheck_prod_mt(nvars, k, t, cl, st, co, lens, pt, ev, nthreads)
+    elif variant == "ref":
+        lib().oc_sumcheck_ref_prod(nvars, k, t, cl, st, co, lens, pt, ev)
+    else:
+        lib().oc_sumcheck_prod(nvars, k, t, cl, st, co, lens, pt, ev)
     r_polys = [[_unmont(co[4 * (j * (k + 1) + i):4 * (j * (k + 1) + i) + 4], R_MOD)
                 for i in range(lens[j])] for j in range(nvars)]
     point = [_unmont(pt[4 * j:4 * j + 4], R_MOD) for j in range(nvars)]
@@ -143,6 +159,46 @@ def bench_msm_arrays(xy, inf, scalars):
                               sc.ctypes.data_as(P64), C.c_size_t(n), C.byref(tm), C.byref(tc),
                               out, C.byref(oinf))
     return tm.value, tc.value, (list(out), oinf.value)
+
+
+def usable_cores(cap: int = 16) -> int:
+    """CPU threads for the all-cores baselines: this process's affinity, capped
+    (the GPU box's share for one GPU is 16 threads)"""
+    try:
+        n = len(os.sched_getaffinity(0))
+    except (AttributeError, OSError):
+        n = os.cpu_count() or 1
+    return max(1, min(cap, n))
+
+
+def bench_msm_arrays_mt(xy, inf, scalars, nthreads):
+    """ark-ec's parallel window split on nthreads threads, same arrays and
+    output as bench_msm_arrays.  Returns (seconds, (xy limbs, inf))."""
+    import numpy as np
+    n = len(inf)
+    xy = np.ascontiguousarray(xy, dtype=np.uint64)
+    inf = np.ascontiguousarray(inf, dtype=np.uint8)
+    sc = np.ascontiguousarray(scalars, dtype=np.uint64)
+    tm = C.c_double()
+    out = (C.c_uint64 * 8)()
+    oinf = C.c_uint8()
+    P64, P8 = C.POINTER(C.c_uint64), C.POINTER(C.c_uint8)
+    lib().oc_bench_msm_arrays_mt(xy.ctypes.data_as(P64), inf.ctypes.data_as(P8),
+                                 sc.ctypes.data_as(P64), C.c_size_t(n), nthreads, C.byref(tm),
+                                 out, C.byref(oinf))
+    return tm.value, (list(out), oinf.value)
+
+
+def bench_sumcheck_ref(log_n: int, seed: int = 0x5155494C4C):
+    s = C.c_double()
+    lib().oc_bench_sumcheck_ref(log_n, seed, C.byref(s))
+    return s.value
+
+
+def bench_sumcheck_mt(log_n: int, nthreads: int, seed: int = 0x5155494C4C):
+    s = C.c_double()
+    lib().oc_bench_sumcheck_mt(log_n, seed, nthreads, C.byref(s))
+    return s.value
 
 
 def bench_sumcheck_baseline(log_n: int = 16, seed: int = 0x5155494C4C):

@@ -6,7 +6,9 @@ TCC block cannot hold FETCH_SIZE and WRITE_SIZE in one pass), each a child
 started before the parent touches the GPU.  Corrections (same guide, "HBM"):
 FETCH_SIZE / WRITE_SIZE are reported in KiB; on gfx950 FETCH_SIZE counts half
 the bytes of wide streaming reads, so it is doubled; WRITE_SIZE is taken as is.
-Per-launch bytes are returned for the dominant kernels."""
+Per-launch bytes are returned for every kernel of the probe, with the achieved
+HBM GB/s against the 8 TB/s peak from a third, kernel-trace-only pass (clean
+per-launch durations)."""
 from __future__ import annotations
 
 import csv
@@ -36,6 +38,35 @@ def _short(name):
     return n.split("::")[-1].split("<")[0]
 
 
+def kernel_durations(probe_args, timeout=300):
+    """{kernel: (launches, average duration in us)} from a kernel-trace-only pass
+    of the same probe (no counters: clean per-launch durations)"""
+    exe = shutil.which("rocprofv3")
+    if exe is None:
+        raise RuntimeError("rocprofv3 not found")
+    outdir = tempfile.mkdtemp(prefix="qg_kt_")
+    try:
+        cmd = [exe, "--kernel-trace", "-d", outdir, "-o", "kt", "-f", "csv", "--", sys.executable,
+               os.path.join(ROOT, "bench.py"), "--traffic-probe"] + probe_args
+        p = subprocess.run(cmd, stdout=subprocess.PIPE, stderr=subprocess.STDOUT, timeout=timeout)
+        if p.returncode != 0:
+            raise RuntimeError(f"rocprofv3 --kernel-trace exited {p.returncode}: "
+                               + p.stdout.decode(errors="replace")[-800:])
+        acc = {}
+        for f in glob.glob(os.path.join(outdir, "**", "*kernel_trace.csv"), recursive=True):
+            with open(f) as fh:
+                for r in csv.DictReader(fh):
+                    k = _short(r["Kernel_Name"])
+                    d = (int(r["End_Timestamp"]) - int(r["Start_Timestamp"])) / 1e3
+                    for key in (k, f"{k}@{r['Grid_Size_X']}"):
+                        a = acc.setdefault(key, [0, 0.0])
+                        a[0] += 1
+                        a[1] += d
+        return {k: (n, t / n) for k, (n, t) in acc.items()}
+    finally:
+        shutil.rmtree(outdir, ignore_errors=True)
+
+
 def run_pass(counter, probe_args, timeout=300):
     """one rocprofv3 pass; `counter` is one name or a list that fits one pass
     (MI355X_MICROARCH.md "rocprofv3 PMC slots": <= 8 SQ, 4 TCC, 2 GRBM)"""
@@ -57,8 +88,9 @@ def run_pass(counter, probe_args, timeout=300):
         if not rows:
             raise RuntimeError(f"no counter rows for {counters}")
         if isinstance(counter, str):
-            return [(int(r["Dispatch_Id"]), _short(r["Kernel_Name"]), float(r["Counter_Value"]))
-                    for r in rows if r["Counter_Name"] == counter]
+            # (dispatch, kernel, value, grid work-items)
+            return [(int(r["Dispatch_Id"]), _short(r["Kernel_Name"]), float(r["Counter_Value"]),
+                     int(r.get("Grid_Size") or 0)) for r in rows if r["Counter_Name"] == counter]
         return [(int(r["Dispatch_Id"]), _short(r["Kernel_Name"]), r["Counter_Name"],
                  float(r["Counter_Value"])) for r in rows]
     finally:
@@ -89,17 +121,37 @@ def collect(probe_args, timeout=300):
     fetch = run_pass("FETCH_SIZE", probe_args, timeout)
     write = run_pass("WRITE_SIZE", probe_args, timeout)
     out = {}
+    # per kernel, and per kernel@grid (one launch shape = one problem size)
     for rows, key, fac in ((fetch, "read_bytes", FETCH_FACTOR), (write, "write_bytes", WRITE_FACTOR)):
-        for _, k, v in rows:
-            d = out.setdefault(k, {"launches": 0, "read_bytes": 0.0, "write_bytes": 0.0})
-            d[key] += v * fac
+        for _, k, v, g in rows:
+            for kk in (k, f"{k}@{g}"):
+                d = out.setdefault(kk, {"launches": 0, "read_bytes": 0.0, "write_bytes": 0.0})
+                d[key] += v * fac
     for k, d in out.items():
-        d["launches"] = sum(1 for _, kk, _ in fetch if kk == k)
+        d["launches"] = sum(1 for _, kk, _, g in fetch if kk == k or f"{kk}@{g}" == k)
     for d in out.values():
+        if "read_bytes" not in d:
+            continue
         n = max(d["launches"], 1)
         d["read_bytes_per_launch"] = d.pop("read_bytes") / n
         d["write_bytes_per_launch"] = d.pop("write_bytes") / n
+    # achieved HBM GB/s per kernel: PMC bytes per launch / clean average duration
+    try:
+        dur = kernel_durations(probe_args, timeout)
+    except Exception as e:  # reported, never substituted
+        dur = {}
+        out["_duration_error"] = {"error": str(e)[-300:]}
+    for k, d in out.items():
+        if k in dur and "read_bytes_per_launch" in d:
+            us = dur[k][1]
+            gbps = (d["read_bytes_per_launch"] + d["write_bytes_per_launch"]) / (us * 1e-6) / 1e9
+            d["avg_us"] = us
+            d["hbm_gbps"] = gbps
+            d["frac_hbm_peak"] = gbps / HBM_PEAK_GBPS
     return out
+
+
+HBM_PEAK_GBPS = 8000.0  # MI355X_MICROARCH.md: HBM3E 8.0 TB/s
 
 
 if __name__ == "__main__":
