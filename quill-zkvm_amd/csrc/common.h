@@ -214,6 +214,10 @@ Fr fr_import(const uint64_t v[4]);
 void fr_export(const Fr& a, uint64_t v[4]);
 // eq(bin(i), z) table on the device (sumcheck.hip)
 void eq_table_device(qg_ctx* ctx, const Fr* d_z, uint32_t nvars, Fr* d_out);
+// h(x) per row by the generic expression interpreter (sumcheck.hip)
+void expr_table_device(qg_ctx* ctx, size_t n, uint32_t ntables, const std::vector<const Fr*>& tabs,
+                       const qg_expr_op* prog, size_t prog_len, const uint64_t* consts,
+                       size_t nconsts, Fr* d_out);
 // RCCL helpers (comm.hip); no-ops when world == 1
 void comm_allgather_bytes(qg_ctx* ctx, const void* d_send, void* d_recv, size_t bytes);
 void comm_release(qg_ctx* ctx);

@@ -438,14 +438,30 @@ static Fr logup_run(qg_ctx* ctx, uint32_t nvars, uint32_t ntables, const std::ve
   memset(&img, 0, sizeof(img));
   std::vector<uint32_t> used;
   uint32_t nfac = 0;
-  const SopProgram sh = compile_program(hp, hl, hc, hn, ntables);
-  lg_compile(img, 0, sh, fr_import(beta), true, 261, used, nfac);
-  if (mp && ml) {
-    const SopProgram sm = compile_program(mp, ml, mc, mn, ntables);
-    lg_compile(img, 1, sm, Fr::zero(), false, 256, used, nfac);
-  } else {
-    SopProgram one;
-    lg_compile(img, 1, one, Fr::one(), true, 256, used, nfac);
+  try {
+    const SopProgram sh = compile_program(hp, hl, hc, hn, ntables);
+    lg_compile(img, 0, sh, fr_import(beta), true, 261, used, nfac);
+    if (mp && ml) {
+      const SopProgram sm = compile_program(mp, ml, mc, mn, ntables);
+      lg_compile(img, 1, sm, Fr::zero(), false, 256, used, nfac);
+    } else {
+      SopProgram one;
+      lg_compile(img, 1, one, Fr::one(), true, 256, used, nfac);
+    }
+  } catch (const Error& e) {
+    if (e.code != QG_ERR_UNSUPPORTED) throw;
+    // outside the compiled envelope (more than 128 monomials, 512 factors or
+    // 64 tables): materialise h (and m) with the generic interpreter, then run
+    // the column over those tables with h = Input(0), m = Input(1)
+    const bool has_m = mp && ml;
+    Fr* ev = ctx->scratch_as<Fr>("lg_gen_tabs", n * (has_m ? 2 : 1));
+    expr_table_device(ctx, n, ntables, tabs, hp, hl, hc, hn, ev);
+    if (has_m) expr_table_device(ctx, n, ntables, tabs, mp, ml, mc, mn, ev + n);
+    const qg_expr_op h0[1] = {{QG_OP_INPUT, 0}}, m1[1] = {{QG_OP_INPUT, 1}};
+    std::vector<const Fr*> t2{ev};
+    if (has_m) t2.push_back(ev + n);
+    return logup_run(ctx, nvars, (uint32_t)t2.size(), t2, h0, 1, nullptr, 0, has_m ? m1 : nullptr,
+                     has_m ? 1 : 0, nullptr, 0, beta, d_out);
   }
   for (size_t s = 0; s < used.size(); s++) img.tab[s] = tabs[used[s]];
 
@@ -598,14 +614,37 @@ int qg_expr_first_nonzero_dev(qg_ctx* ctx, uint32_t nvars, uint32_t ntables,
     memset(&img, 0, sizeof(img));
     std::vector<uint32_t> used;
     uint32_t nfac = 0;
-    const SopProgram sp = compile_program(prog, len, consts, nconsts, ntables);
-    if (sp.mono_len.empty()) return;  // identically zero
-    // scale 256 + 5f: values come out in arkworks form (x 2^256); zero test only
-    lg_compile(img, 0, sp, Fr::zero(), false, 256, used, nfac);
-    for (size_t s = 0; s < used.size(); s++) {
-      QG_CHECK(tables[used[s]] && tables[used[s]]->n >= n, QG_ERR_INVALID,
-               "table buffer missing or too short");
-      img.tab[s] = tables[used[s]]->d;
+    bool generic = false;
+    try {
+      const SopProgram sp = compile_program(prog, len, consts, nconsts, ntables);
+      if (sp.mono_len.empty()) return;  // identically zero
+      // scale 256 + 5f: values come out in arkworks form (x 2^256); zero test only
+      lg_compile(img, 0, sp, Fr::zero(), false, 256, used, nfac);
+    } catch (const Error& e) {
+      if (e.code != QG_ERR_UNSUPPORTED) throw;
+      generic = true;
+    }
+    if (generic) {
+      // h(x) materialised by the generic interpreter, then tested as Input(0)
+      std::vector<const Fr*> tabs(ntables, nullptr);
+      for (uint32_t i = 0; i < ntables; i++) {
+        QG_CHECK(tables[i] && tables[i]->n >= n, QG_ERR_INVALID, "table buffer missing or too short");
+        tabs[i] = tables[i]->d;
+      }
+      Fr* ev = ctx->scratch_as<Fr>("fnz_gen_tab", n);
+      expr_table_device(ctx, n, ntables, tabs, prog, len, consts, nconsts, ev);
+      memset(&img, 0, sizeof(img));
+      used.clear();
+      nfac = 0;
+      const qg_expr_op h0[1] = {{QG_OP_INPUT, 0}};
+      lg_compile(img, 0, compile_program(h0, 1, nullptr, 0, 1), Fr::zero(), false, 256, used, nfac);
+      img.tab[0] = ev;
+    } else {
+      for (size_t s = 0; s < used.size(); s++) {
+        QG_CHECK(tables[used[s]] && tables[used[s]]->n >= n, QG_ERR_INVALID,
+                 "table buffer missing or too short");
+        img.tab[s] = tables[used[s]]->d;
+      }
     }
     uint8_t* io = ctx->scratch_as<uint8_t>("lg_io", sizeof(LgDev) + 64);
     LgDev* d_img = reinterpret_cast<LgDev*>(io);

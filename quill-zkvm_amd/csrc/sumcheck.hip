@@ -983,6 +983,110 @@ __global__ void __launch_bounds__(TAIL_BLOCK)
   if (pending && tid >= 64 && tid < 128) b3_hash_quad(pend, 80, ro.st->state, 8);
 }
 
+// ---------------------------------------------------------------------------
+// Generic expressions: everything the compiled fast path does not take (more
+// than 8 tables, degree above 15, a monomial expansion beyond 256 / 1024
+// terms, or one that does not expand at all).  The postfix program itself is
+// interpreted per (pair, point) — the reference's evaluate_expr_poly tree walk
+// (virtual_polynomial.rs:300-320) on point values instead of polynomials —
+// with every value in the R = 2^261 domain (inputs converted on load), so
+// Add / Mul need no scale bookkeeping.  Per round: a fold kernel (all slots,
+// r_{j-1}), the evaluation kernel (per-block per-point partial rows), a
+// one-block row sum; the transcript step runs on the host (one round trip
+// per round: this path is for coverage, the fast path stays on the device).
+// ---------------------------------------------------------------------------
+static constexpr int GEN_NPMAX = 32;  // points per round (syntactic degree <= 31)
+static constexpr int GEN_STACK = 32;  // interpreter stack (postfix depth)
+
+struct GenOp {
+  uint32_t op, arg;  // QG_OP_*; INPUT: used-slot index; CONST: constant index
+};
+
+// postfix interpreter; load(slot) returns the slot's value in the 2^261 domain
+template <class Load>
+__device__ __forceinline__ R29 gen_interp(const GenOp* __restrict__ ops, uint32_t len,
+                                          const L9* __restrict__ consts29, Load load) {
+  R29 stk[GEN_STACK];
+  uint32_t sp = 0;
+  for (uint32_t i = 0; i < len; i++) {
+    const GenOp o = ops[i];
+    if (o.op == QG_OP_INPUT) {
+      stk[sp++] = load(o.arg);
+    } else if (o.op == QG_OP_CONST) {
+      stk[sp++] = R29::from_l9(consts29[o.arg]);
+    } else {
+      const R29 b = stk[--sp], a = stk[--sp];
+      stk[sp++] = o.op == QG_OP_ADD ? red2p29(add29(a, b)) : mul29(a, b);
+    }
+  }
+  return stk[0];
+}
+
+template <int NPP>
+__global__ void __launch_bounds__(256)
+    k_gen_eval(const Fr* const* __restrict__ tabs, size_t npairs, uint32_t np,
+               const GenOp* __restrict__ ops, uint32_t len, const L9* __restrict__ consts29,
+               const L9* __restrict__ t29, Fr* __restrict__ partial) {
+  __shared__ R29 red[4 * NPP];
+  __shared__ R29 res[NPP];
+  constexpr uint32_t PB = 256 / NPP;
+  const uint32_t tid = threadIdx.x, t = tid % NPP, pl = tid / NPP;
+  const R29 to261 = R29::from_l9(F29P<FrP>::TO261);
+  R29 acc = R29::zero();
+  for (size_t base = (size_t)blockIdx.x * PB; base < npairs; base += (size_t)gridDim.x * PB) {
+    const size_t p = base + pl;
+    if (p >= npairs || t >= np) continue;
+    const R29 tt = R29::from_l9(t29[t]);
+    const R29 v = gen_interp(ops, len, consts29, [&](uint32_t s) {
+      const Fr* tb = tabs[s];
+      const R29 lo = to29(tb[2 * p]), hi = to29(tb[2 * p + 1]);
+      // lo + t (hi - lo) in arkworks form (< 2p), then into the 2^261 domain
+      return mul29(red6p(add29(lo, mul29(sub29(hi, lo), tt))), to261);
+    });
+    acc = red2p29(add29(acc, v));
+  }
+  block_reduce_pts<NPP>(acc, np, red, res);
+  if (tid < NPP) partial[(size_t)blockIdx.x * NPP + tid] = from29(canon29(tid < np ? res[tid] : R29::zero()));
+}
+
+// out[x] = h(x) for every row (canonical Montgomery words)
+__global__ void __launch_bounds__(256)
+    k_gen_table(const Fr* const* __restrict__ tabs, size_t n, const GenOp* __restrict__ ops,
+                uint32_t len, const L9* __restrict__ consts29, Fr* __restrict__ out) {
+  const size_t x = (size_t)blockIdx.x * blockDim.x + threadIdx.x;
+  if (x >= n) return;
+  const R29 to261 = R29::from_l9(F29P<FrP>::TO261);
+  const R29 v = gen_interp(ops, len, consts29,
+                           [&](uint32_t s) { return mul29(to29(tabs[s][x]), to261); });
+  out[x] = from29(canon29(mul29(v, R29::from_l9(F29P<FrP>::TO256))));
+}
+
+// one block: per-point sums of the partial rows, 2^261 domain -> Montgomery
+// (x 2^256) words for the host's interpolation
+template <int NPP>
+__global__ void __launch_bounds__(256)
+    k_gen_rows(const Fr* __restrict__ partial, uint32_t nrows, uint32_t np, Fr* __restrict__ out) {
+  __shared__ R29 red[4 * NPP];
+  __shared__ R29 res[NPP];
+  sum_rows29<NPP>(partial, nrows, np, red, res);
+  if (threadIdx.x < np)
+    out[threadIdx.x] = from29(canon29(mul29(res[threadIdx.x], R29::from_l9(F29P<FrP>::TO256))));
+}
+
+// fold every slot by r (x 2^261 in st->r29): dst[s][q] = x0 + r (x1 - x0) (< 2p)
+__global__ void k_gen_fold(const Fr* const* __restrict__ src, Fr* const* __restrict__ dst,
+                           uint32_t nslots, size_t nq, const ScState* __restrict__ st) {
+  const size_t i = (size_t)blockIdx.x * blockDim.x + threadIdx.x;
+  if (i >= nq * nslots) return;
+  const uint32_t s = (uint32_t)(i / nq);
+  const size_t q = i % nq;
+  R29 r;
+#pragma unroll
+  for (int k = 0; k < 9; k++) r.l[k] = st->r29[k];
+  const R29 x0 = to29(src[s][2 * q]), x1 = to29(src[s][2 * q + 1]);
+  dst[s][q] = from29(red6p(add29(x0, mul29(sub29(x1, x0), r))));
+}
+
 // eq(bin(i), z) for i < 2^nbits over z[off .. off+nbits)   (eq_eval.rs:6-31)
 __global__ void k_eq_small(const Fr* __restrict__ z, uint32_t off, uint32_t nbits,
                            Fr* __restrict__ out) {
@@ -1441,13 +1545,268 @@ static void run_rounds_any(qg_ctx* ctx, uint32_t nvars, const std::vector<const 
   else run_rounds<K, NP>(ctx, nvars, src, d_sp, h, ro, bar, d_final, d_eval);
 }
 
+// inverse Vandermonde on nodes 0..np-1 for any np <= GEN_NPMAX: V[t][u]
+// (Montgomery) with coefficient t of the interpolant = sum_u V[t][u] ev[u]
+static std::vector<Fr> vinv_general(uint32_t np) {
+  std::vector<Fr> V((size_t)np * np, Fr::zero());
+  for (uint32_t j = 0; j < np; j++) {
+    std::vector<Fr> poly(1, Fr::one());
+    Fr den = Fr::one();
+    for (uint32_t m = 0; m < np; m++) {
+      if (m == j) continue;
+      std::vector<Fr> np2(poly.size() + 1, Fr::zero());
+      const Fr negm = fneg(from_u64<FrP>(m));
+      for (size_t k = 0; k < poly.size(); k++) {
+        np2[k] = np2[k] + poly[k] * negm;
+        np2[k + 1] = np2[k + 1] + poly[k];
+      }
+      poly = np2;
+      den = den * ((j >= m) ? from_u64<FrP>(j - m) : fneg(from_u64<FrP>(m - j)));
+    }
+    const Fr dinv = finv(den);
+    for (uint32_t i = 0; i < np; i++) V[(size_t)i * np + j] = poly[i] * dinv;
+  }
+  return V;
+}
+
+// value of the postfix program on host values (Montgomery), per input table
+static Fr host_eval_postfix(const qg_expr_op* prog, size_t len, const uint64_t* consts,
+                            const std::vector<Fr>& in) {
+  std::vector<Fr> st;
+  for (size_t i = 0; i < len; i++) {
+    const uint32_t op = prog[i].op, arg = prog[i].arg;
+    if (op == QG_OP_INPUT) {
+      st.push_back(in[arg]);
+    } else if (op == QG_OP_CONST) {
+      st.push_back(fr_import(consts + 4 * (size_t)arg));
+    } else {
+      const Fr b = st.back();
+      st.pop_back();
+      const Fr a = st.back();
+      st.pop_back();
+      st.push_back(op == QG_OP_ADD ? a + b : a * b);
+    }
+  }
+  return st.back();
+}
+
+template <int NPP>
+static void gen_round_kernels(qg_ctx* ctx, const Fr* const* d_ptrs, size_t half, uint32_t np,
+                              const GenOp* d_ops, uint32_t len, const L9* d_c29, const L9* d_t29,
+                              Fr* partial, Fr* d_out) {
+  constexpr size_t PB = 256 / NPP;
+  const unsigned grid = (unsigned)std::max<size_t>(1, std::min<size_t>(div_up(half, PB), 1024));
+  hipLaunchKernelGGL((k_gen_eval<NPP>), dim3(grid), dim3(256), 0, ctx->stream, d_ptrs, half, np,
+                     d_ops, len, d_c29, d_t29, partial);
+  QG_LAUNCH_CHECK();
+  hipLaunchKernelGGL((k_gen_rows<NPP>), dim3(1), dim3(256), 0, ctx->stream, partial, grid, np,
+                     d_out);
+  QG_LAUNCH_CHECK();
+}
+
+// postfix program for the interpreter: used tables (first appearance), remapped
+// ops, constants x 2^261; validates the program like expr_degree does
+struct GenProg {
+  std::vector<GenOp> ops;
+  std::vector<uint32_t> used;
+  std::vector<L9> c29;
+};
+
+static GenProg gen_prepare(const qg_expr_op* prog, size_t prog_len, const uint64_t* consts,
+                           size_t nconsts, uint32_t ntables) {
+  GenProg g;
+  std::vector<uint32_t> slot_of(ntables, ~0u);
+  g.ops.resize(prog_len);
+  int depth = 0, maxd = 0;
+  for (size_t i = 0; i < prog_len; i++) {
+    const uint32_t op = prog[i].op, arg = prog[i].arg;
+    if (op == QG_OP_INPUT) {
+      QG_CHECK(arg < ntables, QG_ERR_INVALID, "expression input index out of range");
+      if (slot_of[arg] == ~0u) {
+        slot_of[arg] = (uint32_t)g.used.size();
+        g.used.push_back(arg);
+      }
+      g.ops[i] = {op, slot_of[arg]};
+      depth++;
+    } else if (op == QG_OP_CONST) {
+      QG_CHECK(arg < nconsts, QG_ERR_INVALID, "expression constant index out of range");
+      g.ops[i] = {op, arg};
+      depth++;
+    } else {
+      QG_CHECK(op == QG_OP_ADD || op == QG_OP_MUL, QG_ERR_INVALID, "unknown expression opcode");
+      QG_CHECK(depth >= 2, QG_ERR_INVALID, "malformed expression (stack underflow)");
+      g.ops[i] = {op, 0};
+      depth--;
+    }
+    maxd = std::max(maxd, depth);
+  }
+  QG_CHECK(depth == 1, QG_ERR_INVALID, "malformed expression (stack size != 1)");
+  QG_CHECK(maxd <= GEN_STACK, QG_ERR_UNSUPPORTED, "expression stack deeper than 32");
+  g.c29.resize(std::max<size_t>(nconsts, 1));
+  for (size_t i = 0; i < nconsts; i++)
+    g.c29[i] = l9_of(plain_mul(from_mont(fr_import(consts + 4 * i)), pow2_mod_plain<FrP>(261)));
+  return g;
+}
+
+// uploads ops and constants into scratch `tag`; returns (ops, consts) device pointers
+static std::pair<GenOp*, L9*> gen_upload(qg_ctx* ctx, const GenProg& g, const std::string& tag) {
+  const size_t ob = sizeof(GenOp) * std::max<size_t>(g.ops.size(), 1);
+  const size_t ob_al = (ob + 63) & ~size_t(63);
+  uint8_t* d = ctx->scratch_as<uint8_t>(tag, ob_al + sizeof(L9) * g.c29.size());
+  QG_HIP(hipMemcpyAsync(d, g.ops.data(), sizeof(GenOp) * g.ops.size(), hipMemcpyHostToDevice,
+                        ctx->stream));
+  QG_HIP(hipMemcpyAsync(d + ob_al, g.c29.data(), sizeof(L9) * g.c29.size(), hipMemcpyHostToDevice,
+                        ctx->stream));
+  return {reinterpret_cast<GenOp*>(d), reinterpret_cast<L9*>(d + ob_al)};
+}
+
+// h(x) for the n rows of `tabs` into d_out (Logup / constraint-check fallback
+// for expressions outside their compiled envelopes).  Synchronous: the host
+// copies of the program are stack-local.
+void expr_table_device(qg_ctx* ctx, size_t n, uint32_t ntables, const std::vector<const Fr*>& tabs,
+                       const qg_expr_op* prog, size_t prog_len, const uint64_t* consts,
+                       size_t nconsts, Fr* d_out) {
+  const GenProg g = gen_prepare(prog, prog_len, consts, nconsts, ntables);
+  auto dp = gen_upload(ctx, g, "gen_tab_prog");
+  std::vector<const Fr*> hp(std::max<size_t>(g.used.size(), 1), nullptr);
+  for (size_t s2 = 0; s2 < g.used.size(); s2++) hp[s2] = tabs[g.used[s2]];
+  const Fr** d_ptrs = ctx->scratch_as<const Fr*>("gen_tab_ptrs", hp.size());
+  QG_HIP(hipMemcpyAsync(d_ptrs, hp.data(), sizeof(Fr*) * hp.size(), hipMemcpyHostToDevice,
+                        ctx->stream));
+  hipLaunchKernelGGL(k_gen_table, dim3(div_up(n, 256)), dim3(256), 0, ctx->stream, d_ptrs, n,
+                     dp.first, (uint32_t)g.ops.size(), dp.second, d_out);
+  QG_LAUNCH_CHECK();
+  ctx->sync();
+}
+
+// Sumcheck over the generic interpreter (see k_gen_eval); same transcript,
+// proof and claim as the fast path (sumcheck.rs:28-114)
+static void sumcheck_run_generic(qg_ctx* ctx, uint32_t nvars, uint32_t ntables,
+                                 const std::vector<const Fr*>& d_tables, const qg_expr_op* prog,
+                                 size_t prog_len, const uint64_t* consts, size_t nconsts,
+                                 const uint64_t claimed_sum[4], uint8_t state[32],
+                                 uint64_t* round_coeffs, uint32_t* round_lens, uint64_t* point,
+                                 uint64_t evaluation[4]) {
+  QG_CHECK(ctx->world == 1, QG_ERR_UNSUPPORTED,
+           "generic (interpreted) sumcheck expressions run on one GPU");
+  const uint32_t width = expr_degree(prog, prog_len) + 1;
+  const uint32_t np = width;
+  QG_CHECK(np <= (uint32_t)GEN_NPMAX, QG_ERR_UNSUPPORTED, "expression degree above 31");
+  const GenProg g = gen_prepare(prog, prog_len, consts, nconsts, ntables);
+  const std::vector<uint32_t>& used = g.used;
+  const uint32_t K = (uint32_t)used.size();
+  const size_t N = (size_t)1 << nvars;
+  // t x 2^261 (plain integers, 29-bit limbs)
+  std::vector<L9> t29(GEN_NPMAX);
+  for (uint32_t t = 0; t < (uint32_t)GEN_NPMAX; t++)
+    t29[t] = l9_of(plain_mul(from_u64_plain(t), pow2_mod_plain<FrP>(261)));
+  const std::vector<Fr> V = vinv_general(np);
+  // device data: ops | consts | t | per-round slot pointers | fold scratch
+  const auto dprog = gen_upload(ctx, g, "gen_prog");
+  const GenOp* d_ops = dprog.first;
+  const L9* d_c29 = dprog.second;
+  L9* d_t29 = ctx->scratch_as<L9>("gen_t29", GEN_NPMAX);
+  QG_HIP(hipMemcpyAsync(d_t29, t29.data(), sizeof(L9) * GEN_NPMAX, hipMemcpyHostToDevice,
+                        ctx->stream));
+  const size_t Ks = std::max<uint32_t>(K, 1);
+  Fr* X = ctx->scratch_as<Fr>("gen_x", std::max<size_t>(1, (N / 2) * Ks));
+  Fr* Y = ctx->scratch_as<Fr>("gen_y", std::max<size_t>(1, (N / 4) * Ks));
+  // round j's tables: inputs (j = 0), X (j odd), Y (j even >= 2)
+  std::vector<const Fr*> hp((size_t)nvars * Ks, nullptr);
+  for (uint32_t j = 0; j < nvars; j++)
+    for (uint32_t s2 = 0; s2 < K; s2++)
+      hp[(size_t)j * Ks + s2] = j == 0 ? d_tables[used[s2]]
+                                       : ((j & 1) ? X + (N / 2) * s2 : Y + std::max<size_t>(1, N / 4) * s2);
+  const Fr** d_ptrs = ctx->scratch_as<const Fr*>("gen_ptrs", hp.size());
+  QG_HIP(hipMemcpyAsync(d_ptrs, hp.data(), sizeof(Fr*) * hp.size(), hipMemcpyHostToDevice,
+                        ctx->stream));
+  ScState* d_st = ctx->scratch_as<ScState>("gen_st", 1);
+  Fr* partial = ctx->scratch_as<Fr>("gen_partial", (size_t)1024 * GEN_NPMAX);
+  Fr* d_out = ctx->scratch_as<Fr>("gen_out", GEN_NPMAX);
+  // transcript: append num_vars (usize) and claimed_sum (sumcheck.rs:35-36)
+  {
+    uint8_t b8[8], b32[32];
+    u64_to_bytes(nvars, b8);
+    transcript_append(state, b8, 8);
+    fr_to_bytes(fr_import(claimed_sum), b32);
+    transcript_append(state, b32, 32);
+  }
+  uint32_t npp = 4;
+  while (npp < np) npp <<= 1;
+  std::vector<Fr> ev(np);
+  Fr r = Fr::zero();
+  QgTimed tm(ctx, "sumcheck_round");
+  for (uint32_t j = 0; j < nvars; j++) {
+    const size_t half = N >> (j + 1);
+    if (j > 0 && K > 0) {
+      const size_t nq = 2 * half;
+      hipLaunchKernelGGL(k_gen_fold, dim3(div_up(nq * K, 256)), dim3(256), 0, ctx->stream,
+                         d_ptrs + (size_t)(j - 1) * Ks, (Fr* const*)(d_ptrs + (size_t)j * Ks), K, nq,
+                         d_st);
+      QG_LAUNCH_CHECK();
+    }
+    const Fr* const* dp = d_ptrs + (size_t)j * Ks;
+    switch (npp) {
+      case 4: gen_round_kernels<4>(ctx, dp, half, np, d_ops, (uint32_t)prog_len, d_c29, d_t29, partial, d_out); break;
+      case 8: gen_round_kernels<8>(ctx, dp, half, np, d_ops, (uint32_t)prog_len, d_c29, d_t29, partial, d_out); break;
+      case 16: gen_round_kernels<16>(ctx, dp, half, np, d_ops, (uint32_t)prog_len, d_c29, d_t29, partial, d_out); break;
+      default: gen_round_kernels<32>(ctx, dp, half, np, d_ops, (uint32_t)prog_len, d_c29, d_t29, partial, d_out); break;
+    }
+    QG_HIP(hipMemcpyAsync(ev.data(), d_out, sizeof(Fr) * np, hipMemcpyDeviceToHost, ctx->stream));
+    ctx->sync();
+    // coefficients, trim, absorb (u64 length + canonical coefficients), draw r
+    std::vector<Fr> co(np);
+    uint32_t len = 0;
+    for (uint32_t t = 0; t < np; t++) {
+      Fr a = Fr::zero();
+      for (uint32_t u = 0; u < np; u++) a = a + V[(size_t)t * np + u] * ev[u];
+      co[t] = a;
+      if (!a.is_zero()) len = t + 1;
+    }
+    std::vector<uint8_t> msg(8 + 32 * (size_t)len);
+    u64_to_bytes(len, msg.data());
+    for (uint32_t t = 0; t < len; t++) fr_to_bytes(co[t], msg.data() + 8 + 32 * t);
+    transcript_append(state, msg.data(), msg.size());
+    r = transcript_draw_fr(state);
+    for (uint32_t t = 0; t < width; t++)
+      fr_export(t < len ? co[t] : Fr::zero(), round_coeffs + 4 * ((size_t)j * width + t));
+    round_lens[j] = len;
+    fr_export(r, point + 4 * j);
+    // r x 2^261 for the next fold
+    ScState* hs = reinterpret_cast<ScState*>(ctx->pinned_get("gen_st", sizeof(ScState)));
+    memset(hs, 0, sizeof(ScState));
+    const L9 r29 = l9_of(plain_mul(from_mont(r), pow2_mod_plain<FrP>(261)));
+    for (int k = 0; k < 9; k++) hs->r29[k] = r29.v[k];
+    QG_HIP(hipMemcpyAsync(d_st, hs, sizeof(ScState), hipMemcpyHostToDevice, ctx->stream));
+  }
+  // final fold with r_{n-1} on the host and h at the point (sumcheck.rs:93-99)
+  std::vector<Fr> fin(ntables, Fr::zero());
+  for (uint32_t s2 = 0; s2 < K; s2++) {
+    Fr ab[2];
+    QG_HIP(hipMemcpyAsync(ab, hp[(size_t)(nvars - 1) * Ks + s2], sizeof ab, hipMemcpyDeviceToHost,
+                          ctx->stream));
+    ctx->sync();
+    for (Fr& x : ab) reduce_once<FrP>(x.v), reduce_once<FrP>(x.v);
+    fin[used[s2]] = ab[0] + r * (ab[1] - ab[0]);
+  }
+  fr_export(host_eval_postfix(prog, prog_len, consts, fin), evaluation);
+}
+
 static void sumcheck_run(qg_ctx* ctx, uint32_t nvars, uint32_t ntables,
                          const std::vector<const Fr*>& d_tables, const qg_expr_op* prog,
                          size_t prog_len, const uint64_t* consts, size_t nconsts,
                          const uint64_t claimed_sum[4], uint8_t state[32], uint64_t* round_coeffs,
                          uint32_t* round_lens, uint64_t* point, uint64_t evaluation[4]) {
   QG_CHECK(nvars >= 1 && nvars <= 40, QG_ERR_INVALID, "nvars out of range");
-  auto P = get_program(prog, prog_len, consts, nconsts, ntables);
+  std::shared_ptr<const ScProgram> P;
+  try {
+    P = get_program(prog, prog_len, consts, nconsts, ntables);
+  } catch (const Error& e) {
+    if (e.code != QG_ERR_UNSUPPORTED) throw;
+    // outside the compiled envelope: the interpreted generic path
+    return sumcheck_run_generic(ctx, nvars, ntables, d_tables, prog, prog_len, consts, nconsts,
+                                claimed_sum, state, round_coeffs, round_lens, point, evaluation);
+  }
   const uint32_t width = P->width;
 
   // transcript: append num_vars (usize) and claimed_sum (sumcheck.rs:35-36)
