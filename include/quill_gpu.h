@@ -201,6 +201,37 @@ int qg_mle_open(qg_ctx* ctx, const qg_srs* srs, const uint64_t* poly, size_t n,
 int qg_mle_open_dev(qg_ctx* ctx, const qg_srs* srs, const qg_buf* poly, size_t n,
                     const uint64_t* point, size_t nvars, uint8_t state[32], qg_mle_proof* out);
 
+/* ---------------------------------------------------------------- verifiers (host) */
+/* BN254 G2 affine points on the D-type twist E'/Fq2 (y^2 = x^3 + 3/(9 + u)):
+ * x.c0, x.c1, y.c0, y.c1, each 4 u64 Montgomery limbs (like G1's Fq). */
+/* the standard generator (ark-bn254's G2Affine::generator()) */
+int qg_g2_generator(uint64_t out_xy[16]);
+/* k * Q (k: Fr, Montgomery limbs) — builds g2_points[1] = tau g2 of
+ * KZG::trusted_setup (kzg.rs:52-53).  QG_ERR_INVALID off the curve. */
+int qg_g2_mul(const uint64_t xy[16], uint8_t inf, const uint64_t k[4], uint64_t out_xy[16],
+              uint8_t* out_inf);
+/* E::pairing(P, Q) (ark-bn254 optimal ate, called at kzg.rs:104-105): the
+ * reduced pairing in Fq12 = Fq6[w]/(w^2 - v), Fq6 = Fq2[v]/(v^3 - (9 + u)):
+ * out = c0.c0, c0.c1, c0.c2, c1.c0, c1.c1, c1.c2, each (re, im), Montgomery. */
+int qg_pairing(const uint64_t p_xy[8], uint8_t p_inf, const uint64_t q_xy[16], uint8_t q_inf,
+               uint64_t out[48]);
+/* The verifier's view of KZG (kzg.rs:10-23): g1, g2 = g2_points[0],
+ * g2_tau = g2_points[1]. */
+typedef struct qg_kzg_vk {
+  uint64_t g1_xy[8];
+  uint64_t g2_xy[16];
+  uint64_t g2_tau_xy[16];
+} qg_kzg_vk;
+/* KZG::verify (kzg.rs:98-108): *ok = e(C - y g1, g2) == e(proof, g2_tau - x g2). */
+int qg_kzg_verify(const qg_kzg_vk* vk, const uint64_t comm_xy[8], uint8_t comm_inf,
+                  const qg_kzg_opening* opening, int* ok);
+/* MLEvalProof::verify (mlpcs.rs:126-161): replays the transcript (append
+ * point, evaluation, s_comm; draw r), verifies the four openings and the
+ * inner-product equation at r.  `state` advances exactly as the prover's. */
+int qg_mle_verify(const qg_kzg_vk* vk, const uint64_t comm_xy[8], uint8_t comm_inf,
+                  const uint64_t* point, size_t nvars, const qg_mle_proof* proof,
+                  uint8_t state[32], int* ok);
+
 /* Building blocks of the opening, exposed for testing and for callers that
  * batch their own protocol:
  *  compute_pr (mlpcs.rs:68-78) == eq(bin(i), point) table, untrimmed (2^nvars) */

@@ -8,10 +8,12 @@ from ._lib import LIB_PATH, QuillGpuError, lib  # noqa: F401
 from .device import Device, DeviceVec, Srs  # noqa: F401
 from .hyperplonk import (SumcheckProof, VirtualPolyExpr, VirtualPolynomialStore,  # noqa: F401
                          ZeroCheckProof)
-from .pcs import KZG, EvaluationClaim, KZGOpeningProof, MLEvalProof  # noqa: F401
+from .pcs import (KZG, EvaluationClaim, KZGOpeningProof, MLEvalProof, g2_generator,  # noqa: F401
+                  g2_mul, pairing)
 from .transcript import Transcript  # noqa: F401
 from .logup import (LookupMode, LookupProof, MultisetEqualityProof,  # noqa: F401
                     PermutationCheckProof, SetInclusionProof)
 from .frontend import StateCell, TransitionCircuit, TransitionCircuitTarget  # noqa: F401
 from .proof import (HyperPlonk, HyperPlonkProof, TracePK, TraceProof, TraceVK,  # noqa: F401
                     TraceWitness)
+from .serialize import deserialize, serialize  # noqa: F401

@@ -40,6 +40,11 @@ class MleProof(C.Structure):
                 ("s_opening", KzgOpening), ("s_opening_inv", KzgOpening)]
 
 
+class KzgVk(C.Structure):
+    _fields_ = [("g1_xy", C.c_uint64 * 8), ("g2_xy", C.c_uint64 * 16),
+                ("g2_tau_xy", C.c_uint64 * 16)]
+
+
 class ExprOp(C.Structure):
     _fields_ = [("op", C.c_uint32), ("arg", C.c_uint32)]
 
@@ -93,6 +98,13 @@ PROTOTYPES = {
     "qg_kzg_commit": (C.c_int, [P, P, U64P, SZ, U64P, U8P]),
     "qg_kzg_open": (C.c_int, [P, P, U64P, SZ, U64P, C.POINTER(KzgOpening)]),
     "qg_mle_open": (C.c_int, [P, P, U64P, SZ, U64P, SZ, U8P, C.POINTER(MleProof)]),
+    "qg_g2_generator": (C.c_int, [U64P]),
+    "qg_g2_mul": (C.c_int, [U64P, C.c_uint8, U64P, U64P, U8P]),
+    "qg_pairing": (C.c_int, [U64P, C.c_uint8, U64P, C.c_uint8, U64P]),
+    "qg_kzg_verify": (C.c_int, [C.POINTER(KzgVk), U64P, C.c_uint8, C.POINTER(KzgOpening),
+                                C.POINTER(C.c_int)]),
+    "qg_mle_verify": (C.c_int, [C.POINTER(KzgVk), U64P, C.c_uint8, U64P, SZ,
+                                C.POINTER(MleProof), U8P, C.POINTER(C.c_int)]),
     "qg_mle_open_dev": (C.c_int, [P, P, P, SZ, U64P, SZ, U8P, C.POINTER(MleProof)]),
     "qg_eq_table": (C.c_int, [P, U64P, SZ, U64P]),
     "qg_eq_table_dev": (C.c_int, [P, U64P, SZ, P]),

@@ -100,3 +100,21 @@ def g1_to_abi(P):
         xy[i] = lx[i]
         xy[4 + i] = ly[i]
     return xy, 0
+
+
+def g2_from_abi(xy, inf):
+    """ABI G2 (x.c0, x.c1, y.c0, y.c1 Montgomery limbs) -> ((x0, x1), (y0, y1)) or None"""
+    if inf:
+        return None
+    v = [fq_from_mont_limbs(list(xy)[4 * k:4 * k + 4]) for k in range(4)]
+    return ((v[0], v[1]), (v[2], v[3]))
+
+
+def g2_to_abi(Q):
+    xy = (C.c_uint64 * 16)()
+    if Q is None:
+        return xy, 1
+    for k, c in enumerate((Q[0][0], Q[0][1], Q[1][0], Q[1][1])):
+        for i, limb in enumerate(fq_to_mont_limbs(c)):
+            xy[4 * k + i] = limb
+    return xy, 0

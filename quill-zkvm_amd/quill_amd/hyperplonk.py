@@ -204,11 +204,50 @@ class SumcheckProof:
         return SumcheckProof(num_vars, claimed_sum % R_MOD, r_polys), EvaluationClaim(pt, e)
 
 
+def _poly_eval(coeffs, x):
+    acc = 0
+    for c in reversed(coeffs):
+        acc = (acc * x + c) % R_MOD
+    return acc
+
+
+def _sumcheck_verify(self, transcript: Transcript) -> EvaluationClaim:
+    """sumcheck.rs:116-150: r_i(0) + r_i(1) == v per round; raises ValueError
+    with the reference's Err message"""
+    transcript.append_u64(self.num_vars)
+    transcript.append_fr(self.claimed_sum)
+    v = self.claimed_sum % R_MOD
+    point = []
+    for rp in self.r_polys:
+        if (_poly_eval(rp, 0) + _poly_eval(rp, 1)) % R_MOD != v:
+            raise ValueError("Sumcheck polynomial does not sum to previous value")
+        transcript.append_poly(rp)
+        r = transcript.draw_field_element()
+        point.append(r)
+        v = _poly_eval(rp, r)
+    return EvaluationClaim(point, v)
+
+
+SumcheckProof.verify = _sumcheck_verify
+
+
 @dataclass
 class ZeroCheckProof:
     """zerocheck.rs:8-11"""
     num_vars: int
     sumcheck_proof: SumcheckProof
+
+    def verify(self, transcript: Transcript) -> EvaluationClaim:
+        """zerocheck.rs:51-75"""
+        z = [transcript.draw_field_element() for _ in range(self.num_vars)]
+        if self.sumcheck_proof.claimed_sum % R_MOD != 0:
+            raise ValueError("Sumcheck claimed sum is not zero")
+        if self.sumcheck_proof.num_vars != self.num_vars:
+            raise ValueError("Sumcheck proof num_vars does not match zerocheck num_vars")
+        claim = self.sumcheck_proof.verify(transcript)
+        # division by eq_eval: ark's `/` panics on zero, like fr_inv here
+        e = eq_eval(z, claim.point)
+        return EvaluationClaim(claim.point, claim.evaluation * fr_inv(e) % R_MOD)
 
     @staticmethod
     def prove(store: VirtualPolynomialStore, h, transcript: Transcript, dev: Device = None):

@@ -14,7 +14,7 @@ import numpy as np
 
 from ._lib import check, lib
 from .device import Device, DeviceVec
-from .field import R_MOD, fr_c, fr_from_mont_limbs, fr_list, u64p
+from .field import R_MOD, eq_eval, fr_c, fr_from_mont_limbs, fr_list, u64p
 from .hyperplonk import (SumcheckProof, VirtualPolyExpr, VirtualPolynomialStore, _default_device,
                          _program_c, _tables_c)
 from .pcs import EvaluationClaim
@@ -127,6 +127,48 @@ class MultisetEqualityProof:
         orr = pcs.open(right, claim.point, transcript)
         return MultisetEqualityProof(cl, cr, sc, ol, orr), claim.point
 
+    def verify(self, transcript: Transcript, pcs, left_h_eval: EvaluationClaim,
+               right_h_eval: EvaluationClaim, mode=LookupMode.Equality,
+               multiplicities_eval: EvaluationClaim = None):
+        """multiset_check.rs:185-292; raises ValueError with the reference's Err"""
+        beta = transcript.draw_field_element()
+        transcript.append_g1(self.denom_left_commitment)
+        transcript.append_g1(self.denom_right_commitment)
+        lam = transcript.draw_field_element()
+        alpha = transcript.draw_field_element()
+        z = [transcript.draw_field_element() for _ in range(len(left_h_eval.point))]
+        if self.sumcheck_proof.claimed_sum % R_MOD != 0:
+            raise ValueError("Multiset equality sumcheck claimed sum is not zero")
+        claim = self.sumcheck_proof.verify(transcript)
+        ok_l = pcs.verify(self.denom_left_commitment, self.opening_proof_denom_left, transcript)
+        ok_r = pcs.verify(self.denom_right_commitment, self.opening_proof_denom_right, transcript)
+        if not ok_l or not ok_r:
+            raise ValueError("Multiset equality opening proof verification failed")
+        if self.opening_proof_denom_left.point() != claim.point or \
+                self.opening_proof_denom_right.point() != claim.point:
+            raise ValueError("Multiset equality opening proof evaluation point does not match "
+                             "sumcheck")
+        if left_h_eval.point != claim.point or right_h_eval.point != claim.point:
+            raise ValueError("Multiset equality h evaluation point does not match sumcheck")
+        m = 1
+        if mode == LookupMode.Subset:
+            assert multiplicities_eval is not None, \
+                "Multiplicities evaluation must be provided in subset mode"
+            if multiplicities_eval.point != claim.point:
+                raise ValueError("Multiset equality multiplicities evaluation point does not "
+                                 "match sumcheck")
+            m = multiplicities_eval.evaluation
+        else:
+            assert multiplicities_eval is None, \
+                "Multiplicities evaluation must not be provided in equality mode"
+        dl = self.opening_proof_denom_left.evaluation
+        dr = self.opening_proof_denom_right.evaluation
+        zc = (dl * (beta + left_h_eval.evaluation) - 1
+              + lam * (dr * (beta + right_h_eval.evaluation) - m)) % R_MOD
+        final = (zc * eq_eval(z, left_h_eval.point) % R_MOD * alpha + dl - dr) % R_MOD
+        if final != claim.evaluation % R_MOD:
+            raise ValueError("Multiset equality final evaluation does not match sumcheck")
+
 
 @dataclass
 class SetInclusionProof:
@@ -200,6 +242,18 @@ class PermutationCheckProof:
         proof, point = MultisetEqualityProof.prove(store, lh, rh, transcript, pcs,
                                                    LookupMode.Equality, None)
         return PermutationCheckProof(proof), point
+
+    def verify(self, transcript: Transcript, pcs, left_h_eval: EvaluationClaim,
+               right_h_eval: EvaluationClaim, id_eval: EvaluationClaim,
+               perm_eval: EvaluationClaim):
+        """permutation_check.rs:61-92"""
+        alpha = transcript.draw_field_element()
+        lhat = EvaluationClaim(list(left_h_eval.point),
+                               (id_eval.evaluation + alpha * left_h_eval.evaluation) % R_MOD)
+        rhat = EvaluationClaim(list(right_h_eval.point),
+                               (perm_eval.evaluation + alpha * right_h_eval.evaluation) % R_MOD)
+        self.multiset_equality_proof.verify(transcript, pcs, lhat, rhat, LookupMode.Equality,
+                                            None)
 
 
 @dataclass

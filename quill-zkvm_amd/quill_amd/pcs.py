@@ -9,9 +9,10 @@ from dataclasses import dataclass
 
 import numpy as np
 
-from ._lib import KzgOpening, MleProof, QuillGpuError, check, lib
+from ._lib import KzgOpening, KzgVk, MleProof, QuillGpuError, check, lib
 from .device import Device, DeviceVec, Srs
-from .field import fr_array, fr_c, fr_from_mont_limbs, g1_from_abi, u64p
+from .field import (fq_from_mont_limbs, fr_array, fr_c, fr_from_mont_limbs, g1_from_abi,
+                    g1_to_abi, g2_from_abi, g2_to_abi, u64p)
 from .transcript import Transcript
 
 
@@ -30,6 +31,57 @@ class KZGOpeningProof:
     proof: object
 
 
+def _opening_c(o: KZGOpeningProof) -> KzgOpening:
+    c = KzgOpening()
+    C.memmove(c.x, fr_c(o.x), 32)
+    C.memmove(c.y, fr_c(o.y), 32)
+    xy, inf = g1_to_abi(o.proof)
+    C.memmove(c.proof_xy, xy, 64)
+    c.proof_inf = inf
+    return c
+
+
+def _mle_proof_c(p: "MLEvalProof") -> MleProof:
+    c = MleProof()
+    C.memmove(c.evaluation, fr_c(p.evaluation), 32)
+    xy, inf = g1_to_abi(p.s_comm)
+    C.memmove(c.s_comm_xy, xy, 64)
+    c.s_comm_inf = inf
+    c.poly_opening = _opening_c(p.poly_opening)
+    c.poly_opening_inv = _opening_c(p.poly_opening_inv)
+    c.s_opening = _opening_c(p.s_opening)
+    c.s_opening_inv = _opening_c(p.s_opening_inv)
+    return c
+
+
+# ---------------------------------------------------------------- pairing group G2
+G1_GENERATOR = (1, 2)
+
+
+def g2_generator():
+    """ark-bn254 G2Affine::generator() as ((x0, x1), (y0, y1))"""
+    xy = (C.c_uint64 * 16)()
+    check(lib().qg_g2_generator(xy))
+    return g2_from_abi(xy, 0)
+
+
+def g2_mul(Q, k: int):
+    xy, inf = g2_to_abi(Q)
+    out, oinf = (C.c_uint64 * 16)(), C.c_uint8()
+    check(lib().qg_g2_mul(xy, inf, fr_c(k), out, C.byref(oinf)))
+    return g2_from_abi(out, oinf.value)
+
+
+def pairing(P, Q):
+    """E::pairing(P, Q) (ark-bn254 optimal ate) in the tower layout of
+    qg_pairing: 12 canonical Fq ints (c0.c0.re, c0.c0.im, c0.c1.re, ...)"""
+    pxy, pinf = g1_to_abi(P)
+    qxy, qinf = g2_to_abi(Q)
+    out = (C.c_uint64 * 48)()
+    check(lib().qg_pairing(pxy, pinf, qxy, qinf, out))
+    return [fq_from_mont_limbs(list(out)[4 * k:4 * k + 4]) for k in range(12)]
+
+
 def _opening(o: KzgOpening) -> KZGOpeningProof:
     return KZGOpeningProof(fr_from_mont_limbs(list(o.x)), fr_from_mont_limbs(list(o.y)),
                            g1_from_abi(o.proof_xy, o.proof_inf))
@@ -46,6 +98,10 @@ class MLEvalProof:
     s_opening: KZGOpeningProof
     s_opening_inv: KZGOpeningProof
 
+    def verify(self, commitment, kzg: "KZG", transcript: Transcript) -> bool:
+        """mlpcs.rs:126-161 (host pairing check, qg_mle_verify)"""
+        return kzg.verify(commitment, self, transcript)
+
     # MultilinearPCSProof (pcs/src/lib.rs:15-24)
     def point(self):
         return list(self.evaluation_point)
@@ -61,12 +117,20 @@ class KZG:
     (kzg.rs:35-59 with an explicit tau instead of an rng; MultilinearPCS's
     thread_rng setup (mlpcs.rs:178-182) is not reproducible and is not offered)."""
 
-    def __init__(self, dev: Device, srs: Srs, max_degree: int, tau: int = None, g=None):
+    def __init__(self, dev: Device, srs: Srs, max_degree: int, tau: int = None, g=None,
+                 g2_points=None):
         self.dev = dev
         self.srs = srs
         self._max_degree = max_degree
         self._tau, self._g = tau, g
         self._shards = {}
+        # the verifier's part of the CRS (kzg.rs:14-22): g1, g2 = g2_points[0],
+        # g2_points[1] = tau g2 (kzg.rs:52-53)
+        self.g1 = g if g is not None else G1_GENERATOR
+        if g2_points is None and tau is not None:
+            g2 = g2_generator()
+            g2_points = [g2, g2_mul(g2, tau)]
+        self.g2_points = g2_points
 
     @classmethod
     def trusted_setup(cls, max_degree: int, tau: int, dev: Device = None, g=None):
@@ -102,9 +166,54 @@ class KZG:
         self._shards = {}
 
     @classmethod
-    def from_points(cls, g1_points, dev: Device = None):
+    def from_points(cls, g1_points, dev: Device = None, g2_points=None):
+        """an uploaded CRS; verification needs g2_points = [g2, tau g2] and
+        takes g1 = g1_points[0]"""
         dev = dev or Device(0)
-        return cls(dev, Srs.upload(dev, g1_points), len(g1_points) - 1)
+        return cls(dev, Srs.upload(dev, g1_points), len(g1_points) - 1, None, g1_points[0],
+                   g2_points)
+
+    @classmethod
+    def verifier(cls, tau: int = None, g1=None, g2_points=None):
+        """the verifier's view only (g1, g2_points; no device SRS): built from
+        tau like trusted_setup, or from published points"""
+        if tau is None and g2_points is None:
+            raise QuillGpuError(-1, "verifier needs tau or g2_points")
+        return cls(None, None, -1, tau, g1, g2_points)
+
+    def _vk(self) -> KzgVk:
+        if self.g2_points is None:
+            raise QuillGpuError(-1, "no G2 points: verification needs g2 and tau g2")
+        vk = KzgVk()
+        xy, inf = g1_to_abi(self.g1)
+        if inf:
+            raise QuillGpuError(-1, "g1 generator is the identity")
+        C.memmove(vk.g1_xy, xy, 64)
+        for fld, Q in (("g2_xy", self.g2_points[0]), ("g2_tau_xy", self.g2_points[1])):
+            qxy, qinf = g2_to_abi(Q)
+            if qinf:
+                raise QuillGpuError(-1, "G2 point is the identity")
+            C.memmove(getattr(vk, fld), qxy, 128)
+        return vk
+
+    # KZG::verify (kzg.rs:98-108)
+    def verify_univariate(self, commitment, opening: KZGOpeningProof) -> bool:
+        xy, inf = g1_to_abi(commitment)
+        ok = C.c_int()
+        check(lib().qg_kzg_verify(C.byref(self._vk()), xy, inf, C.byref(_opening_c(opening)),
+                                  C.byref(ok)))
+        return bool(ok.value)
+
+    # MultilinearPCS::verify == MLEvalProof::verify (lib.rs:35-40, mlpcs.rs:126-161)
+    def verify(self, commitment, proof: MLEvalProof, transcript: Transcript) -> bool:
+        xy, inf = g1_to_abi(commitment)
+        pt = proof.evaluation_point
+        arr = fr_array(pt) if len(pt) else np.zeros((1, 4), dtype=np.uint64)
+        ok = C.c_int()
+        check(lib().qg_mle_verify(C.byref(self._vk()), xy, inf, u64p(arr), len(pt),
+                                  C.byref(_mle_proof_c(proof)), transcript.c_state(),
+                                  C.byref(ok)))
+        return bool(ok.value)
 
     # MultilinearPCS::max_degree (lib.rs:32)
     def max_degree(self) -> int:

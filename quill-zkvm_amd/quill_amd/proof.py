@@ -7,8 +7,9 @@ zero-check store's witness columns are views into it, so nothing is copied or
 re-uploaded between the zero-check, the permutation check and the openings.
 The transcript is the only host-side state; each step is one C-ABI call
 (MSM, Logup column, eq table, sumcheck, ML-PCS opening) on the trace's
-device vectors.  The verifier is not mirrored (CPU-only in the reference's
-model; the oracle's restatement checks these proofs in tests)."""
+device vectors.  The verifier (proof.rs:303-522) runs on the host: field
+arithmetic on Python ints, the transcript and the KZG pairing checks through
+the C-ABI (qg_mle_verify)."""
 from __future__ import annotations
 
 import ctypes as C
@@ -43,6 +44,78 @@ class HyperPlonkProof:
     """proof.rs:27-30"""
     witness_commitment: list
     trace_proofs: list
+
+
+def _verify_opening(comm, proof: MLEvalProof, expected_point, expected_nv, pcs,
+                    transcript: Transcript) -> bool:
+    """proof.rs:304-323"""
+    if len(proof.point()) != expected_nv:
+        return False
+    if expected_point is not None and proof.point() != list(expected_point):
+        return False
+    return pcs.verify(comm, proof, transcript)
+
+
+def _verify_trace_proof(witness_commitment, vk: "TraceVK", pcs, proof: TraceProof,
+                        transcript: Transcript):
+    """proof.rs:396-492 (with get_and_verify_column_evaluations :325-381 and
+    recover_zerocheck_expr_evaluation :383-394); raises ValueError"""
+    alpha = transcript.draw_field_element()
+    zclaim = proof.zero_check_proof.verify(transcript)
+    circuit = vk.circuit
+    log2_cols, log2_rows = _log2(circuit.num_cols()), _log2(circuit.num_rows())
+    if len(zclaim.point) != log2_rows:
+        raise ValueError("Zero check evaluation claim point length mismatch")
+    pt_claim = proof.opening_permutation_trace.evaluation_claim()
+    proof.permutation_check_proof.verify(transcript, pcs, pt_claim, pt_claim,
+                                         proof.opening_id.evaluation_claim(),
+                                         proof.opening_permutation.evaluation_claim())
+    # column evaluations
+    points = [list(zclaim.point) + [(col >> i) & 1 for i in range(log2_cols)]
+              for col in range(circuit.num_cols())]
+    evals = []
+    for i, op in enumerate(proof.openings_zero_check):
+        if i >= len(points) or op.point() != points[i]:
+            raise ValueError("Zero check opening point mismatch")
+        if not pcs.verify(witness_commitment, op, transcript):
+            raise ValueError("Zero check opening verification failed")
+        evals.append(op.evaluation)
+    for i, op in enumerate(proof.openings_public):
+        if not _verify_opening(vk.public_columns_commitments[i], op, zclaim.point, log2_rows, pcs,
+                               transcript):
+            raise ValueError("Public opening verification failed")
+        evals.append(op.evaluation)
+    acc = 0
+    for i, e in enumerate(circuit.zero_check_expressions()):
+        acc = (acc + pow(alpha, i, R_MOD) * e.evaluate(evals)) % R_MOD
+    if acc != zclaim.evaluation % R_MOD:
+        raise ValueError("Zero check evaluation mismatch")
+    nv = log2_rows + log2_cols
+    if not _verify_opening(vk.id_commitment, proof.opening_id, None, nv, pcs, transcript):
+        raise ValueError("ID commitment opening verification failed")
+    if not _verify_opening(vk.permutation_commitment, proof.opening_permutation, None, nv, pcs,
+                           transcript):
+        raise ValueError("Permutation commitment opening verification failed")
+    if not _verify_opening(witness_commitment, proof.opening_permutation_trace, None, nv, pcs,
+                           transcript):
+        raise ValueError("Permutation trace commitment opening verification failed")
+
+
+def _hyperplonk_verify(self, vk, pcs) -> Transcript:
+    """proof.rs:494-521: raises ValueError on rejection; returns the final
+    transcript (equal to the prover's when the proof verifies)"""
+    t = Transcript(b"hyperplonk_proof")
+    for c in self.witness_commitment:
+        t.append_g1(c)
+    vks = vk.trace_vks if hasattr(vk, "trace_vks") else list(vk)
+    if len(vks) != len(self.trace_proofs):
+        raise ValueError("Number of trace VKS and proofs mismatch")
+    for c, tvk, tp in zip(self.witness_commitment, vks, self.trace_proofs):
+        _verify_trace_proof(c, tvk, pcs, tp, t)
+    return t
+
+
+HyperPlonkProof.verify = _hyperplonk_verify
 
 
 @dataclass
