@@ -144,6 +144,111 @@ static void suffix_horner(qg_ctx* ctx, const Fr* c, size_t L, const Fr& x, Fr* s
   QG_LAUNCH_CHECK();
 }
 
+// Batched form (up to 4 independent scans per launch, blockIdx.y = scan) in
+// 9 x 29-bit limbs: the per-chunk Horner chain is the latency of the whole
+// recursion, and the 29-bit multiply's dependent latency is half the 32-bit
+// one's.  x is passed as x 2^261 (plain limbs), so mul29 keeps the arkworks
+// scale of the coefficients.
+struct ShJob {
+  const Fr* c;  // coefficients (arkworks form)
+  size_t L;
+  L9 x;         // x 2^261 mod p
+  Fr* A;        // chunk values (local pass)
+  const Fr* T;  // chunk carries (apply pass)
+  size_t nch;
+  Fr* s;        // output suffixes
+};
+struct ShJobs {
+  ShJob j[4];
+};
+
+__global__ void k_sh_local_b(ShJobs jb) {
+  const ShJob& J = jb.j[blockIdx.y];
+  const size_t k = (size_t)blockIdx.x * blockDim.x + threadIdx.x;
+  const size_t s = k * SH_B;
+  if (s >= J.L) return;
+  const size_t e = s + SH_B < J.L ? s + SH_B : J.L;
+  const F29<FrP> x = F29<FrP>::from_l9(J.x);
+  F29<FrP> acc = F29<FrP>::zero();
+  for (size_t i = e; i-- > s;) acc = red6p29(add29(to29(J.c[i]), mul29(x, acc)));
+  J.A[k] = from29(canon29(acc));
+}
+
+__global__ void k_sh_apply_b(ShJobs jb) {
+  const ShJob& J = jb.j[blockIdx.y];
+  const size_t k = (size_t)blockIdx.x * blockDim.x + threadIdx.x;
+  const size_t s = k * SH_B;
+  if (s >= J.L) return;
+  const size_t e = s + SH_B < J.L ? s + SH_B : J.L;
+  const F29<FrP> x = F29<FrP>::from_l9(J.x);
+  F29<FrP> acc = (k + 1 < J.nch) ? to29(J.T[k + 1]) : F29<FrP>::zero();
+  for (size_t i = e; i-- > s;) {
+    acc = red6p29(add29(to29(J.c[i]), mul29(x, acc)));
+    J.s[i] = from29(canon29(acc));
+  }
+}
+
+__global__ void k_sh_serial_b(ShJobs jb) {
+  const ShJob& J = jb.j[blockIdx.y];
+  if (threadIdx.x != 0) return;
+  const F29<FrP> x = F29<FrP>::from_l9(J.x);
+  F29<FrP> acc = F29<FrP>::zero();
+  for (size_t i = J.L; i-- > 0;) {
+    acc = red6p29(add29(to29(J.c[i]), mul29(x, acc)));
+    J.s[i] = from29(canon29(acc));
+  }
+}
+
+struct ShIn {
+  const Fr* c;
+  size_t L;
+  Fr x;  // Montgomery
+  Fr* s;
+};
+
+static L9 x261_of(const Fr& x) {
+  const Fr t = from_mont(to_mont(from_mont(x)) * to_mont(pow2_mod_plain<FrP>(261)));
+  const F29<FrP> r = to29(t);
+  L9 o{};
+  for (int i = 0; i < 9; i++) o.v[i] = r.l[i];
+  return o;
+}
+
+// s_i = c_i + x s_{i+1} for up to 4 independent (c, L, x) at once
+static void suffix_horner_batch(qg_ctx* ctx, const std::vector<ShIn>& in, int depth = 0) {
+  std::vector<ShIn> small, big;
+  for (const ShIn& q : in)
+    if (q.L > SH_B) big.push_back(q);
+    else if (q.L > 0) small.push_back(q);
+  QG_CHECK(in.size() <= 4, QG_ERR_ASSERT, "suffix-Horner batch of at most 4");
+  if (!small.empty()) {
+    ShJobs jb{};
+    for (size_t q = 0; q < small.size(); q++)
+      jb.j[q] = {small[q].c, small[q].L, x261_of(small[q].x), nullptr, nullptr, 0, small[q].s};
+    hipLaunchKernelGGL(k_sh_serial_b, dim3(1, (unsigned)small.size()), dim3(64), 0, ctx->stream, jb);
+    QG_LAUNCH_CHECK();
+  }
+  if (big.empty()) return;
+  ShJobs jb{};
+  std::vector<ShIn> up;
+  size_t maxch = 0;
+  for (size_t q = 0; q < big.size(); q++) {
+    const size_t nch = (big[q].L + SH_B - 1) / SH_B;
+    const std::string tag = std::to_string(depth) + "_" + std::to_string(q);
+    Fr* A = ctx->scratch_as<Fr>("shb_A" + tag, nch);
+    Fr* T = ctx->scratch_as<Fr>("shb_T" + tag, nch);
+    jb.j[q] = {big[q].c, big[q].L, x261_of(big[q].x), A, T, nch, big[q].s};
+    up.push_back({A, nch, fpow_small(big[q].x, SH_B), T});  // T_k = A_k + x^B T_{k+1}
+    maxch = std::max(maxch, nch);
+  }
+  const dim3 grid((unsigned)div_up(maxch, ML_BLOCK), (unsigned)big.size());
+  hipLaunchKernelGGL(k_sh_local_b, grid, dim3(ML_BLOCK), 0, ctx->stream, jb);
+  QG_LAUNCH_CHECK();
+  suffix_horner_batch(ctx, up, depth + 1);
+  hipLaunchKernelGGL(k_sh_apply_b, grid, dim3(ML_BLOCK), 0, ctx->stream, jb);
+  QG_LAUNCH_CHECK();
+}
+
 // ---------------------------------------------------------------- NTT
 // Radix-2 NTT passes of up to 11 stages each on LDS tiles of 2048 elements
 // held as 9 x 29-bit limbs (SoA: conflict-free), so a 2^23-point transform is
@@ -369,8 +474,42 @@ static void ntt_twiddles(qg_ctx* ctx, int logn, Fr** tw, Fr** twi) {
   ctx->memo["ntt_tw"] = memo;
 }
 
-// S polynomial (M - 1 coefficients, untrimmed) of f (nf) and g (ng), device in/out
-static void s_poly_device(qg_ctx* ctx, const Fr* f, size_t nf, const Fr* g, size_t ng, Fr* S) {
+// Transform of the eq table without an NTT.  g = eq(., z) over nz variables is
+// the coefficient vector of G(X) = prod_t ((1 - z_t) + z_t X^(2^t)), so
+//   G(w^j) = Q_0(j),  Q_t(j) = ((1 - z_t) + z_t w^(j 2^t)) Q_{t+1}(j),  Q_nz = 1,
+// where Q_t depends only on j mod 2^(L-t).  In the bit-reversed order of the
+// DIF outputs (k' = bitrev_{L-t}(j mod 2^(L-t))) the recursion is streaming:
+//   Q_t[k'] = f_t(k') Q_{t+1}[k' >> 1].
+// One level per launch, 2^(L-t) entries; ~2 multiplies per entry over all
+// levels (~4 x 2^L in total) instead of L/2 per entry of a forward NTT.
+// Q is kept in arkworks form (x 2^256), the factor in the 2^261 domain.
+__global__ void k_eqdft_level(const Fr* __restrict__ qnext, L9 a261, L9 z261,
+                              const Fr* __restrict__ tw, int logn, int t, Fr* __restrict__ q) {
+  const size_t len = (size_t)1 << (logn - t);
+  const size_t k = (size_t)blockIdx.x * blockDim.x + threadIdx.x;
+  if (k >= len) return;
+  // j = bitrev_{L-t}(k); w^(j 2^t): tw[] holds w^m 2^261 for m < 2^(L-1)
+  const size_t j = (size_t)(__brevll((unsigned long long)k) >> (64 - (logn - t)));
+  const size_t m = j << t, half = (size_t)1 << (logn - 1);
+  R29 w = to29(tw[m & (half - 1)]);
+  if (m & half) w = sub29(R29::zero(), w);  // w^(2^(L-1)) = -1 (lazy 4p - w)
+  const R29 f = red6p29(add29(R29::from_l9(a261), mul29(R29::from_l9(z261), w)));
+  const R29 qn = qnext ? to29(qnext[k >> 1]) : to29(Fr::one());
+  q[k] = from29(canon29(mul29(f, qn)));
+}
+
+static L9 l9_of29(const Fr& x) {
+  const R29 t = to29(x);
+  L9 c{};
+  for (int i = 0; i < 9; i++) c.v[i] = t.l[i];
+  return c;
+}
+
+// S polynomial (M - 1 coefficients, untrimmed) of f (nf) and g (ng), device in/out.
+// eq_z (nz variables, host Montgomery): g is eq(., eq_z) over 2^nz entries, and
+// its transform comes from the product formula (k_eqdft_level) instead of an NTT.
+static void s_poly_device(qg_ctx* ctx, const Fr* f, size_t nf, const Fr* g, size_t ng, Fr* S,
+                          const uint64_t* eq_z = nullptr, size_t nz = 0) {
   const size_t M = nf > ng ? nf : ng;
   if (M <= 1) return;
   QgTimed tm(ctx, "s_polynomial");
@@ -403,7 +542,24 @@ static void s_poly_device(qg_ctx* ctx, const Fr* f, size_t nf, const Fr* g, size
   QG_LAUNCH_CHECK();
   // forward DIF of f and g (zero-extended), bit-reversed outputs
   ntt_run(ctx, true, f, nf, F, tw, logn, 0, 0, nullptr);
-  ntt_run(ctx, true, g, ng, G, tw, logn, 0, 0, nullptr);
+  if (eq_z && ((size_t)1 << nz) == ng && (int)nz < logn) {
+    // levels t = nz-1 .. 0 ping-pong between G and H (H is free until the combine),
+    // ending in G (t = 0: 2^logn entries, bit-reversed order)
+    for (int t = (int)nz - 1; t >= 0; t--) {
+      const Fr z = fr_import(eq_z + 4 * t);
+      const Fr zp = from_mont(z), ap = from_mont(Fr::one() - z);
+      const L9 z9 = l9_of29(ml_plain_mul(zp, pow2_mod_plain<FrP>(261)));
+      const L9 a9 = l9_of29(ml_plain_mul(ap, pow2_mod_plain<FrP>(261)));
+      Fr* dst = (t & 1) == 0 ? G : H;
+      const Fr* src = t == (int)nz - 1 ? nullptr : ((t & 1) == 0 ? H : G);
+      const size_t len = (size_t)1 << (logn - t);
+      hipLaunchKernelGGL(k_eqdft_level, dim3(div_up(len, 256)), dim3(256), 0, ctx->stream, src,
+                         a9, z9, tw, logn, t, dst);
+      QG_LAUNCH_CHECK();
+    }
+  } else {
+    ntt_run(ctx, true, g, ng, G, tw, logn, 0, 0, nullptr);
+  }
   hipLaunchKernelGGL(k_s_combine_br, dim3(div_up(n, 256)), dim3(256), 0, ctx->stream, F, G, twM,
                      logn, H);
   QG_LAUNCH_CHECK();
@@ -442,31 +598,46 @@ static size_t trimmed_len(qg_ctx* ctx, const Fr* a, size_t n) {
   return (size_t)h;
 }
 
-// KZG::open quotient on a device polynomial: x, y into `out`, the quotient
-// coefficients q_i = s_{i+1} (i < Lt - 1) in scratch slot `slot`; returns the
-// quotient pointer and its length for the (batched) commitment
-static std::pair<const Fr*, size_t> kzg_quotient_device(qg_ctx* ctx, const qg_srs* srs,
-                                                        const Fr* c, size_t L, const Fr& x,
-                                                        qg_kzg_opening* out, int slot) {
-  fr_export(x, out->x);
-  size_t Lt = trimmed_len(ctx, c, L);  // DensePolynomial::from_coefficients_slice trims
-  Fr y = Fr::zero();
-  const Fr* q = nullptr;
-  size_t qn = 0;
-  if (Lt > 0) {
-    Fr* s = ctx->scratch_as<Fr>("open_s#" + std::to_string(slot), Lt);
-    {
-      QgTimed tm(ctx, "kzg_division");
-      suffix_horner(ctx, c, Lt, x, s);
-    }
-    QG_HIP(hipMemcpyAsync(&y, s, sizeof(Fr), hipMemcpyDeviceToHost, ctx->stream));
-    ctx->sync();
-    QG_CHECK(Lt - 1 <= srs->n, QG_ERR_INVALID, "Polynomial degree exceeds max degree");
-    q = s + 1;
-    qn = Lt - 1;
+// four KZG::open quotients at once (the ML opening's poly and S at r and
+// 1/r): one trimmed length per distinct polynomial, one batched suffix-Horner
+// recursion, one transfer of the four values y = s_0
+static void kzg_quotients_batch(qg_ctx* ctx, const qg_srs* srs, const Fr* const polys[4],
+                                const size_t lens[4], const Fr xs[4], qg_kzg_opening* const outs[4],
+                                std::vector<const Fr*>& qs, std::vector<size_t>& qns) {
+  size_t Lt[4];
+  for (int i = 0; i < 4; i++) {
+    int same = -1;
+    for (int k = 0; k < i; k++)
+      if (polys[k] == polys[i] && lens[k] == lens[i]) same = k;
+    Lt[i] = same >= 0 ? Lt[same] : trimmed_len(ctx, polys[i], lens[i]);
   }
-  fr_export(y, out->y);
-  return {q, qn};
+  std::vector<ShIn> jobs;
+  Fr* s[4] = {nullptr, nullptr, nullptr, nullptr};
+  for (int i = 0; i < 4; i++) {
+    fr_export(xs[i], outs[i]->x);
+    if (Lt[i] == 0) continue;
+    QG_CHECK(Lt[i] - 1 <= srs->n, QG_ERR_INVALID, "Polynomial degree exceeds max degree");
+    s[i] = ctx->scratch_as<Fr>("open_s#" + std::to_string(i), Lt[i]);
+    jobs.push_back({polys[i], Lt[i], xs[i], s[i]});
+  }
+  {
+    QgTimed tm(ctx, "kzg_division");
+    suffix_horner_batch(ctx, jobs);
+  }
+  Fr* d_y = ctx->scratch_as<Fr>("open_y", 4);
+  for (int i = 0; i < 4; i++)
+    if (s[i])
+      QG_HIP(hipMemcpyAsync(d_y + i, s[i], sizeof(Fr), hipMemcpyDeviceToDevice, ctx->stream));
+  Fr y[4];
+  QG_HIP(hipMemcpyAsync(y, d_y, sizeof(y), hipMemcpyDeviceToHost, ctx->stream));
+  ctx->sync();
+  qs.clear();
+  qns.clear();
+  for (int i = 0; i < 4; i++) {
+    fr_export(s[i] ? y[i] : Fr::zero(), outs[i]->y);
+    qs.push_back(s[i] ? s[i] + 1 : nullptr);
+    qns.push_back(s[i] ? Lt[i] - 1 : 0);
+  }
 }
 
 // KZG::open on a device polynomial; fills x, y, proof
@@ -599,7 +770,7 @@ static void mle_open_sharded(qg_ctx* ctx, const qg_srs* srs, const Fr* dpoly, si
   Fr* dS = ctx->scratch_as<Fr>("mle_S", N > 1 ? N - 1 : 1);
   size_t Slen = 0;
   if (N > 1) {
-    s_poly_device(ctx, dfull, N, dpr, N, dS);
+    s_poly_device(ctx, dfull, N, dpr, N, dS, point, nvars);
     Slen = trimmed_len(ctx, dS, N - 1);
   }
   const size_t sloc = Slen > off ? std::min(L, Slen - off) : 0;
@@ -645,7 +816,7 @@ static void mle_open_device(qg_ctx* ctx, const qg_srs* srs, const Fr* dpoly, siz
   Fr* dS = ctx->scratch_as<Fr>("mle_S", M > 1 ? M - 1 : 1);
   size_t Slen = 0;
   if (M > 1) {
-    s_poly_device(ctx, dpoly, n, dpr, N, dS);
+    s_poly_device(ctx, dpoly, n, dpr, N, dS, point, nvars);
     Slen = trimmed_len(ctx, dS, M - 1);
   }
   QG_CHECK(Slen <= srs->n, QG_ERR_INVALID, "Polynomial degree exceeds max degree");
@@ -674,11 +845,7 @@ static void mle_open_device(qg_ctx* ctx, const qg_srs* srs, const Fr* dpoly, siz
   const Fr xs[4] = {r, r_inv, r, r_inv};
   std::vector<const Fr*> qs;
   std::vector<size_t> qns;
-  for (int i = 0; i < 4; i++) {
-    auto q = kzg_quotient_device(ctx, srs, polys[i], lens[i], xs[i], outs[i], i);
-    qs.push_back(q.first);
-    qns.push_back(q.second);
-  }
+  kzg_quotients_batch(ctx, srs, polys, lens, xs, outs, qs, qns);
   const std::vector<G1Affine> pis = msm_device_batch(ctx, srs, qs, qns);
   for (int i = 0; i < 4; i++) g1_export(pis[i], outs[i]->proof_xy, &outs[i]->proof_inf);
 }
