@@ -1323,3 +1323,171 @@ int oc_bench_sumcheck_mt(int log_n, uint64_t seed, int nthreads, double* seconds
   free(pt);
   return 0;
 }
+
+/* ---------------------------------------------------------------- MLEvalProof::prove
+ * mlpcs.rs:83-124 as the reference runs it (single thread, ark-poly data flow):
+ *   pr = compute_pr(point): eval_pr (mlpcs.rs:52-63) at the 2^n domain elements,
+ *        then the domain's IFFT (mlpcs.rs:68-78);
+ *   evaluation = <poly, pr> over the common prefix (mlpcs.rs:91-94);
+ *   S = compute_s_polynomial(poly, pr) (ipa.rs:122-157): poly * rev(pr) +
+ *       rev(poly) * pr with ark-poly FFT products (dp_mul), h[M ..], trimmed;
+ *   s_comm = commit(S) (msm_ark); transcript: point, evaluation, s_comm; r;
+ *   four KZG::open (kzg.rs:75-96): y = p(x) (Horner), q = (p - y) / (X - x)
+ *       (long division), assert q (X - x) == p - y (an FFT product, as the
+ *       reference's assert! does), commit(q).
+ * Bases [tau^i] g are generated before the clock starts.  Outputs for the
+ * parity test; *seconds = the timed prove. */
+static fp eval_pr_c(const fp* r, int n, fp x) {
+  fp acc = f_one(&FR), one = f_one(&FR);
+  for (int i = 0; i < n; i++) {
+    acc = f_mul(&FR, acc, f_add(&FR, f_mul(&FR, r[i], x), f_sub(&FR, one, r[i])));
+    x = f_mul(&FR, x, x);
+  }
+  return acc;
+}
+static void g1_ser_c(const g1a* a, uint8_t out[64]) {
+  memset(out, 0, 64);
+  if (a->inf) {
+    out[63] |= 0x40;
+    return;
+  }
+  fp x = f_from_mont(&FQ, a->x), y = f_from_mont(&FQ, a->y);
+  fp ny = f_from_mont(&FQ, f_sub(&FQ, (fp){{0, 0, 0, 0}}, a->y));
+  memcpy(out, x.v, 32);
+  memcpy(out + 32, y.v, 32);
+  int gt = 0;
+  for (int i = 3; i >= 0; i--)
+    if (y.v[i] != ny.v[i]) {
+      gt = y.v[i] > ny.v[i];
+      break;
+    }
+  if (gt) out[63] |= 0x80;
+}
+static void kzg_open_c(const g1a* bases, const fp* c, int n, fp x, fp* y_out, g1a* pi_out) {
+  dpoly p = dp_new(n);
+  memcpy(p.c, c, sizeof(fp) * n);
+  dp_trim(&p);
+  fp y = (fp){{0, 0, 0, 0}};
+  for (int i = p.n; i-- > 0;) y = f_add(&FR, f_mul(&FR, y, x), p.c[i]);
+  /* numerator = p - y (trimmed), q = numerator / (X - x) by long division */
+  dpoly num = dp_new(p.n > 0 ? p.n : 1);
+  if (p.n > 0) memcpy(num.c, p.c, sizeof(fp) * (size_t)p.n);
+  num.c[0] = f_sub(&FR, num.c[0], y);
+  dp_trim(&num);
+  dpoly q = dp_new(num.n > 1 ? num.n - 1 : 0);
+  {
+    fp carry = (fp){{0, 0, 0, 0}};
+    for (int i = num.n - 1; i >= 1; i--) {
+      carry = f_add(&FR, num.c[i], f_mul(&FR, carry, x));
+      q.c[i - 1] = carry;
+    }
+  }
+  dp_trim(&q);
+  /* assert!(&q * &denominator == numerator) (kzg.rs:85) */
+  dpoly den = dp_new(2);
+  den.c[0] = f_sub(&FR, (fp){{0, 0, 0, 0}}, x);
+  den.c[1] = f_one(&FR);
+  dpoly chk = dp_mul(&q, &den);
+  int ok = chk.n == num.n;
+  for (int i = 0; ok && i < num.n; i++) ok = f_eq(chk.c[i], num.c[i]);
+  if (!ok && num.n > 0) abort(); /* the reference panics */
+  g1j acc = msm_ark(bases, q.c, (size_t)q.n);
+  *pi_out = j_to_affine(&acc);
+  *y_out = y;
+  dp_free(&p);
+  dp_free(&num);
+  dp_free(&q);
+  dp_free(&den);
+  dp_free(&chk);
+}
+int oc_mle_open_ref(int nvars, const uint64_t* poly, const uint64_t* point, const uint64_t tau[4],
+                    uint8_t state[32], double* seconds, uint64_t out_eval[4],
+                    uint64_t out_scomm_xy[8], uint8_t* out_scomm_inf, uint64_t out_y[16],
+                    uint64_t out_pi_xy[32], uint8_t out_pi_inf[4]) {
+  const int N = 1 << nvars;
+  fp tauf;
+  memcpy(tauf.v, tau, 32);
+  g1a* bases = (g1a*)malloc(sizeof(g1a) * (size_t)(N > 1 ? N : 2));
+  gen_srs(tauf, (size_t)(N > 1 ? N : 2), bases);
+  const fp* r = (const fp*)point;
+  const double t0 = now_s();
+  /* compute_pr: evaluations on the domain, IFFT */
+  dom d = dom_new(N);
+  fp* pr = (fp*)malloc(sizeof(fp) * N);
+  {
+    fp g = f_one(&FR);
+    for (int k = 0; k < N; k++) {
+      pr[k] = eval_pr_c(r, nvars, g);
+      g = f_mul(&FR, g, d.g);
+    }
+    fft_inplace(pr, d.lg, d.gi);
+    for (int k = 0; k < N; k++) pr[k] = f_mul(&FR, pr[k], d.size_inv);
+  }
+  fp ev = (fp){{0, 0, 0, 0}};
+  for (int i = 0; i < N; i++) ev = f_add(&FR, ev, f_mul(&FR, ((const fp*)poly)[i], pr[i]));
+  /* compute_s_polynomial */
+  dpoly p1 = dp_new(N), p2 = dp_new(N), p1r = dp_new(N), p2r = dp_new(N);
+  for (int i = 0; i < N; i++) {
+    p1.c[i] = ((const fp*)poly)[i];
+    p2.c[i] = pr[i];
+    p1r.c[N - 1 - i] = ((const fp*)poly)[i];
+    p2r.c[N - 1 - i] = pr[i];
+  }
+  dp_trim(&p1);
+  dp_trim(&p2);
+  dp_trim(&p1r);
+  dp_trim(&p2r);
+  dpoly a = dp_mul(&p1, &p2r), b = dp_mul(&p1r, &p2);
+  dpoly h = dp_add(&a, &b);
+  const int hl = 2 * N - 1;
+  fp* hc = (fp*)calloc((size_t)hl, sizeof(fp));
+  memcpy(hc, h.c, sizeof(fp) * (size_t)(h.n < hl ? h.n : hl));
+  dpoly S = dp_new(N > 1 ? N - 1 : 0);
+  if (N > 1) memcpy(S.c, hc + N, sizeof(fp) * (size_t)(N - 1));
+  dp_trim(&S);
+  g1j sacc = msm_ark(bases, S.c, (size_t)S.n);
+  g1a scomm = j_to_affine(&sacc);
+  /* transcript: point (Vec<Fr>), evaluation, s_comm; draw r (mlpcs.rs:100-107) */
+  {
+    uint8_t* msg = (uint8_t*)malloc(8 + 32 * (size_t)nvars);
+    for (int i = 0; i < 8; i++) msg[i] = (uint8_t)((uint64_t)nvars >> (8 * i));
+    for (int i = 0; i < nvars; i++) fr_bytes(r[i], msg + 8 + 32 * i);
+    tr_append(state, msg, 8 + 32 * (size_t)nvars);
+    free(msg);
+    uint8_t b32[32], b64[64];
+    fr_bytes(ev, b32);
+    tr_append(state, b32, 32);
+    g1_ser_c(&scomm, b64);
+    tr_append(state, b64, 64);
+  }
+  const fp x = tr_draw_fr(state), xi = f_inv(&FR, x);
+  fp ys[4];
+  g1a pis[4];
+  kzg_open_c(bases, (const fp*)poly, N, x, &ys[0], &pis[0]);
+  kzg_open_c(bases, (const fp*)poly, N, xi, &ys[1], &pis[1]);
+  kzg_open_c(bases, S.c, S.n, x, &ys[2], &pis[2]);
+  kzg_open_c(bases, S.c, S.n, xi, &ys[3], &pis[3]);
+  *seconds = now_s() - t0;
+  memcpy(out_eval, ev.v, 32);
+  memcpy(out_scomm_xy, scomm.x.v, 32);
+  memcpy(out_scomm_xy + 4, scomm.y.v, 32);
+  *out_scomm_inf = (uint8_t)scomm.inf;
+  for (int k = 0; k < 4; k++) {
+    memcpy(out_y + 4 * k, ys[k].v, 32);
+    memcpy(out_pi_xy + 8 * k, pis[k].x.v, 32);
+    memcpy(out_pi_xy + 8 * k + 4, pis[k].y.v, 32);
+    out_pi_inf[k] = (uint8_t)pis[k].inf;
+  }
+  free(pr);
+  free(hc);
+  dp_free(&p1);
+  dp_free(&p2);
+  dp_free(&p1r);
+  dp_free(&p2r);
+  dp_free(&a);
+  dp_free(&b);
+  dp_free(&h);
+  dp_free(&S);
+  free(bases);
+  return 0;
+}

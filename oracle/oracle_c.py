@@ -189,6 +189,37 @@ def bench_msm_arrays_mt(xy, inf, scalars, nthreads):
     return tm.value, (list(out), oinf.value)
 
 
+def mle_open_ref(nvars: int, poly, point, tau: int, state: bytes):
+    """C restatement of MLEvalProof::prove (mlpcs.rs:83-124) with the reference's
+    data flow; bases [tau^i] g.  Returns (proof dict, new state, seconds)."""
+    P64, P8 = C.POINTER(C.c_uint64), C.POINTER(C.c_uint8)
+    pa = np.array([_mont(x, R_MOD) for x in poly], dtype=np.uint64).reshape(-1, 4)
+    pt = np.array([_mont(x, R_MOD) for x in point] or [[0, 0, 0, 0]],
+                  dtype=np.uint64).reshape(-1, 4)
+    st = (C.c_uint8 * 32)(*state)
+    sec = C.c_double()
+    ev, sc, y, pi = (C.c_uint64 * 4)(), (C.c_uint64 * 8)(), (C.c_uint64 * 16)(), (C.c_uint64 * 32)()
+    sci, pii = C.c_uint8(), (C.c_uint8 * 4)()
+    lib().oc_mle_open_ref(nvars, pa.ctypes.data_as(P64), pt.ctypes.data_as(P64),
+                          (C.c_uint64 * 4)(*_mont(tau, R_MOD)), st, C.byref(sec), ev, sc,
+                          C.byref(sci), y, pi, pii)
+    g1 = lambda xy, inf: None if inf else (_unmont(list(xy)[:4], P_MOD), _unmont(list(xy)[4:8], P_MOD))
+    out = {"evaluation": _unmont(list(ev), R_MOD), "s_comm": g1(sc, sci.value),
+           "y": [_unmont(list(y)[4 * k:4 * k + 4], R_MOD) for k in range(4)],
+           "proof": [g1(list(pi)[8 * k:8 * k + 8], pii[k]) for k in range(4)]}
+    return out, bytes(st), sec.value
+
+
+def bench_mle_open_ref(log_n: int, seed: int = 0x5155494C4C):
+    """timed C MLEvalProof::prove at 2^log_n (random poly / point, fixed tau)"""
+    import random
+    rnd = random.Random(seed)
+    poly = [rnd.randrange(R_MOD) for _ in range(1 << log_n)]
+    point = [rnd.randrange(R_MOD) for _ in range(log_n)]
+    _, _, sec = mle_open_ref(log_n, poly, point, 0x5155494C4C2D53525321, bytes(32))
+    return sec
+
+
 def bench_sumcheck_ref(log_n: int, seed: int = 0x5155494C4C):
     s = C.c_double()
     lib().oc_bench_sumcheck_ref(log_n, seed, C.byref(s))

@@ -104,3 +104,24 @@ def test_c_msm_mt_matches_single_thread():
     _, _, single = oc.bench_msm_arrays(xy, inf, s)
     _, multi = oc.bench_msm_arrays_mt(xy, inf, s, 4)
     assert single == multi
+
+
+@pytest.mark.parametrize("nv", [0, 1, 3, 6])
+def test_c_mle_open_matches_oracle(nv):
+    """oc_mle_open_ref (the C restatement of MLEvalProof::prove used as the
+    ML-open CPU baseline) gives the Python oracle's proof and transcript state"""
+    import random
+    rnd = random.Random(nv)
+    R = o.R_MOD
+    poly = [rnd.randrange(R) for _ in range(1 << nv)]
+    pt = [rnd.randrange(R) for _ in range(nv)]
+    tau = 0x5155494C4C2D53525321
+    t = o.Transcript(b"mle_c")
+    st0 = bytes(t.state)
+    pr = o.MLEvalProof.prove(poly, pt, o.KZG(max(2, 1 << nv), tau), t)
+    out, st, _ = oc.mle_open_ref(nv, poly, pt, tau, st0)
+    assert out["evaluation"] == pr.evaluation and out["s_comm"] == pr.s_comm
+    assert st == bytes(t.state)
+    ops = (pr.poly_opening, pr.poly_opening_inv, pr.s_opening, pr.s_opening_inv)
+    assert out["y"] == [op[1] for op in ops]
+    assert out["proof"] == [op[2] for op in ops]
