@@ -292,7 +292,9 @@ QG_HD F29<C> mulsub29(const F29<C>& a, const F29<C>& b, const F29<C>& c, const F
 // product itself is the compiler's v_mad_u64_u32.
 __device__ __forceinline__ uint64_t mad_vv(uint32_t a, uint32_t b, uint64_t c) {
   uint64_t r = (uint64_t)a * b + c;
+#ifndef QG_MAD_PLAIN
   asm("" : "+v"(r));
+#endif
   return r;
 }
 __device__ __forceinline__ uint64_t mad_vs(uint32_t a, uint32_t b, uint64_t c) {
@@ -300,7 +302,9 @@ __device__ __forceinline__ uint64_t mad_vs(uint32_t a, uint32_t b, uint64_t c) {
 }
 __device__ __forceinline__ int64_t mad_i_vv(int32_t a, int32_t b, int64_t c) {
   int64_t r = (int64_t)a * b + c;
+#ifndef QG_MAD_PLAIN
   asm("" : "+v"(r));
+#endif
   return r;
 }
 __device__ __forceinline__ int64_t mad_u_signed(uint32_t a, uint32_t b, int64_t c) {

@@ -12,6 +12,9 @@ ROOT = os.path.dirname(os.path.dirname(os.path.dirname(os.path.abspath(__file__)
 sys.path.insert(0, os.path.join(ROOT, "quill-zkvm_amd"))
 sys.path.insert(0, os.path.join(ROOT, "oracle"))
 
+if os.environ.get("QG_LIB"):  # A/B builds of the library (micro benchmark only)
+    import quill_amd._lib as _L  # noqa: E402
+    _L.LIB_PATH = os.path.abspath(os.environ["QG_LIB"])
 import quill_amd as q  # noqa: E402
 import oracle_c as oc  # noqa: E402
 
