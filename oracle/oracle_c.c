@@ -1400,38 +1400,36 @@ static void kzg_open_c(const g1a* bases, const fp* c, int n, fp x, fp* y_out, g1
   dp_free(&den);
   dp_free(&chk);
 }
-int oc_mle_open_ref(int nvars, const uint64_t* poly, const uint64_t* point, const uint64_t tau[4],
-                    uint8_t state[32], double* seconds, uint64_t out_eval[4],
-                    uint64_t out_scomm_xy[8], uint8_t* out_scomm_inf, uint64_t out_y[16],
-                    uint64_t out_pi_xy[32], uint8_t out_pi_inf[4]) {
-  const int N = 1 << nvars;
-  fp tauf;
-  memcpy(tauf.v, tau, 32);
-  g1a* bases = (g1a*)malloc(sizeof(g1a) * (size_t)(N > 1 ? N : 2));
-  gen_srs(tauf, (size_t)(N > 1 ? N : 2), bases);
-  const fp* r = (const fp*)point;
-  const double t0 = now_s();
+/* the prove over given bases: poly has n coefficients, the point nvars
+ * coordinates (Montgomery); outputs evaluation, s_comm, four (y, proof) */
+static void mle_open_core(const g1a* bases, const fp* poly, size_t n, const fp* r, int nvars,
+                          uint8_t state[32], fp* ev_out, g1a* scomm_out, fp ys[4], g1a pis[4],
+                          fp* x_out) {
+  const size_t N = (size_t)1 << nvars;
+  const size_t M = n > N ? n : N;
   /* compute_pr: evaluations on the domain, IFFT */
-  dom d = dom_new(N);
+  dom d = dom_new((int)N);
   fp* pr = (fp*)malloc(sizeof(fp) * N);
   {
     fp g = f_one(&FR);
-    for (int k = 0; k < N; k++) {
+    for (size_t k = 0; k < N; k++) {
       pr[k] = eval_pr_c(r, nvars, g);
       g = f_mul(&FR, g, d.g);
     }
     fft_inplace(pr, d.lg, d.gi);
-    for (int k = 0; k < N; k++) pr[k] = f_mul(&FR, pr[k], d.size_inv);
+    for (size_t k = 0; k < N; k++) pr[k] = f_mul(&FR, pr[k], d.size_inv);
   }
   fp ev = (fp){{0, 0, 0, 0}};
-  for (int i = 0; i < N; i++) ev = f_add(&FR, ev, f_mul(&FR, ((const fp*)poly)[i], pr[i]));
-  /* compute_s_polynomial */
-  dpoly p1 = dp_new(N), p2 = dp_new(N), p1r = dp_new(N), p2r = dp_new(N);
-  for (int i = 0; i < N; i++) {
-    p1.c[i] = ((const fp*)poly)[i];
-    p2.c[i] = pr[i];
-    p1r.c[N - 1 - i] = ((const fp*)poly)[i];
-    p2r.c[N - 1 - i] = pr[i];
+  for (size_t i = 0; i < (n < N ? n : N); i++) ev = f_add(&FR, ev, f_mul(&FR, poly[i], pr[i]));
+  /* compute_s_polynomial with both vectors padded to M */
+  dpoly p1 = dp_new((int)M), p2 = dp_new((int)M), p1r = dp_new((int)M), p2r = dp_new((int)M);
+  for (size_t i = 0; i < M; i++) {
+    const fp a = i < n ? poly[i] : (fp){{0, 0, 0, 0}};
+    const fp b = i < N ? pr[i] : (fp){{0, 0, 0, 0}};
+    p1.c[i] = a;
+    p2.c[i] = b;
+    p1r.c[M - 1 - i] = a;
+    p2r.c[M - 1 - i] = b;
   }
   dp_trim(&p1);
   dp_trim(&p2);
@@ -1439,14 +1437,14 @@ int oc_mle_open_ref(int nvars, const uint64_t* poly, const uint64_t* point, cons
   dp_trim(&p2r);
   dpoly a = dp_mul(&p1, &p2r), b = dp_mul(&p1r, &p2);
   dpoly h = dp_add(&a, &b);
-  const int hl = 2 * N - 1;
-  fp* hc = (fp*)calloc((size_t)hl, sizeof(fp));
-  memcpy(hc, h.c, sizeof(fp) * (size_t)(h.n < hl ? h.n : hl));
-  dpoly S = dp_new(N > 1 ? N - 1 : 0);
-  if (N > 1) memcpy(S.c, hc + N, sizeof(fp) * (size_t)(N - 1));
+  const size_t hl = 2 * M - 1;
+  fp* hc = (fp*)calloc(hl, sizeof(fp));
+  if (h.n > 0) memcpy(hc, h.c, sizeof(fp) * ((size_t)h.n < hl ? (size_t)h.n : hl));
+  dpoly S = dp_new(M > 1 ? (int)(M - 1) : 0);
+  if (M > 1) memcpy(S.c, hc + M, sizeof(fp) * (M - 1));
   dp_trim(&S);
   g1j sacc = msm_ark(bases, S.c, (size_t)S.n);
-  g1a scomm = j_to_affine(&sacc);
+  const g1a scomm = j_to_affine(&sacc);
   /* transcript: point (Vec<Fr>), evaluation, s_comm; draw r (mlpcs.rs:100-107) */
   {
     uint8_t* msg = (uint8_t*)malloc(8 + 32 * (size_t)nvars);
@@ -1461,23 +1459,13 @@ int oc_mle_open_ref(int nvars, const uint64_t* poly, const uint64_t* point, cons
     tr_append(state, b64, 64);
   }
   const fp x = tr_draw_fr(state), xi = f_inv(&FR, x);
-  fp ys[4];
-  g1a pis[4];
-  kzg_open_c(bases, (const fp*)poly, N, x, &ys[0], &pis[0]);
-  kzg_open_c(bases, (const fp*)poly, N, xi, &ys[1], &pis[1]);
+  if (x_out) *x_out = x;
+  kzg_open_c(bases, poly, (int)n, x, &ys[0], &pis[0]);
+  kzg_open_c(bases, poly, (int)n, xi, &ys[1], &pis[1]);
   kzg_open_c(bases, S.c, S.n, x, &ys[2], &pis[2]);
   kzg_open_c(bases, S.c, S.n, xi, &ys[3], &pis[3]);
-  *seconds = now_s() - t0;
-  memcpy(out_eval, ev.v, 32);
-  memcpy(out_scomm_xy, scomm.x.v, 32);
-  memcpy(out_scomm_xy + 4, scomm.y.v, 32);
-  *out_scomm_inf = (uint8_t)scomm.inf;
-  for (int k = 0; k < 4; k++) {
-    memcpy(out_y + 4 * k, ys[k].v, 32);
-    memcpy(out_pi_xy + 8 * k, pis[k].x.v, 32);
-    memcpy(out_pi_xy + 8 * k + 4, pis[k].y.v, 32);
-    out_pi_inf[k] = (uint8_t)pis[k].inf;
-  }
+  *ev_out = ev;
+  *scomm_out = scomm;
   free(pr);
   free(hc);
   dp_free(&p1);
@@ -1488,6 +1476,281 @@ int oc_mle_open_ref(int nvars, const uint64_t* poly, const uint64_t* point, cons
   dp_free(&b);
   dp_free(&h);
   dp_free(&S);
+}
+
+static void mle_out(const fp* ev, const g1a* scomm, const fp ys[4], const g1a pis[4],
+                    uint64_t out_eval[4], uint64_t out_scomm_xy[8], uint8_t* out_scomm_inf,
+                    uint64_t out_y[16], uint64_t out_pi_xy[32], uint8_t out_pi_inf[4]) {
+  memcpy(out_eval, ev->v, 32);
+  memcpy(out_scomm_xy, scomm->x.v, 32);
+  memcpy(out_scomm_xy + 4, scomm->y.v, 32);
+  *out_scomm_inf = (uint8_t)scomm->inf;
+  for (int k = 0; k < 4; k++) {
+    memcpy(out_y + 4 * k, ys[k].v, 32);
+    memcpy(out_pi_xy + 8 * k, pis[k].x.v, 32);
+    memcpy(out_pi_xy + 8 * k + 4, pis[k].y.v, 32);
+    out_pi_inf[k] = (uint8_t)pis[k].inf;
+  }
+}
+
+int oc_mle_open_ref(int nvars, const uint64_t* poly, const uint64_t* point, const uint64_t tau[4],
+                    uint8_t state[32], double* seconds, uint64_t out_eval[4],
+                    uint64_t out_scomm_xy[8], uint8_t* out_scomm_inf, uint64_t out_y[16],
+                    uint64_t out_pi_xy[32], uint8_t out_pi_inf[4]) {
+  const size_t N = (size_t)1 << nvars;
+  fp tauf;
+  memcpy(tauf.v, tau, 32);
+  g1a* bases = (g1a*)malloc(sizeof(g1a) * (N > 1 ? N : 2));
+  gen_srs(tauf, N > 1 ? N : 2, bases);
+  const double t0 = now_s();
+  fp ev, ys[4];
+  g1a scomm, pis[4];
+  mle_open_core(bases, (const fp*)poly, N, (const fp*)point, nvars, state, &ev, &scomm, ys, pis,
+                NULL);
+  *seconds = now_s() - t0;
+  mle_out(&ev, &scomm, ys, pis, out_eval, out_scomm_xy, out_scomm_inf, out_y, out_pi_xy,
+          out_pi_inf);
   free(bases);
+  return 0;
+}
+
+/* ---------------------------------------------------------------- HyperPlonk building blocks
+ * The heavy steps of HyperPlonk::prove (proof.rs:145-301) with the reference's
+ * data flow, driven by oracle/hyperplonk_c.py (which keeps the transcript
+ * order of the Python restatement).  Field inputs and outputs are CANONICAL
+ * little-endian limbs (the driver converts nothing per element); every
+ * function converts to Montgomery internally.  One cached SRS ([tau^i] g). */
+static g1a* g_srs = NULL;
+static size_t g_srs_n = 0;
+
+static fp canon_in(const uint64_t* v) {
+  fp x;
+  memcpy(x.v, v, 32);
+  return f_to_mont(&FR, x);
+}
+static void canon_out(fp x, uint64_t* v) {
+  x = f_from_mont(&FR, x);
+  memcpy(v, x.v, 32);
+}
+static fp* canon_vec(const uint64_t* v, size_t n) {
+  fp* r = (fp*)malloc(sizeof(fp) * (n ? n : 1));
+  for (size_t i = 0; i < n; i++) r[i] = canon_in(v + 4 * i);
+  return r;
+}
+
+int oc_srs_set(const uint64_t tau_canon[4], size_t n) {
+  free(g_srs);
+  g_srs = (g1a*)malloc(sizeof(g1a) * (n ? n : 1));
+  gen_srs(canon_in(tau_canon), n, g_srs);
+  g_srs_n = n;
+  return 0;
+}
+
+/* KZG::commit = msm_unchecked over the cached SRS (kzg.rs:61-73) */
+int oc_commit(const uint64_t* coeffs, size_t n, uint64_t out_xy[8], uint8_t* out_inf) {
+  if (n > g_srs_n) return -1;
+  fp* c = canon_vec(coeffs, n);
+  g1j acc = msm_ark(g_srs, c, n);
+  g1a a = j_to_affine(&acc);
+  memcpy(out_xy, a.x.v, 32);
+  memcpy(out_xy + 4, a.y.v, 32);
+  *out_inf = (uint8_t)a.inf;
+  free(c);
+  return 0;
+}
+
+/* MLEvalProof::prove over the cached SRS; outputs canonical field elements
+ * and Montgomery G1 coordinates (like oc_mle_open_ref) */
+int oc_mle_open(const uint64_t* poly, size_t n, const uint64_t* point, int nvars,
+                uint8_t state[32], uint64_t out_eval[4], uint64_t out_scomm_xy[8],
+                uint8_t* out_scomm_inf, uint64_t out_y[16], uint64_t out_pi_xy[32],
+                uint8_t out_pi_inf[4], uint64_t out_x[4]) {
+  const size_t N = (size_t)1 << nvars;
+  if ((n > N ? n : N) > g_srs_n) return -1;
+  fp* p = canon_vec(poly, n);
+  fp* r = canon_vec(point, (size_t)nvars);
+  fp ev, ys[4];
+  g1a scomm, pis[4];
+  fp x;
+  mle_open_core(g_srs, p, n, r, nvars, state, &ev, &scomm, ys, pis, &x);
+  canon_out(x, out_x);
+  mle_out(&ev, &scomm, ys, pis, out_eval, out_scomm_xy, out_scomm_inf, out_y, out_pi_xy,
+          out_pi_inf);
+  for (int k = 0; k < 4; k++) canon_out(ys[k], out_y + 4 * k);
+  canon_out(ev, out_eval);
+  free(p);
+  free(r);
+  return 0;
+}
+
+/* postfix programs: (op, arg) pairs, 0 INPUT, 1 CONST, 2 ADD, 3 MUL */
+static fp expr_eval_scalar(const uint32_t* prog, int len, const fp* consts, const fp* vals) {
+  fp st[64];
+  int sp = 0;
+  for (int i = 0; i < len; i++) {
+    const uint32_t op = prog[2 * i], arg = prog[2 * i + 1];
+    if (op == 0) st[sp++] = vals[arg];
+    else if (op == 1) st[sp++] = consts[arg];
+    else {
+      const fp b = st[--sp], a = st[--sp];
+      st[sp++] = op == 2 ? f_add(&FR, a, b) : f_mul(&FR, a, b);
+    }
+  }
+  return st[0];
+}
+/* evaluate_expr_poly (virtual_polynomial.rs:300-320) on the pair's linear polys */
+static dpoly expr_eval_poly(const uint32_t* prog, int len, const fp* consts, const dpoly* lin) {
+  dpoly st[64];
+  int sp = 0;
+  for (int i = 0; i < len; i++) {
+    const uint32_t op = prog[2 * i], arg = prog[2 * i + 1];
+    if (op == 0) {
+      st[sp++] = dp_clone(&lin[arg]);
+    } else if (op == 1) {
+      dpoly c = dp_new(1);
+      c.c[0] = consts[arg];
+      dp_trim(&c);
+      st[sp++] = c;
+    } else {
+      dpoly b = st[--sp], a = st[--sp];
+      st[sp++] = op == 2 ? dp_add(&a, &b) : dp_mul(&a, &b);
+      dp_free(&a);
+      dp_free(&b);
+    }
+  }
+  return st[0];
+}
+
+/* SumcheckProof::prove (sumcheck.rs:28-114), reference-structured, any
+ * expression: per pair every table becomes low + X (high - low), the message is
+ * the sum of evaluate_expr_poly over the pairs; all tables fold by r.  coeffs:
+ * nvars x maxw canonical (trimmed length in lens); point canonical; evaluation. */
+int oc_sumcheck_ref_expr(int nvars, int ntab, const uint64_t* tables, const uint32_t* prog,
+                         int plen, const uint64_t* consts, int nconsts, const uint64_t claimed[4],
+                         uint8_t state[32], int maxw, uint64_t* coeffs, uint32_t* lens,
+                         uint64_t* point, uint64_t evaluation[4]) {
+  size_t N = (size_t)1 << nvars;
+  fp** gs = (fp**)malloc(sizeof(fp*) * (ntab ? ntab : 1));
+  for (int i = 0; i < ntab; i++) gs[i] = canon_vec(tables + 4 * N * i, N);
+  fp* cs = canon_vec(consts, (size_t)nconsts);
+  uint8_t m8[8], b32[32];
+  for (int i = 0; i < 8; i++) m8[i] = (uint8_t)((uint64_t)nvars >> (8 * i));
+  tr_append(state, m8, 8);
+  fr_bytes(canon_in(claimed), b32);
+  tr_append(state, b32, 32);
+  dpoly* lin = (dpoly*)malloc(sizeof(dpoly) * (ntab ? ntab : 1));
+  int rc = 0;
+  for (int j = 0; j < nvars; j++) {
+    const size_t half = N >> 1;
+    dpoly msg = dp_new(0);
+    for (size_t p = 0; p < half; p++) {
+      for (int i = 0; i < ntab; i++) {
+        lin[i] = dp_new(2);
+        lin[i].c[0] = gs[i][2 * p];
+        lin[i].c[1] = f_sub(&FR, gs[i][2 * p + 1], gs[i][2 * p]);
+        dp_trim(&lin[i]);
+      }
+      dpoly v = expr_eval_poly(prog, plen, cs, lin);
+      dpoly nm = dp_add(&msg, &v);
+      dp_free(&msg);
+      dp_free(&v);
+      msg = nm;
+      for (int i = 0; i < ntab; i++) dp_free(&lin[i]);
+    }
+    if (msg.n > maxw) {
+      rc = -1;
+      dp_free(&msg);
+      break;
+    }
+    /* append_serializable(&poly): u64 length + coefficients */
+    uint8_t* buf = (uint8_t*)malloc(8 + 32 * (size_t)msg.n);
+    for (int i = 0; i < 8; i++) buf[i] = (uint8_t)((uint64_t)msg.n >> (8 * i));
+    for (int i = 0; i < msg.n; i++) fr_bytes(msg.c[i], buf + 8 + 32 * i);
+    tr_append(state, buf, 8 + 32 * (size_t)msg.n);
+    free(buf);
+    lens[j] = (uint32_t)msg.n;
+    for (int i = 0; i < maxw; i++)
+      canon_out(i < msg.n ? msg.c[i] : (fp){{0, 0, 0, 0}}, coeffs + 4 * ((size_t)j * maxw + i));
+    dp_free(&msg);
+    const fp r = tr_draw_fr(state);
+    canon_out(r, point + 4 * j);
+    for (int i = 0; i < ntab; i++)
+      for (size_t p = 0; p < half; p++)
+        gs[i][p] = f_add(&FR, gs[i][2 * p], f_mul(&FR, r, f_sub(&FR, gs[i][2 * p + 1], gs[i][2 * p])));
+    N = half;
+  }
+  if (rc == 0) {
+    fp* vals = (fp*)malloc(sizeof(fp) * (ntab ? ntab : 1));
+    for (int i = 0; i < ntab; i++) vals[i] = gs[i][0];
+    canon_out(expr_eval_scalar(prog, plen, cs, vals), evaluation);
+    free(vals);
+  }
+  for (int i = 0; i < ntab; i++) free(gs[i]);
+  free(gs);
+  free(cs);
+  free(lin);
+  return rc;
+}
+
+/* logup_column (multiset_check.rs:43-95): out = m(x) / (beta + h(x)); batch
+ * inversion; -2 on a zero denominator (the reference's inverse().unwrap()) */
+int oc_logup_expr(int ntab, size_t n, const uint64_t* tables, const uint32_t* hprog, int hlen,
+                  const uint64_t* hconsts, int hn, const uint32_t* mprog, int mlen,
+                  const uint64_t* mconsts, int mn, const uint64_t beta[4], uint64_t* out) {
+  fp** gs = (fp**)malloc(sizeof(fp*) * (ntab ? ntab : 1));
+  for (int i = 0; i < ntab; i++) gs[i] = canon_vec(tables + 4 * n * i, n);
+  fp* hc = canon_vec(hconsts, (size_t)hn);
+  fp* mc = canon_vec(mconsts, (size_t)mn);
+  const fp b = canon_in(beta);
+  fp* den = (fp*)malloc(sizeof(fp) * (n ? n : 1));
+  fp* pre = (fp*)malloc(sizeof(fp) * (n ? n : 1));
+  fp* vals = (fp*)malloc(sizeof(fp) * (ntab ? ntab : 1));
+  fp acc = f_one(&FR);
+  int rc = 0;
+  for (size_t i = 0; i < n; i++) {
+    for (int t = 0; t < ntab; t++) vals[t] = gs[t][i];
+    den[i] = f_add(&FR, b, expr_eval_scalar(hprog, hlen, hc, vals));
+    if (f_is_zero(den[i])) rc = -2;
+    acc = f_mul(&FR, acc, den[i]);
+    pre[i] = acc;
+  }
+  if (rc == 0) {
+    fp inv = f_inv(&FR, acc);
+    for (size_t i = n; i-- > 0;) {
+      fp v = f_mul(&FR, inv, i ? pre[i - 1] : f_one(&FR));
+      inv = f_mul(&FR, inv, den[i]);
+      if (mprog && mlen) {
+        for (int t = 0; t < ntab; t++) vals[t] = gs[t][i];
+        v = f_mul(&FR, v, expr_eval_scalar(mprog, mlen, mc, vals));
+      }
+      canon_out(v, out + 4 * i);
+    }
+  }
+  for (int i = 0; i < ntab; i++) free(gs[i]);
+  free(gs);
+  free(hc);
+  free(mc);
+  free(den);
+  free(pre);
+  free(vals);
+  return rc;
+}
+
+/* fast_eq_eval_hypercube (eq_eval.rs:6-31), canonical in / out */
+int oc_eq_table(const uint64_t* point, int n, uint64_t* out) {
+  fp* e = (fp*)malloc(sizeof(fp) << n);
+  e[0] = f_one(&FR);
+  size_t len = 1;
+  for (int i = n - 1; i >= 0; i--) {
+    const fp r = canon_in(point + 4 * i), omr = f_sub(&FR, f_one(&FR), r);
+    for (size_t k = len; k-- > 0;) {
+      const fp v = e[k];
+      e[2 * k] = f_mul(&FR, v, omr);
+      e[2 * k + 1] = f_mul(&FR, v, r);
+    }
+    len <<= 1;
+  }
+  for (size_t k = 0; k < len; k++) canon_out(e[k], out + 4 * k);
+  free(e);
   return 0;
 }

@@ -50,6 +50,16 @@ def lib():
                                            U64P, C.POINTER(C.c_uint32), U64P, U64P]
         L.oc_bench_sumcheck_ref.argtypes = [C.c_int, C.c_uint64, C.POINTER(C.c_double)]
         L.oc_bench_sumcheck_mt.argtypes = [C.c_int, C.c_uint64, C.c_int, C.POINTER(C.c_double)]
+        U8P, U32P = C.POINTER(C.c_uint8), C.POINTER(C.c_uint32)
+        L.oc_srs_set.argtypes = [U64P, C.c_size_t]
+        L.oc_commit.argtypes = [U64P, C.c_size_t, U64P, U8P]
+        L.oc_mle_open.argtypes = [U64P, C.c_size_t, U64P, C.c_int, U8P, U64P, U64P, U8P, U64P,
+                                  U64P, U8P, U64P]
+        L.oc_sumcheck_ref_expr.argtypes = [C.c_int, C.c_int, U64P, U32P, C.c_int, U64P, C.c_int,
+                                           U64P, U8P, C.c_int, U64P, U32P, U64P, U64P]
+        L.oc_logup_expr.argtypes = [C.c_int, C.c_size_t, U64P, U32P, C.c_int, U64P, C.c_int,
+                                    U32P, C.c_int, U64P, C.c_int, U64P, U64P]
+        L.oc_eq_table.argtypes = [U64P, C.c_int, U64P]
         _lib = L
     return _lib
 

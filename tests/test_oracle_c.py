@@ -125,3 +125,32 @@ def test_c_mle_open_matches_oracle(nv):
     ops = (pr.poly_opening, pr.poly_opening_inv, pr.s_opening, pr.s_opening_inv)
     assert out["y"] == [op[1] for op in ops]
     assert out["proof"] == [op[2] for op in ops]
+
+
+@pytest.mark.parametrize("rows", [8, 32])
+def test_c_hyperplonk_matches_oracle(rows):
+    """hyperplonk_c.c_backend (the C5 CPU baseline: commitments, openings,
+    sumchecks, Logup columns and eq tables in C) proves exactly what the pure
+    Python restatement proves: same commitments, messages, openings, final state"""
+    import hyperplonk_c as hc
+    import hyperplonk_oracle as ho
+    tau = 0x48595045524C4F4E4B
+    cws = [ho.fibonacci_circuit_and_trace(rows), ho.modified_fibonacci_circuit_and_trace(rows)]
+    pcs = o.KZG(max(c.num_cols() * c.num_rows() for c, _ in cws), tau)
+    hp = ho.HyperPlonk.preprocess([c for c, _ in cws], pcs)
+    p1, t1 = hp.prove(pcs, [w for _, w in cws])
+    with hc.c_backend(tau, pcs.max_degree + 1):
+        p2, t2 = hp.prove(pcs, [w for _, w in cws])
+    assert t1.state == t2.state
+    assert p1.witness_commitment == p2.witness_commitment
+    for a, b in zip(p1.trace_proofs, p2.trace_proofs):
+        assert a.zero_check_proof.sumcheck_proof.r_polys == b.zero_check_proof.sumcheck_proof.r_polys
+        ma, mb = a.permutation_check_proof, b.permutation_check_proof
+        assert (ma.denom_left_commitment, ma.denom_right_commitment) == \
+            (mb.denom_left_commitment, mb.denom_right_commitment)
+        for x, y in zip(a.openings_zero_check + [a.opening_id, a.opening_permutation_trace],
+                        b.openings_zero_check + [b.opening_id, b.opening_permutation_trace]):
+            assert (x.evaluation, x.s_comm, x.poly_opening, x.s_opening_inv) == \
+                (y.evaluation, y.s_comm, y.poly_opening, y.s_opening_inv)
+    # the backend is restored
+    assert o.KZG.commit is not hc._commit
