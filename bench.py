@@ -55,7 +55,7 @@ def parse():
                     help="config C5: HyperPlonk prove, fibonacci + modified fibonacci traces "
                          "at 2^k rows (0: skip)")
     ap.add_argument("--no-cpu-baseline", action="store_true")
-    ap.add_argument("--cpu-hp-rows-log", type=int, default=10,
+    ap.add_argument("--cpu-hp-rows-log", type=int, default=12,
                     help="rows (log2) of the C5 CPU-baseline sample (HyperPlonk prove in C)")
     ap.add_argument("--cpu-sample-log", type=int, default=20,
                     help="log2 size of the CPU-baseline MSM sample (a prefix of the workload)")

@@ -524,22 +524,28 @@ static void s_poly_device(qg_ctx* ctx, const Fr* f, size_t nf, const Fr* g, size
   Fr* twM = ctx->scratch_as<Fr>("ntt_twM", n);
   Fr *tw, *twi;
   ntt_twiddles(ctx, logn, &tw, &twi);
-  // w^{j(M-1)} n^-1 2^266 for j < n: powers of w^{M-1} (x 2^256), then x n^-1 2^271 via mul29
-  const Fr w = root_of_unity(logn);
-  const Fr wM = fpow_small(w, (uint64_t)(M - 1));
-  const int K = 64;
-  hipLaunchKernelGGL(k_powers_ml, dim3(div_up(div_up(n, K), 256)), dim3(256), 0, ctx->stream, wM,
-                     n, K, twM);
-  QG_LAUNCH_CHECK();
-  const Fr ninv_plain = from_mont(finv(from_u64<FrP>(n)));
-  const Fr cM = ml_plain_mul(ninv_plain, pow2_mod_plain<FrP>(271));
-  L9 c9{};
-  {
-    const R29 t = to29(cM);
-    for (int i = 0; i < 9; i++) c9.v[i] = t.l[i];
+  // w^{j(M-1)} n^-1 2^266 for j < n: powers of w^{M-1} (x 2^256), then x n^-1 2^271 via mul29.
+  // Depends on (logn, M) only: cached per context like the twiddles.
+  const std::string twm_memo = std::to_string(logn) + ":" + std::to_string(M) + "@" +
+                               std::to_string((uintptr_t)twM);
+  if (ctx->memo["ntt_twM"] != twm_memo) {
+    const Fr w = root_of_unity(logn);
+    const Fr wM = fpow_small(w, (uint64_t)(M - 1));
+    const int K = 64;
+    hipLaunchKernelGGL(k_powers_ml, dim3(div_up(div_up(n, K), 256)), dim3(256), 0, ctx->stream, wM,
+                       n, K, twM);
+    QG_LAUNCH_CHECK();
+    const Fr ninv_plain = from_mont(finv(from_u64<FrP>(n)));
+    const Fr cM = ml_plain_mul(ninv_plain, pow2_mod_plain<FrP>(271));
+    L9 c9{};
+    {
+      const R29 t = to29(cM);
+      for (int i = 0; i < 9; i++) c9.v[i] = t.l[i];
+    }
+    hipLaunchKernelGGL(k_fr_to261, dim3(div_up(n, 256)), dim3(256), 0, ctx->stream, twM, n, c9);
+    QG_LAUNCH_CHECK();
+    ctx->memo["ntt_twM"] = twm_memo;
   }
-  hipLaunchKernelGGL(k_fr_to261, dim3(div_up(n, 256)), dim3(256), 0, ctx->stream, twM, n, c9);
-  QG_LAUNCH_CHECK();
   // forward DIF of f and g (zero-extended), bit-reversed outputs
   ntt_run(ctx, true, f, nf, F, tw, logn, 0, 0, nullptr);
   if (eq_z && ((size_t)1 << nz) == ng && (int)nz < logn) {
