@@ -47,14 +47,25 @@ namespace qg {
 // Phase timestamps (s_memrealtime, 100 MHz) for latency work: build with
 // -DQG_SC_TRACE (make trace) and read them with qg_debug_sc_trace.
 #ifdef QG_SC_TRACE
-__device__ unsigned long long g_sc_trace[2048];
+__device__ unsigned long long g_sc_trace[2048 + 4 * 1536];
 #define SC_TR(idx)                                                   \
   do {                                                               \
     if (threadIdx.x == 0 && (idx) < 2048) g_sc_trace[idx] = wall_clock64(); \
   } while (0)
+// per-block (start, sweep end, CU id) of big rounds 0..3, blocks < 512
+#define SC_TB(j, k)                                                                   \
+  do {                                                                                \
+    if (threadIdx.x == 0 && (j) < 4 && blockIdx.x < 512) {                            \
+      g_sc_trace[2048 + (j) * 1536 + 3 * blockIdx.x + (k)] = wall_clock64();          \
+      if ((k) == 0) g_sc_trace[2048 + (j) * 1536 + 3 * blockIdx.x + 2] = __smid();    \
+    }                                                                                 \
+  } while (0)
 #else
 #define SC_TR(idx) \
   do {             \
+  } while (0)
+#define SC_TB(j, k) \
+  do {              \
   } while (0)
 #endif
 
@@ -782,6 +793,7 @@ __global__ void __launch_bounds__(SC_BLOCK)
   const uint32_t tr = 1024 + 16 * j;
   const bool fold = j > 0;
   if (blockIdx.x == 0) SC_TR(tr + 0);
+  SC_TB(j, 0);
   sop_load<NP>(sp, spg, h, loc == nullptr);
   R29 r = R29::zero();
   if (fold) {
@@ -804,6 +816,7 @@ __global__ void __launch_bounds__(SC_BLOCK)
   sweep_pairs<K, NP, PURE, PF>(tb, j, fold, r, npairs, (size_t)blockIdx.x * SC_BLOCK + tid,
                            (size_t)gridDim.x * SC_BLOCK, sp, h, acc);
   if (blockIdx.x == 0) SC_TR(tr + 1);
+  SC_TB(j, 1);
   block_sums29<NP>(acc, np, red, res);
   if (tid < np) partial[(size_t)blockIdx.x * NP + tid] = from29(canon29(res[tid]));
   __syncthreads();
@@ -1951,7 +1964,7 @@ extern "C" {
 
 #ifdef QG_SC_TRACE
 int qg_debug_sc_trace(uint64_t* out, size_t n) {
-  if (n > 2048) n = 2048;
+  if (n > 2048 + 4 * 1536) n = 2048 + 4 * 1536;
   return hipMemcpyFromSymbol(out, HIP_SYMBOL(g_sc_trace), n * 8) == hipSuccess ? QG_OK : QG_ERR_DEVICE;
 }
 #endif
