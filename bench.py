@@ -128,6 +128,16 @@ def measure_traffic(args):
 TAU = 0x5155494C4C2D53525321  # fixed synthetic trapdoor
 
 
+_T0 = time.perf_counter()
+
+
+def _progress(rank, msg):
+    """one stderr line per bench leg (rank 0): keeps long runs visibly alive;
+    stdout carries only the JSON line"""
+    if rank == 0:
+        print(f"[bench {time.perf_counter() - _T0:7.1f}s] {msg}", file=sys.stderr, flush=True)
+
+
 def main():
     args = parse()
     if args.traffic_probe:
@@ -169,11 +179,13 @@ def main():
         dev.attach_comm(rank, world, obj[0])
 
     n = 1 << args.log_msm
+    _progress(rank, f"SRS generation 2^{args.log_msm}")
     t0 = time.perf_counter()
     srs = q.Srs.generate(dev, TAU, n, offset=rank * n)
     scalars = q.DeviceVec(dev, n).fill_random(0x5155494C4C + 2 + rank)
     setup_s = time.perf_counter() - t0
 
+    _progress(rank, "MSM headline")
     for _ in range(args.warmup):
         srs.msm_dev(scalars)
     dev.enable_timing(True)
@@ -248,12 +260,14 @@ def main():
     if traffic is not None:
         out["pmc"] = traffic
     if not args.no_sumcheck:
+        _progress(rank, "sumcheck")
         out["sumcheck"] = bench_sumcheck(q, dev, args, barrier_sync, max_over_ranks, rank)
         if traffic is not None and "error" not in traffic:
             tot = sum((traffic[k]["read_bytes_per_launch"] + traffic[k]["write_bytes_per_launch"])
                       * traffic[k]["launches"] for k in SC_KERNELS if k in traffic)
             out["sumcheck"]["roofline"]["traffic"] = tot
     if not args.no_scaling_modes:
+        _progress(rank, "scaling modes")
         out["msm_strong_scaling"] = bench_msm_strong(q, dev, args, barrier_sync, max_over_ranks,
                                                      rank, world, srs if world == 1 else None,
                                                      scalars if world == 1 else None)
@@ -261,14 +275,18 @@ def main():
             out["sumcheck_weak_scaling"] = bench_sumcheck(q, dev, args, barrier_sync,
                                                           max_over_ranks, rank, weak=True)
     if args.log_mle > 0:
+        _progress(rank, "ML-PCS open")
         out["mle_open"] = bench_mle(q, dev, args, barrier_sync, max_over_ranks, rank, world)
     if args.log_logup > 0:
+        _progress(rank, "Logup")
         out["logup"] = bench_logup(q, dev, args, barrier_sync, max_over_ranks, rank, world,
                                    traffic)
     if args.log_hp_rows > 0:
+        _progress(rank, "HyperPlonk")
         out["hyperplonk"] = bench_hyperplonk(q, dev, args, barrier_sync, max_over_ranks, rank,
                                              world)
     if rank == 0 and not args.no_cpu_baseline:
+        _progress(rank, "CPU baselines")
         out["cpu_baseline"] = cpu_baseline(args, srs, scalars)
         if not args.no_sumcheck:
             out["sumcheck"]["cpu_baseline"] = cpu_baseline_sumcheck(args)
