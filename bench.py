@@ -82,6 +82,10 @@ def traffic_probe(args):
     srs.msm_dev(scalars)
     srs.close()
     scalars.close()
+    # FETCH_SIZE calibration launches: known counts of random 128-B row gathers
+    # (the accumulate's pattern) and of 16-B-per-lane streaming bytes
+    import pmc_traffic
+    dev.microbench_fetch(pmc_traffic.CAL_ROWS, pmc_traffic.CAL_GATHERS)
     if not args.no_sumcheck:
         N = 1 << args.log_sumcheck
         tabs = [q.DeviceVec(dev, N).fill_random(0x5155494C4C + 3 + 7 * i) for i in range(3)]
@@ -233,6 +237,12 @@ def main():
         "roofline": {"bound": "hbm", "kernel": "msm_accumulate", "achieved": achieved,
                      "peak": HBM_PEAK_GBPS, "unit": "GB/s", "frac": achieved / HBM_PEAK_GBPS,
                      "traffic": _headline_traffic(traffic),
+                     "traffic_row_calibrated": _headline_traffic_row_calibrated(traffic),
+                     "traffic_note": "traffic: FETCH_SIZE x2 (the guide's streaming-read "
+                                     "correction) + WRITE_SIZE; traffic_row_calibrated: reads "
+                                     "rescaled so a calibration kernel's random 128-B row "
+                                     "gathers (k_msm_accumulate's load pattern) count 128 B "
+                                     "each (pmc._fetch_calibration)",
                      "algorithmic_bytes": MSM_BYTES_PER_SCALAR * n,
                      "note": "MSM is integer-VALU bound (no MFMA form): see compute"},
         "compute": {"fq_mul_per_s_peak_microbench": fq_peak,
@@ -616,6 +626,20 @@ def _headline_traffic(traffic):
     d = traffic[big]
     # per MSM: every launch of that shape in the probe belongs to its pieces
     return (d["read_bytes_per_launch"] + d["write_bytes_per_launch"]) * max(d.get("launches", 1), 1)
+
+
+def _headline_traffic_row_calibrated(traffic):
+    """the same bytes with the read side scaled by the row-gather calibration
+    (pmc_traffic.py CAL_*): random 128-B row gathers counted at 128 B each"""
+    cal = (traffic or {}).get("_fetch_calibration")
+    if not cal or "error" in traffic:
+        return None
+    shapes = [k for k in traffic if k.startswith("k_msm_accumulate@")]
+    if not shapes:
+        return None
+    d = traffic[max(shapes, key=lambda k: int(k.split("@")[1]))]
+    return ((d["read_bytes_per_launch"] * cal["gather_read_factor"] + d["write_bytes_per_launch"])
+            * max(d.get("launches", 1), 1))
 
 
 def _oracle_c():

@@ -353,6 +353,12 @@ int qg_ctx_enable_timing(qg_ctx* ctx, int enable);
  * a dependent-chain microbenchmark saturating every CU: the compute roof the
  * MSM's 11-Fq-mult-per-add cost is priced against. */
 int qg_microbench_fq_mul(qg_ctx* ctx, double* mul_per_s);
+/* FETCH_SIZE calibration for the PMC traffic figures: `gathers` random
+ * 128-B table-row gathers in k_msm_accumulate's load pattern (k_fetch_gather),
+ * then one 16-B-per-lane streaming read of the whole rows x 128-B table
+ * (k_fetch_stream); device ms of each.  Known byte counts for rocprofv3. */
+int qg_microbench_fetch(qg_ctx* ctx, size_t rows, size_t gathers, double* gather_ms,
+                        double* stream_ms);
 int qg_ctx_kernel_time(const qg_ctx* ctx, const char* name, double* total_ms, uint32_t* launches);
 
 #ifdef __cplusplus

@@ -22,6 +22,12 @@ import tempfile
 ROOT = os.path.dirname(os.path.abspath(__file__))
 FETCH_FACTOR = 2 * 1024  # KiB -> B, x2 gfx950 FETCH_SIZE half-count
 WRITE_FACTOR = 1024
+# calibration launches of the probe (qg_microbench_fetch): CAL_GATHERS random
+# 128-B row gathers from, then one streaming read of, a CAL_ROWS x 128-B table
+# (8 GiB: far past the 256 MiB Infinity Cache)
+CAL_ROWS = 1 << 26
+CAL_GATHERS = 1 << 26
+ROW_BYTES = 128
 
 
 def _read_counters(outdir):
@@ -141,7 +147,20 @@ def collect(probe_args, timeout=300):
     except Exception as e:  # reported, never substituted
         dur = {}
         out["_duration_error"] = {"error": str(e)[-300:]}
+    g, st = out.get("k_fetch_gather"), out.get("k_fetch_stream")
+    if g and st and "read_bytes_per_launch" in g and "read_bytes_per_launch" in st:
+        per_row = g["read_bytes_per_launch"] / CAL_GATHERS  # after the x2 correction
+        out["_fetch_calibration"] = {
+            "gather_rows": CAL_GATHERS, "table_bytes": CAL_ROWS * ROW_BYTES,
+            "gather_corrected_bytes_per_row": per_row,
+            "gather_read_factor": ROW_BYTES / per_row if per_row else None,
+            "stream_corrected_over_true": st["read_bytes_per_launch"] / (CAL_ROWS * ROW_BYTES),
+            "note": "corrected = FETCH_SIZE x2; stream_corrected_over_true ~1 confirms the x2 for "
+                    "16-B-per-lane streams; gather_read_factor rescales reads so one random row "
+                    "gather (five 16-B loads of a 128-B row, as msm_pt_load) counts 128 B"}
     for k, d in out.items():
+        if k.startswith("_"):
+            continue
         if k in dur and "read_bytes_per_launch" in d:
             us = dur[k][1]
             gbps = (d["read_bytes_per_launch"] + d["write_bytes_per_launch"]) / (us * 1e-6) / 1e9

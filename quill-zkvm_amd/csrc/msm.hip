@@ -575,6 +575,17 @@ QG_DEV X29 msm_partial(const X29Raw* partial, uint32_t slot) {
   return x29_acc_finish(x29_unraw(partial[slot]));
 }
 
+// entries e .. e + 3 (those < e1); one 16-B load when aligned and in range
+QG_DEV uint4 msm_entries4(const uint32_t* __restrict__ entries, uint32_t e, uint32_t e1) {
+  if ((e & 3u) == 0 && e + 4 <= e1) return *reinterpret_cast<const uint4*>(entries + e);
+  uint4 r = make_uint4(0, 0, 0, 0);
+  if (e < e1) r.x = entries[e];
+  if (e + 1 < e1) r.y = entries[e + 1];
+  if (e + 2 < e1) r.z = entries[e + 2];
+  if (e + 3 < e1) r.w = entries[e + 3];
+  return r;
+}
+
 __global__ void __launch_bounds__(MSM_BLOCK)
     k_msm_accumulate(const MsmPt* __restrict__ table, const uint32_t* __restrict__ entries,
                      const uint32_t* __restrict__ bstart, uint32_t nb, uint32_t L,
@@ -598,8 +609,16 @@ __global__ void __launch_bounds__(MSM_BLOCK)
   // rows are canonical in the R = 2^261 domain, the signed digit picks y or p - y
   X29 acc;
   bool inf = true;
-  uint32_t ent = entries[e0];
+  // entries arrive four at a time (one 16-B load per group of four, the next
+  // group in flight during the current one): a thread revisits its entry line
+  // only every few microseconds, long after L2 has evicted it, so single-entry
+  // loads refetched a whole 128-B line per entry (as many bytes as the rows)
+  uint4 cur = msm_entries4(entries, e0, e1), nxt = cur;
   for (uint32_t e = e0; e < e1; e++) {
+    const uint32_t k = (e - e0) & 3u;  // wave-uniform (same trip count per lane)
+    if (k == 0 && e + 4 < e1) nxt = msm_entries4(entries, e + 4, e1);
+    const uint32_t ent = k == 0 ? cur.x : k == 1 ? cur.y : k == 2 ? cur.z : cur.w;
+    if (k == 3) cur = nxt;
     if (e == next) {  // bucket boundary (at most a few per thread)
       msm_flush(partial, owner, t + b, b, acc, inf);
       inf = true;
@@ -610,7 +629,6 @@ __global__ void __launch_bounds__(MSM_BLOCK)
     }
     Q29 ax, ay;
     const bool pinf = msm_pt_load(table, ent & 0x7fffffffu, (ent >> 31) != 0u, ax, ay);
-    if (e + 1 < e1) ent = entries[e + 1];  // next index in flight during the add
     if (pinf) continue;
     if (inf) {
       acc.X = ax;
@@ -1185,9 +1203,75 @@ __global__ void __launch_bounds__(256) k_fq_mul_bench(Fq* io, int iters) {
   if (s == 0x12345678u) io[i & 1023].v[0] = s;  // keep live
 }
 
+// FETCH_SIZE calibration (pmc_traffic.py): a known count of random table-row
+// gathers in k_msm_accumulate's access pattern (five 16-B loads of one 128-B
+// row per lane, msm_pt_load), and a 16-B-per-lane streaming read of the table
+__global__ void __launch_bounds__(256) k_fetch_gather(const MsmPt* __restrict__ table, size_t rows,
+                                                      size_t n, uint32_t* __restrict__ sink) {
+  const size_t i = (size_t)blockIdx.x * blockDim.x + threadIdx.x;
+  if (i >= n) return;
+  uint64_t h = (i + 1) * 0x9E3779B97F4A7C15ull;
+  h ^= h >> 29;
+  h *= 0xBF58476D1CE4E5B9ull;
+  h ^= h >> 32;
+  Q29 x, y;
+  msm_pt_load(table, (uint32_t)(h % rows), (h >> 63) != 0, x, y);
+  uint32_t s = 0;
+#pragma unroll
+  for (int l = 0; l < 9; l++) s ^= x.l[l] ^ y.l[l];
+  sink[i] = s;
+}
+
+__global__ void __launch_bounds__(256) k_fetch_stream(const uint4* __restrict__ src, size_t n16,
+                                                      uint32_t* __restrict__ sink) {
+  const size_t t = (size_t)blockIdx.x * blockDim.x + threadIdx.x;
+  const size_t T = (size_t)gridDim.x * blockDim.x;
+  uint32_t s = 0;
+  for (size_t i = t; i < n16; i += T) {
+    const uint4 v = src[i];
+    s ^= v.x ^ v.y ^ v.z ^ v.w;
+  }
+  sink[t] = s;
+}
+
 }  // namespace qg
 
 extern "C" {
+
+int qg_microbench_fetch(qg_ctx* ctx, size_t rows, size_t gathers, double* gather_ms,
+                        double* stream_ms) {
+  if (!ctx || !rows || !gathers || !gather_ms || !stream_ms || rows > 0xffffffffull)
+    return QG_ERR_INVALID;
+  return qg_guard(ctx, [&] {
+    QG_HIP(hipSetDevice(ctx->device));
+    MsmPt* table = ctx->scratch_as<MsmPt>("mb_fetch_table", rows);
+    const unsigned sblocks = 256 * 8;
+    uint32_t* sink = ctx->scratch_as<uint32_t>("mb_fetch_sink", std::max<size_t>(gathers, sblocks * 256));
+    QG_HIP(hipMemsetAsync(table, 0x5a, rows * sizeof(MsmPt), ctx->stream));
+    hipEvent_t a, b, c;
+    QG_HIP(hipEventCreate(&a));
+    QG_HIP(hipEventCreate(&b));
+    QG_HIP(hipEventCreate(&c));
+    QG_HIP(hipEventRecord(a, ctx->stream));
+    hipLaunchKernelGGL(k_fetch_gather, dim3((unsigned)div_up(gathers, (size_t)256)), dim3(256), 0,
+                       ctx->stream, table, rows, gathers, sink);
+    QG_LAUNCH_CHECK();
+    QG_HIP(hipEventRecord(b, ctx->stream));
+    hipLaunchKernelGGL(k_fetch_stream, dim3(sblocks), dim3(256), 0, ctx->stream,
+                       reinterpret_cast<const uint4*>(table), rows * sizeof(MsmPt) / 16, sink);
+    QG_LAUNCH_CHECK();
+    QG_HIP(hipEventRecord(c, ctx->stream));
+    QG_HIP(hipEventSynchronize(c));
+    float m1 = 0, m2 = 0;
+    QG_HIP(hipEventElapsedTime(&m1, a, b));
+    QG_HIP(hipEventElapsedTime(&m2, b, c));
+    (void)hipEventDestroy(a);
+    (void)hipEventDestroy(b);
+    (void)hipEventDestroy(c);
+    *gather_ms = m1;
+    *stream_ms = m2;
+  });
+}
 
 int qg_microbench_fq_mul(qg_ctx* ctx, double* mul_per_s) {
   if (!ctx || !mul_per_s) return QG_ERR_INVALID;

@@ -74,6 +74,12 @@ class Device:
         check(lib().qg_microbench_fq_mul(self.h, C.byref(r)), self.h)
         return r.value
 
+    def microbench_fetch(self, rows: int, gathers: int) -> tuple:
+        """(gather ms, stream ms) of the FETCH_SIZE calibration kernels"""
+        g, t = C.c_double(), C.c_double()
+        check(lib().qg_microbench_fetch(self.h, rows, gathers, C.byref(g), C.byref(t)), self.h)
+        return g.value, t.value
+
     def kernel_time(self, name: str):
         ms = C.c_double()
         n = C.c_uint32()
