@@ -370,3 +370,11 @@ def test_mle_open_dev_matches_host_entry(dev):
     p1 = kzg.open(poly, point, t1)
     p2 = kzg.open_dev(vec, n, point, t2)
     assert p1 == p2 and t1.state == t2.state
+
+
+def test_microbench_entry_points(dev):
+    """qg_microbench_fq_mul / qg_microbench_fetch (the bench's compute peak and
+    the PMC probe's FETCH_SIZE calibration) run and report positive rates"""
+    assert dev.microbench_fq_mul() > 1e9
+    g, s = dev.microbench_fetch(1 << 16, 1 << 16)
+    assert g > 0 and s > 0
