@@ -200,6 +200,15 @@ int qg_mle_open(qg_ctx* ctx, const qg_srs* srs, const uint64_t* poly, size_t n,
 /* Same, on a device-resident evaluation vector (first n entries of `poly`). */
 int qg_mle_open_dev(qg_ctx* ctx, const qg_srs* srs, const qg_buf* poly, size_t n,
                     const uint64_t* point, size_t nvars, uint8_t state[32], qg_mle_proof* out);
+/* Same, with flags.  QG_OPEN_UNCHANGED: the caller guarantees that the first n
+ * entries of `poly` have not changed since an earlier open of this same buffer
+ * on this context; the polynomial's NTT transform from that call is then
+ * reused when the context still holds it (HyperPlonk opens its full witness
+ * once per column, proof.rs:203-224).  The proof is identical either way. */
+#define QG_OPEN_UNCHANGED 1u
+int qg_mle_open_dev_ex(qg_ctx* ctx, const qg_srs* srs, const qg_buf* poly, size_t n,
+                       const uint64_t* point, size_t nvars, uint8_t state[32], uint32_t flags,
+                       qg_mle_proof* out);
 
 /* ---------------------------------------------------------------- verifiers (host) */
 /* BN254 G2 affine points on the D-type twist E'/Fq2 (y^2 = x^3 + 3/(9 + u)):

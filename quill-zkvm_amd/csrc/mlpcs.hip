@@ -508,8 +508,11 @@ static L9 l9_of29(const Fr& x) {
 // S polynomial (M - 1 coefficients, untrimmed) of f (nf) and g (ng), device in/out.
 // eq_z (nz variables, host Montgomery): g is eq(., eq_z) over 2^nz entries, and
 // its transform comes from the product formula (k_eqdft_level) instead of an NTT.
+// reuse_f: the caller guarantees f's contents are unchanged since the last call
+// that transformed this same buffer; F is then reused when this context still
+// holds that transform (memo "ntt_F_src": source pointer, length, size, F).
 static void s_poly_device(qg_ctx* ctx, const Fr* f, size_t nf, const Fr* g, size_t ng, Fr* S,
-                          const uint64_t* eq_z = nullptr, size_t nz = 0) {
+                          const uint64_t* eq_z = nullptr, size_t nz = 0, bool reuse_f = false) {
   const size_t M = nf > ng ? nf : ng;
   if (M <= 1) return;
   QgTimed tm(ctx, "s_polynomial");
@@ -547,7 +550,13 @@ static void s_poly_device(qg_ctx* ctx, const Fr* f, size_t nf, const Fr* g, size
     ctx->memo["ntt_twM"] = twm_memo;
   }
   // forward DIF of f and g (zero-extended), bit-reversed outputs
-  ntt_run(ctx, true, f, nf, F, tw, logn, 0, 0, nullptr);
+  const std::string fkey = std::to_string((uintptr_t)f) + ":" + std::to_string(nf) + ":" +
+                           std::to_string(logn) + "@" + std::to_string((uintptr_t)F);
+  if (!(reuse_f && ctx->memo["ntt_F_src"] == fkey)) {
+    ctx->memo["ntt_F_src"].clear();
+    ntt_run(ctx, true, f, nf, F, tw, logn, 0, 0, nullptr);
+    ctx->memo["ntt_F_src"] = fkey;
+  }
   if (eq_z && ((size_t)1 << nz) == ng && (int)nz < logn) {
     // levels t = nz-1 .. 0 ping-pong between G and H (H is free until the combine),
     // ending in G (t = 0: 2^logn entries, bit-reversed order)
@@ -807,7 +816,7 @@ static void mle_open_sharded(qg_ctx* ctx, const qg_srs* srs, const Fr* dpoly, si
 // MLEvalProof::prove (mlpcs.rs:83-124) on a device-resident evaluation vector
 static void mle_open_device(qg_ctx* ctx, const qg_srs* srs, const Fr* dpoly, size_t n,
                             const uint64_t* point, size_t nvars, uint8_t state[32],
-                            qg_mle_proof* out) {
+                            qg_mle_proof* out, bool unchanged = false) {
   if (ctx->world > 1) return mle_open_sharded(ctx, srs, dpoly, n, point, nvars, state, out);
   const size_t N = (size_t)1 << nvars;
   Fr* dz = ctx->scratch_as<Fr>("mle_z", nvars ? nvars : 1);
@@ -822,7 +831,7 @@ static void mle_open_device(qg_ctx* ctx, const qg_srs* srs, const Fr* dpoly, siz
   Fr* dS = ctx->scratch_as<Fr>("mle_S", M > 1 ? M - 1 : 1);
   size_t Slen = 0;
   if (M > 1) {
-    s_poly_device(ctx, dpoly, n, dpr, N, dS, point, nvars);
+    s_poly_device(ctx, dpoly, n, dpr, N, dS, point, nvars, unchanged);
     Slen = trimmed_len(ctx, dS, M - 1);
   }
   QG_CHECK(Slen <= srs->n, QG_ERR_INVALID, "Polynomial degree exceeds max degree");
@@ -923,6 +932,20 @@ int qg_mle_open_dev(qg_ctx* ctx, const qg_srs* srs, const qg_buf* poly, size_t n
     QG_CHECK(nvars <= 30, QG_ERR_INVALID, "too many variables");
     QG_HIP(hipSetDevice(ctx->device));
     mle_open_device(ctx, srs, poly->d, n, point, nvars, state, out);
+  });
+}
+
+int qg_mle_open_dev_ex(qg_ctx* ctx, const qg_srs* srs, const qg_buf* poly, size_t n,
+                       const uint64_t* point, size_t nvars, uint8_t state[32], uint32_t flags,
+                       qg_mle_proof* out) {
+  if (!ctx || !srs || !poly || n > poly->n || (!point && nvars) || !state || !out ||
+      (flags & ~(uint32_t)QG_OPEN_UNCHANGED))
+    return QG_ERR_INVALID;
+  return qg_guard(ctx, [&] {
+    QG_CHECK(nvars <= 30, QG_ERR_INVALID, "too many variables");
+    QG_HIP(hipSetDevice(ctx->device));
+    mle_open_device(ctx, srs, poly->d, n, point, nvars, state, out,
+                    (flags & QG_OPEN_UNCHANGED) != 0);
   });
 }
 

@@ -106,6 +106,8 @@ PROTOTYPES = {
     "qg_mle_verify": (C.c_int, [C.POINTER(KzgVk), U64P, C.c_uint8, U64P, SZ,
                                 C.POINTER(MleProof), U8P, C.POINTER(C.c_int)]),
     "qg_mle_open_dev": (C.c_int, [P, P, P, SZ, U64P, SZ, U8P, C.POINTER(MleProof)]),
+    "qg_mle_open_dev_ex": (C.c_int, [P, P, P, SZ, U64P, SZ, U8P, C.c_uint32,
+                                     C.POINTER(MleProof)]),
     "qg_eq_table": (C.c_int, [P, U64P, SZ, U64P]),
     "qg_eq_table_dev": (C.c_int, [P, U64P, SZ, P]),
     "qg_s_polynomial": (C.c_int, [P, U64P, SZ, U64P, SZ, U64P]),

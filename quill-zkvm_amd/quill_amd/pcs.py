@@ -241,21 +241,25 @@ class KZG:
         return _opening(out)
 
     # MultilinearPCS::open == MLEvalProof::prove (mlpcs.rs:83-124, 191-198)
-    def open_dev(self, vec, n, eval_point, transcript: Transcript) -> MLEvalProof:
-        """open() on the first n entries of a device-resident DeviceVec"""
+    def open_dev(self, vec, n, eval_point, transcript: Transcript,
+                 unchanged: bool = False) -> MLEvalProof:
+        """open() on the first n entries of a device-resident DeviceVec.
+        unchanged=True: vec has not changed since an earlier open of it on this
+        device (qg_mle_open_dev_ex QG_OPEN_UNCHANGED: its transform is reused)"""
         pt = fr_array(eval_point) if len(eval_point) else np.zeros((1, 4), dtype=np.uint64)
         out = MleProof()
-        check(lib().qg_mle_open_dev(self.dev.h, self.srs_for(n).h, vec.h, n, u64p(pt),
-                                    len(eval_point),
-                                    transcript.c_state(), C.byref(out)), self.dev.h)
+        check(lib().qg_mle_open_dev_ex(self.dev.h, self.srs_for(n).h, vec.h, n, u64p(pt),
+                                       len(eval_point), transcript.c_state(),
+                                       1 if unchanged else 0, C.byref(out)), self.dev.h)
         return MLEvalProof(list(eval_point), fr_from_mont_limbs(list(out.evaluation)),
                            g1_from_abi(out.s_comm_xy, out.s_comm_inf),
                            _opening(out.poly_opening), _opening(out.poly_opening_inv),
                            _opening(out.s_opening), _opening(out.s_opening_inv))
 
-    def open(self, poly, eval_point, transcript: Transcript) -> MLEvalProof:
+    def open(self, poly, eval_point, transcript: Transcript,
+             unchanged: bool = False) -> MLEvalProof:
         if isinstance(poly, DeviceVec):
-            return self.open_dev(poly, len(poly), eval_point, transcript)
+            return self.open_dev(poly, len(poly), eval_point, transcript, unchanged)
         arr = fr_array(poly) if len(poly) else np.zeros((1, 4), dtype=np.uint64)
         pt = fr_array(eval_point) if len(eval_point) else np.zeros((1, 4), dtype=np.uint64)
         out = MleProof()

@@ -280,14 +280,16 @@ class HyperPlonk:
         pproof, ppoint = PermutationCheckProof.prove(store2, wv, wv, pk.id_poly,
                                                      pk.permutation_poly, transcript, pcs)
 
+        # `full` stays unchanged through these openings: its NTT transform is
+        # computed once (unchanged=True, qg_mle_open_dev_ex), proofs identical
         open_zc = []
         for col in range(cols):
             point = list(zclaim.point) + [(col >> i) & 1 for i in range(log2_cols)]
-            open_zc.append(pcs.open(full, point, transcript))
+            open_zc.append(pcs.open(full, point, transcript, unchanged=col > 0))
         open_pub = [pcs.open(p, zclaim.point, transcript) for p in pk.public_rows]
         o_id = pcs.open(pk.id_poly, ppoint, transcript)
         o_perm = pcs.open(pk.permutation_poly, ppoint, transcript)
-        o_pt = pcs.open(full, ppoint, transcript)
+        o_pt = pcs.open(full, ppoint, transcript, unchanged=True)
         for p in store.polynomials[cols + len(pk.public_rows):]:
             p.close()  # eq table (zero-check)
         for p in store2.polynomials[3:]:

@@ -372,6 +372,34 @@ def test_mle_open_dev_matches_host_entry(dev):
     assert p1 == p2 and t1.state == t2.state
 
 
+def test_mle_open_unchanged_reuses_transform(dev):
+    """qg_mle_open_dev_ex(QG_OPEN_UNCHANGED) gives the same proofs as fresh
+    openings: repeated openings of one buffer (the transform reused), an
+    interleaved opening of another buffer (the kept transform is not that
+    buffer's: recomputed), and a changed buffer opened without the flag."""
+    from quill_amd import KZG, DeviceVec, Transcript
+    rnd = random.Random(34)
+    nv = 11
+    kzg = KZG.trusted_setup(1 << nv, rnd.randrange(R), dev)
+    a = DeviceVec(dev, 1 << nv).fill_random(7)
+    b = DeviceVec(dev, 1 << nv).fill_random(8)
+    pts = [[rnd.randrange(R) for _ in range(nv)] for _ in range(4)]
+    seq = [(a, pts[0], False), (a, pts[1], True), (b, pts[2], False), (a, pts[3], True),
+           (a, pts[0], True)]
+    # the device sequence first (host-input openings in between would replace
+    # the kept transform), then the reference openings from host copies
+    t_fast, t_ref = Transcript(b"reuse"), Transcript(b"reuse")
+    fast = [(kzg.open_dev(vec, len(vec), pt, t_fast, unchanged=u), t_fast.state)
+            for vec, pt, u in seq]
+    host = {id(a): a.to_list(), id(b): b.to_list()}
+    for (vec, pt, _), (pf, st) in zip(seq, fast):
+        assert kzg.open(host[id(vec)], pt, t_ref) == pf and t_ref.state == st
+    # a changed buffer, opened without the flag, is transformed afresh
+    a.fill_random(9)
+    t1, t2 = Transcript(b"reuse2"), Transcript(b"reuse2")
+    assert kzg.open_dev(a, len(a), pts[1], t1) == kzg.open(a.to_list(), pts[1], t2)
+
+
 def test_microbench_entry_points(dev):
     """qg_microbench_fq_mul / qg_microbench_fetch (the bench's compute peak and
     the PMC probe's FETCH_SIZE calibration) run and report positive rates"""
