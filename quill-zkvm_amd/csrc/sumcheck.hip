@@ -380,20 +380,30 @@ QG_DEV void block_reduce_pts(R29 acc, uint32_t np, R29* red, R29* res) {
 
 // Sum of nrows rows of NP canonical values (row b at rows[b * NP]) -> res[t]
 // (whole block; thread = (row group, point), lazy sums)
+// All of a thread's rows (8 at 512 blocks) are in flight before any is added.
+// Measured (micro/sc_trace.py "rows-summed"): 5.7 us for 512 rows either way --
+// the time is not the load chain.
 template <int NP>
 QG_DEV void sum_rows29(const Fr* rows, uint32_t nrows, uint32_t np, R29* red, R29* res) {
-  const uint32_t t = threadIdx.x % NP;
+  constexpr int BATCH = 8;  // one round trip for 512 rows at NP = 4
+  const uint32_t t = threadIdx.x % NP, G = blockDim.x / NP;
   R29 a = R29::zero();
-  uint32_t c = 0;
   if (t < np)
-    for (uint32_t b = threadIdx.x / NP; b < nrows; b += blockDim.x / NP) {
-      a = add29(a, to29(rows[(size_t)b * NP + t]));  // canonical: < p
-      if (++c == 6) {  // limbs: 7 normalized terms stay below 2^32
-        a = red16p29<FrP>(a);
-        c = 0;
+    for (uint32_t b0 = threadIdx.x / NP; b0 < nrows; b0 += BATCH * G) {
+      Fr v[BATCH];
+#pragma unroll
+      for (int k = 0; k < BATCH; k++) {
+        const uint32_t b = b0 + k * G;
+        v[k] = b < nrows ? rows[(size_t)b * NP + t] : Fr::zero();
       }
+      // limbs: at most 7 normalized terms (< 2^29 each) between reductions
+#pragma unroll
+      for (int k = 0; k < 6; k++) a = add29(a, to29(v[k]));  // canonical: < p
+      a = red16p29<FrP>(a);
+#pragma unroll
+      for (int k = 6; k < BATCH; k++) a = add29(a, to29(v[k]));
+      a = red16p29<FrP>(a);
     }
-  a = red16p29<FrP>(a);
   block_reduce_pts<NP>(a, np, red, res);
 }
 
@@ -831,6 +841,7 @@ __global__ void __launch_bounds__(SC_BLOCK)
   if (!last) return;
   SC_TR(tr + 2);
   sum_rows29<NP>(partial, gridDim.x, np, red, res);
+  SC_TR(tr + 8);
   if (tid == 0) ro.st->ticket = 0;
   if (loc) {
     if (tid < NP) loc[tid] = tid < np ? from29(canon29(res[tid])) : Fr::zero();
@@ -956,8 +967,18 @@ __global__ void __launch_bounds__(TAIL_BLOCK)
       acc = R29::zero();
       const uint32_t t = tid % NP;
       if (t < np)
-        for (uint32_t b = tid / NP; b < nb; b += PB)
-          acc = red6p(add29(acc, to29(part[(size_t)b * NP + t])));
+        for (uint32_t b0 = tid / NP; b0 < nb; b0 += 4 * PB) {
+          // four partials in flight at once, then acc (< 2p) + 4 values (< p) < 6p
+          Fr v[4];
+#pragma unroll
+          for (int k = 0; k < 4; k++) {
+            const uint32_t b = b0 + k * PB;
+            v[k] = b < nb ? part[(size_t)b * NP + t] : Fr::zero();
+          }
+#pragma unroll
+          for (int k = 0; k < 4; k++) acc = add29(acc, to29(v[k]));
+          acc = red6p(acc);
+        }
       block_reduce_pts<NP>(acc, np, red, res);
     }
     if (writer) SC_TR(16 * j + 2);

@@ -34,7 +34,7 @@ for j in range(nv):
         continue
     t0 = buf[b]
     print(j, " ".join(f"{names_r[k]}={(buf[b + k] - t0) * tick:.2f}" for k in range(1, 8)
-                      if buf[b + k]))
+                      if buf[b + k]), f"rows-summed={(buf[b + 8] - t0) * tick:.2f}" if buf[b + 8] else "")
 names_t = ["start", "evaluated", "reduced", "interp", "hash1", "hash2", "chal", "blockred", "barrier"]
 print("tail rounds, us relative to round start")
 for j in range(nv):
