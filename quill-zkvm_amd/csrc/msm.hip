@@ -969,10 +969,12 @@ static MsmRun msm_accumulate_phase(qg_ctx* ctx, const qg_srs* srs, const Fr* d_s
     uint32_t* entries = ctx->scratch_as<uint32_t>("msm_entries", max_entries + 1);
     const int ntiles = (int)div_up(nb, SCAN_TILE);
     uint2* tile_tot = ctx->scratch_as<uint2>("msm_tiles", ntiles);
-    // entries per accumulation thread (flat chunks, k_msm_accumulate): 64 at
-    // the headline sizes, fewer while that would leave < 8 waves of threads per
-    // resident slot (256 CUs x 12 waves)
-    int elog = 6;
+    // entries per accumulation thread (flat chunks, k_msm_accumulate): 64, or
+    // 128 for the largest MSMs, fewer while that would leave < 8 waves of
+    // threads per resident slot (256 CUs x 12 waves)
+    // (128 from 2^27 entries on: 2^24 x 13 windows measured 19.92 vs 20.03 ms,
+    // fewer partials for the reduction; 2^22 is faster at 64)
+    int elog = max_entries >= ((size_t)1 << 27) ? 7 : 6;
     while (elog > 2 && (max_entries >> elog) < (size_t)ctx->num_cus() * 16 * 64 * 3) elog--;
     if (const char* ov = getenv("QG_MSM_ELOG")) elog = atoi(ov);  // tuning experiments
     QG_CHECK(elog >= 0 && elog <= 12, QG_ERR_INVALID, "QG_MSM_ELOG out of range");
