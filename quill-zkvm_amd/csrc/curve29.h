@@ -94,18 +94,38 @@ QG_HD X29 x29_add_affine(const X29& p, const A29& a) {
 // exceptional cases (doubling / cancellation) off the main path.
 #if defined(__HIP_DEVICE_COMPILE__)
 __device__ __forceinline__ bool x29_acc_madd_tp(X29& p, const Q29& ax, const Q29& ay) {
+#ifdef QG_MADD_SINGLE
   const Q29 U2 = mul29t(ax, p.ZZ);
   const Q29 S2 = mul29t(ay, p.ZZZ);
+#else
+  // independent products in interleaved pairs (field29.h mul29t2)
+  Q29 U2, S2;
+  mul29t2(ax, p.ZZ, ay, p.ZZZ, U2, S2);
+#endif
   const Q29 P = normfull29(subk29(U2, p.X, F29P<FqP>::K17));
   if (is_zero_mod29_fast<FqP, 20>(P)) return false;
   const Q29 R = norm29(subk29(S2, p.Y, F29P<FqP>::K9));
+#ifdef QG_MADD_SINGLE
   const Q29 PP = sqr29t(P);
+  const Q29 RR = sqr29t(R);
   const Q29 PPP = mul29t(P, PP);
   const Q29 Q = mul29t(p.X, PP);
-  const Q29 X3 = norm29(sub29(sub29(sub29(sqr29t(R), PPP), Q), Q));
+#else
+  Q29 PP, RR, PPP, Q;
+  sqr29t2(P, R, PP, RR);
+  mul29t2(P, PP, p.X, PP, PPP, Q);
+#endif
+  const Q29 X3 = norm29(sub29(sub29(sub29(RR, PPP), Q), Q));
   const Q29 Y3 = mulsub29t(R, norm29(subk29(Q, X3, F29P<FqP>::K17)), p.Y, PPP);
+#ifdef QG_MADD_SINGLE
   p.ZZ = mul29t(p.ZZ, PP);
   p.ZZZ = mul29t(p.ZZZ, PPP);
+#else
+  Q29 ZZ3, ZZZ3;
+  mul29t2(p.ZZ, PP, p.ZZZ, PPP, ZZ3, ZZZ3);
+  p.ZZ = ZZ3;
+  p.ZZZ = ZZZ3;
+#endif
   p.X = X3;
   p.Y = Y3;
   return true;

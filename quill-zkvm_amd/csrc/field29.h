@@ -373,6 +373,99 @@ __device__ __forceinline__ F29<C> sqr29t(const F29<C>& a) {
   return r;
 }
 
+// Two independent products with their column chains interleaved mad by mad:
+// no v_mad_u64_u32 result is read by the next instruction, so the hazard
+// s_nop gfx950 places after every dependent mad of a single chain goes away
+// (micro/pair_bench.hip: +2.5 % multiplies/s at full occupancy).  Same
+// arithmetic and operand conditions as mul29t / sqr29t.
+template <class C>
+__device__ __forceinline__ void mul29t2(const F29<C>& a, const F29<C>& b, const F29<C>& c,
+                                        const F29<C>& d, F29<C>& r1, F29<C>& r2) {
+  uint32_t m[9], n[9];
+  uint64_t x = 0, y = 0;
+#pragma unroll
+  for (int k = 0; k < 9; k++) {
+#pragma unroll
+    for (int j = 0; j < k; j++) {
+      x = mad_vv(a.l[j], b.l[k - j], x);
+      y = mad_vv(c.l[j], d.l[k - j], y);
+      x = mad_vs(m[j], F29P<C>::P.v[k - j], x);
+      y = mad_vs(n[j], F29P<C>::P.v[k - j], y);
+    }
+    x = mad_vv(a.l[k], b.l[0], x);
+    y = mad_vv(c.l[k], d.l[0], y);
+    m[k] = ((uint32_t)x * F29P<C>::INV) & M29;
+    n[k] = ((uint32_t)y * F29P<C>::INV) & M29;
+    x = mad_vs(m[k], F29P<C>::P.v[0], x);
+    y = mad_vs(n[k], F29P<C>::P.v[0], y);
+    x >>= 29;
+    y >>= 29;
+  }
+#pragma unroll
+  for (int k = 9; k < 17; k++) {
+#pragma unroll
+    for (int j = k - 8; j < 9; j++) {
+      x = mad_vv(a.l[j], b.l[k - j], x);
+      y = mad_vv(c.l[j], d.l[k - j], y);
+      x = mad_vs(m[j], F29P<C>::P.v[k - j], x);
+      y = mad_vs(n[j], F29P<C>::P.v[k - j], y);
+    }
+    r1.l[k - 9] = (uint32_t)x & M29;
+    r2.l[k - 9] = (uint32_t)y & M29;
+    x >>= 29;
+    y >>= 29;
+  }
+  r1.l[8] = (uint32_t)x;
+  r2.l[8] = (uint32_t)y;
+}
+
+template <class C>
+__device__ __forceinline__ void sqr29t2(const F29<C>& a, const F29<C>& c, F29<C>& r1,
+                                        F29<C>& r2) {
+  uint32_t a2[9], c2[9], m[9], n[9];
+#pragma unroll
+  for (int i = 0; i < 9; i++) {
+    a2[i] = a.l[i] << 1;
+    c2[i] = c.l[i] << 1;
+  }
+  uint64_t x = 0, y = 0;
+#pragma unroll
+  for (int k = 0; k < 17; k++) {
+#pragma unroll
+    for (int i = (k > 8 ? k - 8 : 0); 2 * i < k; i++) {
+      x = mad_vv(a2[i], a.l[k - i], x);
+      y = mad_vv(c2[i], c.l[k - i], y);
+    }
+    if ((k & 1) == 0) {
+      x = mad_vv(a.l[k / 2], a.l[k / 2], x);
+      y = mad_vv(c.l[k / 2], c.l[k / 2], y);
+    }
+    if (k < 9) {
+#pragma unroll
+      for (int j = 0; j < k; j++) {
+        x = mad_vs(m[j], F29P<C>::P.v[k - j], x);
+        y = mad_vs(n[j], F29P<C>::P.v[k - j], y);
+      }
+      m[k] = ((uint32_t)x * F29P<C>::INV) & M29;
+      n[k] = ((uint32_t)y * F29P<C>::INV) & M29;
+      x = mad_vs(m[k], F29P<C>::P.v[0], x);
+      y = mad_vs(n[k], F29P<C>::P.v[0], y);
+    } else {
+#pragma unroll
+      for (int j = k - 8; j < 9; j++) {
+        x = mad_vs(m[j], F29P<C>::P.v[k - j], x);
+        y = mad_vs(n[j], F29P<C>::P.v[k - j], y);
+      }
+      r1.l[k - 9] = (uint32_t)x & M29;
+      r2.l[k - 9] = (uint32_t)y & M29;
+    }
+    x >>= 29;
+    y >>= 29;
+  }
+  r1.l[8] = (uint32_t)x;
+  r2.l[8] = (uint32_t)y;
+}
+
 // mulsub29 with one signed chain per column
 template <class C>
 __device__ __forceinline__ F29<C> mulsub29t(const F29<C>& a, const F29<C>& b, const F29<C>& c,
@@ -414,6 +507,11 @@ template <class C>
 __device__ F29<C> sqr29t(const F29<C>& a);
 template <class C>
 __device__ F29<C> mulsub29t(const F29<C>& a, const F29<C>& b, const F29<C>& c, const F29<C>& d);
+template <class C>
+__device__ void mul29t2(const F29<C>& a, const F29<C>& b, const F29<C>& c, const F29<C>& d,
+                        F29<C>& r1, F29<C>& r2);
+template <class C>
+__device__ void sqr29t2(const F29<C>& a, const F29<C>& c, F29<C>& r1, F29<C>& r2);
 #endif
 
 // limb-wise sum (lazy)

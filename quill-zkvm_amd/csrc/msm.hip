@@ -586,7 +586,8 @@ QG_DEV uint4 msm_entries4(const uint32_t* __restrict__ entries, uint32_t e, uint
   return r;
 }
 
-__global__ void __launch_bounds__(MSM_BLOCK)
+// at most 128 VGPRs: four waves per SIMD (the paired multiplies need ~131)
+__global__ void __launch_bounds__(MSM_BLOCK) __attribute__((amdgpu_waves_per_eu(4)))
     k_msm_accumulate(const MsmPt* __restrict__ table, const uint32_t* __restrict__ entries,
                      const uint32_t* __restrict__ bstart, uint32_t nb, uint32_t L,
                      X29Raw* __restrict__ partial, uint32_t* __restrict__ owner) {
