@@ -1101,7 +1101,9 @@ static void msm_reduce_phase(qg_ctx* ctx, const qg_srs* srs, const std::vector<M
   QG_HIP(hipMemcpyAsync(mx.data(), d_mx, kl * sizeof(uint32_t), hipMemcpyDeviceToHost,
                         ctx->stream));
   QG_HIP(hipStreamSynchronize(ctx->stream));
-  const int slog1 = nb >= 8u * MSM_BLOCK ? 3 : 0;
+  int slog1 = nb >= 8u * MSM_BLOCK ? 3 : 0;
+  if (const char* ov = getenv("QG_MSM_SLOG1")) slog1 = atoi(ov);  // tuning experiments
+  QG_CHECK(slog1 >= 0 && slog1 <= 8, QG_ERR_INVALID, "QG_MSM_SLOG1 out of range");
   const uint32_t nred = div_up(nb, (size_t)MSM_BLOCK << slog1);
   int slog2 = 0;
   while (((size_t)MSM_BLOCK << slog2) < nred) slog2++;
