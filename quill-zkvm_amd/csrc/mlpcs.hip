@@ -323,20 +323,40 @@ __global__ void __launch_bounds__(NTT_THREADS)
   for (int k = 0; k < B; k++) {
     const int b = DIF ? B - 1 - k : k;  // mid bit of this stage
     const int s = s0 + b;
-    for (int p = (int)tid; p < T / 2; p += NTT_THREADS) {
-      const int l = p & (L - 1), q = p >> lgL;
-      const int mid0 = ((q >> b) << (b + 1)) | (q & ((1 << b) - 1));
-      const int e0 = (mid0 << lgL) | l, e1 = e0 | (1 << (b + lgL));
-      const size_t j = ((size_t)(mid0 & ((1 << b) - 1)) << s0) + lo0 + l;  // i0 mod 2^s
-      const R29 w = to29(tw[j << (logn - 1 - s)]);
-      const R29 u = lds_get29(sh, e0), v = lds_get29(sh, e1);
+    // butterflies p and p + NTT_THREADS together: their two Montgomery products
+    // run as interleaved chains (mul29t2); a lone last one alone
+    for (int p0 = (int)tid; p0 < T / 2; p0 += 2 * NTT_THREADS) {
+      const bool two = p0 + NTT_THREADS < T / 2;
+      int e0[2], e1[2];
+      R29 u[2], v[2], w[2];
+#pragma unroll
+      for (int h = 0; h < 2; h++) {
+        const int p = h && two ? p0 + NTT_THREADS : p0;
+        const int l = p & (L - 1), q = p >> lgL;
+        const int mid0 = ((q >> b) << (b + 1)) | (q & ((1 << b) - 1));
+        e0[h] = (mid0 << lgL) | l;
+        e1[h] = e0[h] | (1 << (b + lgL));
+        const size_t j = ((size_t)(mid0 & ((1 << b) - 1)) << s0) + lo0 + l;  // i0 mod 2^s
+        w[h] = to29(tw[j << (logn - 1 - s)]);
+        u[h] = lds_get29(sh, e0[h]);
+        v[h] = lds_get29(sh, e1[h]);
+      }
+      R29 t[2];
       if (DIF) {
-        lds_put29(sh, e0, red2p29(add29(u, v)));
-        lds_put29(sh, e1, mul29(sub29(u, v), w));
+        mul29t2(sub29(u[0], v[0]), w[0], sub29(u[1], v[1]), w[1], t[0], t[1]);
       } else {
-        const R29 t = mul29(v, w);
-        lds_put29(sh, e0, red2p29(add29(u, t)));
-        lds_put29(sh, e1, red6p29(sub29(u, t)));
+        mul29t2(v[0], w[0], v[1], w[1], t[0], t[1]);
+      }
+#pragma unroll
+      for (int h = 0; h < 2; h++) {
+        if (h && !two) break;
+        if (DIF) {
+          lds_put29(sh, e0[h], red2p29(add29(u[h], v[h])));
+          lds_put29(sh, e1[h], t[h]);
+        } else {
+          lds_put29(sh, e0[h], red2p29(add29(u[h], t[h])));
+          lds_put29(sh, e1[h], red6p29(sub29(u[h], t[h])));
+        }
       }
     }
     __syncthreads();
