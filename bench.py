@@ -64,6 +64,9 @@ def parse():
     ap.add_argument("--no-scaling-modes", action="store_true",
                     help="skip the strong-scaling MSM (fixed 2^log-msm total) and weak-scaling "
                          "sumcheck (2^log-sumcheck per GPU) legs")
+    ap.add_argument("--detail-out", default=os.path.join(ROOT, "gpurun_out", "bench_detail.json"),
+                    help="file for the full report (per-shape PMC tables, notes); stdout "
+                         "carries only the compact line ('' disables)")
     ap.add_argument("--traffic-probe", action="store_true", help=argparse.SUPPRESS)
     return ap.parse_args()
 
@@ -142,10 +145,54 @@ def _progress(rank, msg):
         print(f"[bench {time.perf_counter() - _T0:7.1f}s] {msg}", file=sys.stderr, flush=True)
 
 
+def launch_plan(gpus, env):
+    """What `--gpus N` means for this process: "run" (this process is one rank,
+    or the only one), "launch" (no outer launcher and N > 1: start N rank
+    processes as children), or an error string (an outer launcher whose
+    WORLD_SIZE disagrees with --gpus)."""
+    if gpus < 1:
+        return f"--gpus must be >= 1 (got {gpus})"
+    ws = env.get("WORLD_SIZE")
+    if ws is None:
+        return "launch" if gpus > 1 else "run"
+    if int(ws) != gpus:
+        return f"WORLD_SIZE={ws} but --gpus {gpus}"
+    return "run"
+
+
+def launch_cmd(gpus, argv, port):
+    """the child command of launch_plan's "launch": torch.distributed.run with
+    one process per GPU over 127.0.0.1, re-running this script with the same
+    arguments (each child then sees WORLD_SIZE == --gpus)"""
+    return [sys.executable, "-m", "torch.distributed.run", "--nnodes=1",
+            f"--nproc-per-node={gpus}", "--master-addr", "127.0.0.1", f"--master-port={port}",
+            os.path.abspath(__file__)] + list(argv)
+
+
+def _free_port():
+    import socket
+    s = socket.socket()
+    s.bind(("127.0.0.1", 0))
+    p = s.getsockname()[1]
+    s.close()
+    return p
+
+
 def main():
     args = parse()
     if args.traffic_probe:
         return traffic_probe(args)
+    plan = launch_plan(args.gpus, os.environ)
+    if plan == "launch":
+        # a fresh child per rank, started before this process makes any GPU call
+        # (never an exec); this parent only waits and returns the launcher's code
+        import subprocess
+        env = dict(os.environ)
+        env.setdefault("HSA_ENABLE_IPC_MODE_LEGACY", "0")
+        return subprocess.call(launch_cmd(args.gpus, sys.argv[1:], _free_port()), env=env)
+    if plan != "run":
+        print(f"bench.py: {plan}", file=sys.stderr)
+        return 2
     world = int(os.environ.get("WORLD_SIZE", "1"))
     rank = int(os.environ.get("RANK", "0"))
     local_rank = int(os.environ.get("LOCAL_RANK", "0"))
@@ -181,6 +228,9 @@ def main():
         obj = [q.Device.comm_unique_id() if rank == 0 else None]
         tdist.broadcast_object_list(obj, src=0)
         dev.attach_comm(rank, world, obj[0])
+    if dev.world != args.gpus:
+        print(f"bench.py: communicator world {dev.world} != --gpus {args.gpus}", file=sys.stderr)
+        return 2
 
     n = 1 << args.log_msm
     _progress(rank, f"SRS generation 2^{args.log_msm}")
@@ -223,7 +273,7 @@ def main():
         "metric": "G1 MSM scalars/sec at 2^24 + sumcheck-prover ms at 2^20 vars (1/8 GPU)",
         "value": value,
         "unit": "scalars/s",
-        "n_gpus": world,
+        "n_gpus": dev.world,
         "steps": args.steps,
         "warmup": args.warmup,
         "ms_per_step": ms_per_step,
@@ -303,12 +353,90 @@ def main():
         if args.log_mle > 0 and isinstance(out.get("mle_open"), dict):
             out["mle_open"]["cpu_baseline"] = cpu_baseline_mle(args)
     if rank == 0:
-        print(json.dumps(out))
+        write_detail(out, args.detail_out)
+        print(json.dumps(compact(out), separators=(",", ":")), flush=True)
     srs.close()
     scalars.close()
     dev.close()
     if dist is not None:
         dist.destroy_process_group()
+
+
+# ---------------------------------------------------------------- report
+# The driver parses the LAST stdout line, from a bounded tail: the line must stay
+# small (round 2's 36 KB line with the per-shape PMC tables was not parsed).
+# Everything bulky goes to --detail-out; the line keeps the headline fields,
+# roofline, compute, cpu_baseline and one summary per leg.
+LINE_MAX_BYTES = 6000
+_DROP_KEYS = {"note", "traffic_note", "frac_note", "issue_bound_note", "identity", "pmc",
+              "commitment_check", "final_transcript_state", "cpu_model", "metric_note"}
+# sections dropped (in this order) if the line is still over budget
+_SHED_ORDER = ("hbm_by_kernel", "kernels_ms", "sumcheck_weak_scaling", "logup", "mle_open",
+               "hyperplonk", "msm_host_input", "msm_strong_scaling")
+
+
+def _sig(x, digits=4):
+    """floats to `digits` significant digits (JSON bytes, not precision: the
+    full values are in --detail-out)"""
+    if isinstance(x, bool) or not isinstance(x, float):
+        return x
+    if x != x or x in (float("inf"), float("-inf")):
+        return None
+    return float(f"{x:.{digits}g}")
+
+
+def _shrink(v, depth=0):
+    if isinstance(v, dict):
+        return {k: _shrink(x, depth + 1) for k, x in v.items()
+                if k not in _DROP_KEYS and not k.endswith("_note")}
+    if isinstance(v, (list, tuple)):
+        return [_shrink(x, depth + 1) for x in v]
+    if isinstance(v, str) and len(v) > 160:
+        return v[:157] + "..."
+    return _sig(v)
+
+
+def hbm_by_kernel(pmc, top=12):
+    """{kernel: [GB/s, fraction of 8 TB/s, avg us]} for the `top` kernels of the
+    PMC probe by total time (whole-kernel keys, not per-shape)"""
+    if not isinstance(pmc, dict) or "error" in pmc:
+        return None
+    rows = [(k, d) for k, d in pmc.items()
+            if not k.startswith("_") and "@" not in k and isinstance(d, dict) and "hbm_gbps" in d]
+    rows.sort(key=lambda kd: -kd[1]["avg_us"] * kd[1].get("launches", 1))
+    return {k: [_sig(d["hbm_gbps"], 3), _sig(d["frac_hbm_peak"], 3), _sig(d["avg_us"], 4)]
+            for k, d in rows[:top]}
+
+
+def compact(out, limit=LINE_MAX_BYTES):
+    """the stdout line: `out` without notes / PMC tables, floats at 4 digits,
+    sections shed in _SHED_ORDER until it fits `limit` bytes"""
+    line = _shrink(out)
+    hk = hbm_by_kernel(out.get("pmc"))
+    if hk:
+        line["hbm_by_kernel"] = hk
+    if "pmc" in out and isinstance(out["pmc"], dict) and "error" in out["pmc"]:
+        line["pmc_error"] = str(out["pmc"]["error"])[:200]
+    line["detail"] = out.get("detail_file")
+    for key in _SHED_ORDER:
+        if len(json.dumps(line, separators=(",", ":"))) <= limit:
+            break
+        if key in line:
+            line[key] = "shed: see detail"
+    return line
+
+
+def write_detail(out, path):
+    """the full report (every PMC table and note) as a file; never fatal"""
+    if not path:
+        return
+    try:
+        os.makedirs(os.path.dirname(os.path.abspath(path)), exist_ok=True)
+        with open(path, "w") as f:
+            json.dump(out, f, indent=1)
+        out["detail_file"] = os.path.relpath(path, ROOT)
+    except OSError as e:
+        out["detail_file"] = f"unwritten: {e}"[:120]
 
 
 def bench_msm_strong(q, dev, args, barrier_sync, max_over_ranks, rank, world, srs=None,
@@ -753,4 +881,4 @@ def cpu_baseline_sumcheck(args):
 
 
 if __name__ == "__main__":
-    main()
+    sys.exit(main() or 0)

@@ -216,12 +216,21 @@ int qg_mle_open_dev_ex(qg_ctx* ctx, const qg_srs* srs, const qg_buf* poly, size_
 /* the standard generator (ark-bn254's G2Affine::generator()) */
 int qg_g2_generator(uint64_t out_xy[16]);
 /* k * Q (k: Fr, Montgomery limbs) — builds g2_points[1] = tau g2 of
- * KZG::trusted_setup (kzg.rs:52-53).  QG_ERR_INVALID off the curve. */
+ * KZG::trusted_setup (kzg.rs:52-53).  QG_ERR_INVALID off the curve or
+ * outside the prime-order subgroup ([r] Q != O; ark's Validate::Yes). */
 int qg_g2_mul(const uint64_t xy[16], uint8_t inf, const uint64_t k[4], uint64_t out_xy[16],
               uint8_t* out_inf);
-/* E::pairing(P, Q) (ark-bn254 optimal ate, called at kzg.rs:104-105): the
- * reduced pairing in Fq12 = Fq6[w]/(w^2 - v), Fq6 = Fq2[v]/(v^3 - (9 + u)):
- * out = c0.c0, c0.c1, c0.c2, c1.c0, c1.c1, c1.c2, each (re, im), Montgomery. */
+/* The reduced optimal-ate pairing used by E::pairing (called at
+ * kzg.rs:104-105): f_{6x+2,Q}(P) with Frobenius lines, raised to
+ * (p^12 - 1) / r, in Fq12 = Fq6[w]/(w^2 - v), Fq6 = Fq2[v]/(v^3 - (9 + u));
+ * out = c0.c0, c0.c1, c0.c2, c1.c0, c1.c1, c1.c2, each (re, im), Montgomery.
+ * Guaranteed: bilinear, non-degenerate, of order r, so every GT equality
+ * (KZG / ML-PCS verification equations) holds exactly when it does with
+ * ark-bn254.  NOT guaranteed: the raw GT value equals ark-bn254's
+ * `E::pairing(P, Q).0` — ark's hard-part addition chain may return a fixed
+ * power of this value (parity of raw values with ark is unpinned; compare
+ * GT elements only with each other).  G2 inputs must be on the twist and in
+ * the prime-order subgroup (QG_ERR_INVALID otherwise). */
 int qg_pairing(const uint64_t p_xy[8], uint8_t p_inf, const uint64_t q_xy[16], uint8_t q_inf,
                uint64_t out[48]);
 /* The verifier's view of KZG (kzg.rs:10-23): g1, g2 = g2_points[0],

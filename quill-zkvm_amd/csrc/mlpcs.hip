@@ -577,7 +577,7 @@ static void s_poly_device(qg_ctx* ctx, const Fr* f, size_t nf, const Fr* g, size
     ntt_run(ctx, true, f, nf, F, tw, logn, 0, 0, nullptr);
     ctx->memo["ntt_F_src"] = fkey;
   }
-  if (eq_z && ((size_t)1 << nz) == ng && (int)nz < logn) {
+  if (eq_z && nz >= 1 && ((size_t)1 << nz) == ng && (int)nz < logn) {
     // levels t = nz-1 .. 0 ping-pong between G and H (H is free until the combine),
     // ending in G (t = 0: 2^logn entries, bit-reversed order)
     for (int t = (int)nz - 1; t >= 0; t--) {

@@ -19,6 +19,7 @@
 // the reduced pairing f^((p^12 - 1)/r); ark-bn254's addition chain may return
 // a fixed power of it, which no verification equation can observe.
 #include <cstring>
+#include <mutex>
 #include <vector>
 
 #include "../../include/quill_gpu.h"
@@ -279,10 +280,41 @@ Fq fq_in(const uint64_t v[4]) {
 void fq_out(const Fq& a, uint64_t v[4]) {
   for (int i = 0; i < 4; i++) v[i] = (uint64_t)a.v[2 * i] | ((uint64_t)a.v[2 * i + 1] << 32);
 }
+// Prime-order subgroup membership of a twist point: [r - 1] Q == -Q, i.e.
+// [r] Q == O.  The twist's cofactor is not 1, and the Miller loop and the
+// line non-degeneracy assume order r, so every G2 input is checked like ark's
+// CanonicalDeserialize with Validate::Yes.  The check costs one 254-bit
+// double-and-add (a few ms on the host); verifying keys repeat across calls,
+// so the last few accepted points are remembered.
+bool g2_in_subgroup(const G2A& q) {
+  if (q.inf) return true;
+  static std::mutex mu;
+  static std::vector<std::vector<uint8_t>> seen;
+  std::vector<uint8_t> key(2 * sizeof(Fq2));
+  memcpy(key.data(), &q.x, sizeof(Fq2));
+  memcpy(key.data() + sizeof(Fq2), &q.y, sizeof(Fq2));
+  {
+    std::lock_guard<std::mutex> g(mu);
+    for (const auto& k : seen)
+      if (k == key) return true;
+  }
+  const Fr rm1 = from_mont(Fr::zero() - Fr::one());  // r - 1, plain limbs
+  const G2A t = g2_mul(q, rm1);
+  const G2A nq = g2_neg(q);
+  const bool ok = !t.inf && t.x == nq.x && t.y == nq.y;
+  if (ok) {
+    std::lock_guard<std::mutex> g(mu);
+    if (seen.size() >= 16) seen.erase(seen.begin());
+    seen.push_back(key);
+  }
+  return ok;
+}
+
 G2A g2_in(const uint64_t xy[16], uint8_t inf) {
   if (inf) return {Fq2::zero(), Fq2::zero(), true};
   G2A q{{fq_in(xy), fq_in(xy + 4)}, {fq_in(xy + 8), fq_in(xy + 12)}, false};
   QG_CHECK(g2_on_curve(q), QG_ERR_INVALID, "G2 point not on the twist curve");
+  QG_CHECK(g2_in_subgroup(q), QG_ERR_INVALID, "G2 point not in the prime-order subgroup");
   return q;
 }
 void g2_out(const G2A& q, uint64_t xy[16], uint8_t* inf) {

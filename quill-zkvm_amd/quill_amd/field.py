@@ -63,7 +63,10 @@ def fr_inv(x: int) -> int:
 
 
 def eq_eval(x, y) -> int:
-    """eq(x, y) = prod_i (x_i y_i + (1 - x_i)(1 - y_i))  (eq_eval.rs:33-43)"""
+    """eq(x, y) = prod_i (x_i y_i + (1 - x_i)(1 - y_i))  (eq_eval.rs:33-43);
+    unequal lengths raise like the reference's assert_eq! (eq_eval.rs:34)"""
+    if len(x) != len(y):
+        raise ValueError(f"eq_eval: point lengths differ ({len(x)} vs {len(y)})")
     acc = 1
     for a, b in zip(x, y):
         acc = acc * (a * b + (1 - a) * (1 - b)) % R_MOD

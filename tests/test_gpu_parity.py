@@ -247,6 +247,33 @@ def test_mle_open_verifies_with_oracle(dev):
     assert vt.state == t.state
 
 
+@pytest.mark.parametrize("n,nv", [(2, 0), (37, 0), (1 << 10, 0), (2, 1), (33, 2), (64, 3)])
+def test_mle_open_short_point_matches_oracle(dev, n, nv):
+    """Opening a vector longer than 2^|point| (mlpcs.rs:91-94, prefix semantics)
+    incl. the empty point: pr = [1] and S is built from the whole polynomial
+    (the eq-table transform must not run for nvars = 0).  Every
+    field of the proof and the transcript state equal the oracle prover's."""
+    from quill_amd import KZG, Transcript
+    rnd = random.Random(1000 * n + nv)
+    tau = rnd.randrange(R)
+    poly = [rnd.randrange(R) for _ in range(n)]
+    point = [rnd.randrange(R) for _ in range(nv)]
+    kzg = KZG.trusted_setup(n, tau, dev)
+    # a larger open first leaves stale data in the NTT scratch buffers
+    kzg.open([rnd.randrange(R) for _ in range(n)],
+             [rnd.randrange(R) for _ in range(max(1, n.bit_length() - 1))], Transcript(b"stale"))
+    t = Transcript(b"MLPCS short point")
+    proof = kzg.open(poly, point, t)
+    ot = o.Transcript(b"MLPCS short point")
+    ref = o.MLEvalProof.prove(poly, point, o.KZG(n, tau, points=[]), ot)
+    assert proof.evaluation == ref.evaluation
+    assert proof.s_comm == ref.s_comm
+    for k in ("poly_opening", "poly_opening_inv", "s_opening", "s_opening_inv"):
+        op = getattr(proof, k)
+        assert (op.x, op.y, op.proof) == tuple(getattr(ref, k)), k
+    assert t.state == ot.state
+
+
 # ---------------------------------------------------------------- sumcheck / zero-check
 @pytest.mark.parametrize("case", range(5))
 def test_sumcheck_golden(dev, case):

@@ -274,3 +274,102 @@ def test_serialize_layout_and_errors():
     off[96] ^= 1  # y += 1
     with pytest.raises(ValueError, match="not on the curve"):
         deserialize(q.KZGOpeningProof, bytes(off))
+
+
+def test_zerocheck_verify_rejects_extra_num_vars():
+    """ZeroCheckProof::verify draws num_vars challenges z and divides by
+    eq_eval(z, point), which asserts equal lengths (eq_eval.rs:34).  A proof
+    claiming one more variable than it has sumcheck rounds must raise, not be
+    accepted on a silently truncated eq."""
+    q = _q()
+    nv = 3
+    rnd = random.Random(11)
+    st = o.VirtualPolynomialStore(nv)
+    a = st.allocate_polynomial([rnd.randrange(R) for _ in range(1 << nv)])
+    b = st.allocate_polynomial([rnd.randrange(R) for _ in range(1 << nv)])
+    c = st.allocate_polynomial([0] * (1 << nv))
+    h = st.new_virtual_from_expr(o.Expr("add", o.Expr("mul", o.Expr.input(a), o.Expr.input(b)),
+                                        o.Expr("mul", o.Expr.const(R - 1), o.Expr.input(c))))
+    # a * b - c vanishes only where a * b == c: make c = a * b
+    st.polynomials[c] = [x * y % R for x, y in zip(st.polynomials[a], st.polynomials[b])]
+    oz, _ = o.ZeroCheckProof.prove(st, h, o.Transcript(b"zc_tamper"))
+    sp = oz.sumcheck_proof
+    good = q.ZeroCheckProof(nv, q.SumcheckProof(nv, sp.claimed_sum, [list(p) for p in sp.r_polys]))
+    good.verify(q.Transcript(b"zc_tamper"))
+    # the forged proof: nv + 1 challenges z drawn and num_vars = nv + 1 absorbed
+    # (so every sumcheck round checks out), but only nv rounds proved
+    t = o.Transcript(b"zc_tamper")
+    z = [t.draw_field_element() for _ in range(nv + 1)]
+    e = st.allocate_polynomial(o.fast_eq_eval_hypercube(nv, z[:nv]))
+    hh = st.new_virtual_from_virtual(h)
+    st.mul_in_place(hh, e)
+
+    class Forged(o.Transcript):
+        def append_u64(self, v):
+            super().append_u64(nv + 1 if v == nv else v)
+    ft = Forged(b"")
+    ft.state = t.state
+    fsp, _ = o.SumcheckProof.prove_fast(nv, st, hh, 0, ft)
+    bad = q.ZeroCheckProof(nv + 1, q.SumcheckProof(nv + 1, fsp.claimed_sum,
+                                                   [list(p) for p in fsp.r_polys]))
+    with pytest.raises(ValueError, match="lengths differ"):
+        bad.verify(q.Transcript(b"zc_tamper"))
+    with pytest.raises(ValueError):
+        q.field.eq_eval([1, 2], [1])
+
+
+def _twist_point_outside_subgroup():
+    """a point of E'(Fq2) (y^2 = x^3 + 3/(9+u)) whose order is not r: x = k + u
+    for the first k with x^3 + b' a square (Fq2 square root, p = 3 mod 4),
+    kept when [r] Q != O (the twist's cofactor is ~p, so almost every point)"""
+    Pm = po.P
+
+    def fsqrt(v):
+        s = pow(v, (Pm + 1) // 4, Pm)
+        return s if s * s % Pm == v % Pm else None
+
+    def f2sqrt(a):
+        a0, a1 = a
+        alpha = fsqrt((a0 * a0 + a1 * a1) % Pm)
+        if alpha is None:
+            return None
+        half = (Pm + 1) // 2
+        for d in ((a0 + alpha) * half % Pm, (a0 - alpha) * half % Pm):
+            x0 = fsqrt(d)
+            if x0:
+                x1 = a1 * pow(2 * x0, Pm - 2, Pm) % Pm
+                if po.f2_mul((x0, x1), (x0, x1)) == (a0 % Pm, a1 % Pm):
+                    return (x0, x1)
+        return None
+    for k in range(1, 200):
+        x = (k, 1)
+        y = f2sqrt(po.f2_add(po.f2_mul(po.f2_mul(x, x), x), po.B2))
+        if y is None:
+            continue
+        Q = (x, y)
+        assert po.g2_on_curve(Q)
+        acc = po.g2_add(po.g2_mul(Q, R - 1), Q)  # [r] Q
+        if acc is not None:
+            return Q
+    raise AssertionError("no twist point found")
+
+
+def test_g2_rejects_point_outside_subgroup():
+    """G2 inputs are checked for the prime-order subgroup (ark's Validate::Yes),
+    not only for the twist equation: qg_g2_mul, qg_pairing and a
+    verifying key built from published points all refuse such a point."""
+    q = _q()
+    Q = _twist_point_outside_subgroup()
+    with pytest.raises(q.QuillGpuError):
+        q.g2_mul(Q, 3)
+    with pytest.raises(q.QuillGpuError):
+        q.pairing((1, 2), Q)
+    okzg = o.KZG(4, TAU)
+    poly = [1, 2, 3]
+    ox, oy, opi = okzg.open(poly, 5)
+    vk = q.KZG.verifier(g2_points=[q.g2_generator(), Q])
+    with pytest.raises(q.QuillGpuError):
+        vk.verify_univariate(okzg.commit(poly), q.KZGOpeningProof(ox, oy, opi))
+    # subgroup points still pass (generator and a multiple)
+    g2 = q.g2_generator()
+    assert q.g2_mul(q.g2_mul(g2, 12345), 1) == q.g2_mul(g2, 12345)
