@@ -59,6 +59,9 @@ def parse():
                     help="rows (log2) of the C5 CPU-baseline sample (HyperPlonk prove in C)")
     ap.add_argument("--cpu-sample-log", type=int, default=20,
                     help="log2 size of the CPU-baseline MSM sample (a prefix of the workload)")
+    ap.add_argument("--no-host-input", dest="host_input", action="store_false",
+                    help="skip the drop-in leg: the same commitment from host memory "
+                         "(qg_kzg_commit, H2D inside the timed region)")
     ap.add_argument("--no-traffic", action="store_true",
                     help="skip the two rocprofv3 PMC passes that measure HBM traffic")
     ap.add_argument("--no-scaling-modes", action="store_true",
@@ -326,6 +329,10 @@ def main():
             tot = sum((traffic[k]["read_bytes_per_launch"] + traffic[k]["write_bytes_per_launch"])
                       * traffic[k]["launches"] for k in SC_KERNELS if k in traffic)
             out["sumcheck"]["roofline"]["traffic"] = tot
+    if args.host_input:
+        _progress(rank, "MSM from host memory")
+        out["msm_host_input"] = bench_msm_host(q, dev, args, barrier_sync, max_over_ranks, srs,
+                                               scalars, ms_per_step, res)
     if not args.no_scaling_modes:
         _progress(rank, "scaling modes")
         out["msm_strong_scaling"] = bench_msm_strong(q, dev, args, barrier_sync, max_over_ranks,
@@ -437,6 +444,30 @@ def write_detail(out, path):
         out["detail_file"] = os.path.relpath(path, ROOT)
     except OSError as e:
         out["detail_file"] = f"unwritten: {e}"[:120]
+
+
+def bench_msm_host(q, dev, args, barrier_sync, max_over_ranks, srs, scalars, resident_ms, res):
+    """The drop-in cost of KZG::commit (kzg.rs:61-73): the same 2^log-msm
+    commitment with the scalars in pageable host memory (an arkworks `&[Fr]`
+    passed to qg_kzg_commit, H2D inside the timed region), next to the
+    resident headline; the result must equal the resident commitment."""
+    n = 1 << args.log_msm
+    arr = scalars.to_numpy()  # (n, 4) Montgomery limbs: arkworks' in-memory Fr
+    steps = max(1, min(args.steps, 3))
+    got = srs.commit_array(arr, n)
+    barrier_sync()
+    t0 = time.perf_counter()
+    for _ in range(steps):
+        got = srs.commit_array(arr, n)
+    barrier_sync()
+    dt = max_over_ranks(time.perf_counter() - t0)
+    ms = dt / steps * 1e3
+    return {"ms_per_step": ms, "value": dev.world * n / (ms * 1e-3), "unit": "scalars/s",
+            "steps": steps, "input_bytes": 32 * n, "h2d_included_ms": ms - resident_ms,
+            "h2d_gbps_effective": 32 * n / ((ms - resident_ms) * 1e-3) / 1e9
+            if ms > resident_ms else None,
+            "matches_resident_commitment": got == res,
+            "note": "pageable host scalars -> qg_kzg_commit; value is never the headline"}
 
 
 def bench_msm_strong(q, dev, args, barrier_sync, max_over_ranks, rank, world, srs=None,

@@ -84,13 +84,12 @@ static unsigned sc_round_blocks(qg_ctx* ctx, size_t npairs) {
   cap = std::min<size_t>(cap, SC_MAX_BLOCKS);
   return (unsigned)std::max<size_t>(1, std::min<size_t>(cap, div_up(npairs, SC_BLOCK)));
 }
-// QG_SC_STAGED=1 selects the LDS-staged round kernels + persistent tail (k_sc_round,
-// k_sc_persist) on one GPU, for A/B runs
+// QG_SC_STAGED=1 selects the LDS-staged round kernels (k_sc_round) for the big
+// rounds on one GPU, for A/B runs
 static bool sc_use_staged() {
   static const bool v = getenv("QG_SC_STAGED") != nullptr;
   return v;
 }
-static constexpr int TAIL_BLOCK = 256;  // persistent-kernel block (one wave per SIMD: latency-bound rounds)
 static constexpr int PERS_LOG = 16;     // tables of <= 2^16 entries: rounds run in one persistent launch
 
 // device-side program image.  The header and byte arrays are copied into LDS
@@ -118,6 +117,7 @@ struct SopDev {
   L9 cr29[4];                // 2^522, 2^778 (-> r * 2^261); 2^517, 2^773 (-> r * 2^256)
   Fr coeff[SOP_MAXM];        // Montgomery coefficients (final claim on the 32-bit path)
   uint8_t is_one[SOP_MAXM];  // (final claim)
+  L9 cs29;                   // 2^(261 - e): Montgomery value -> scale S (the round claim)
 };
 static_assert(offsetof(SopDev, c29) == SOP_HDR_WORDS * 4, "SopDev layout");
 
@@ -210,6 +210,47 @@ struct TablePtrs {
   const Fr* src[8];
   Fr* dst[8];
 };
+
+// ---------------------------------------------------------------- in-launch hand-offs
+// Data handed between workgroups INSIDE one launch (partial rows, the
+// persistent tail's folded tables, the transcript state of the big rounds) is
+// stored write-through and loaded L1-bypassing: agent-scope relaxed atomics on
+// GLOBAL pointers lower to `global_store/load ... sc1` (MI355X_MICROARCH.md
+// "Valid forms", first row: one lane signals by an agent-scope atomic after
+// every storing wave's vmcnt(0) wait and a workgroup barrier; the consumer
+// polls that counter with an sc1 load and loads every handed-off byte with sc1
+// loads).  No release fence, so no `buffer_wbl2` write-back of the XCD L2's
+// dirty table lines on the critical path.
+typedef __attribute__((address_space(1))) uint64_t gu64;
+typedef __attribute__((address_space(1))) uint32_t gu32;
+
+QG_DEV Fr ld_sc1(const Fr* p) {
+  gu64* q = (gu64*)(const_cast<Fr*>(p));
+  Fr r;
+#pragma unroll
+  for (int i = 0; i < 4; i++) {
+    const uint64_t v = __hip_atomic_load(q + i, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+    r.v[2 * i] = (uint32_t)v;
+    r.v[2 * i + 1] = (uint32_t)(v >> 32);
+  }
+  return r;
+}
+QG_DEV void st_sc1(Fr* p, const Fr& x) {
+  gu64* q = (gu64*)p;
+#pragma unroll
+  for (int i = 0; i < 4; i++)
+    __hip_atomic_store(q + i, (uint64_t)x.v[2 * i] | ((uint64_t)x.v[2 * i + 1] << 32),
+                       __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+}
+QG_DEV uint32_t ld_sc1_u32(const uint32_t* p) {
+  return __hip_atomic_load((gu32*)(const_cast<uint32_t*>(p)), __ATOMIC_RELAXED,
+                           __HIP_MEMORY_SCOPE_AGENT);
+}
+QG_DEV void st_sc1_u32(uint32_t* p, uint32_t v) {
+  __hip_atomic_store((gu32*)p, v, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+}
+// every storing wave drains its sc1 stores (inline asm: the compiler cannot drop it)
+QG_DEV void drain_stores() { asm volatile("s_waitcnt vmcnt(0)" ::: "memory"); }
 
 QG_DEV Fr shfl_xor_fr(const Fr& a, int m) {
   Fr r;
@@ -394,7 +435,7 @@ QG_DEV void sum_rows29(const Fr* rows, uint32_t nrows, uint32_t np, R29* red, R2
 #pragma unroll
       for (int k = 0; k < BATCH; k++) {
         const uint32_t b = b0 + k * G;
-        v[k] = b < nrows ? rows[(size_t)b * NP + t] : Fr::zero();
+        v[k] = b < nrows ? ld_sc1(rows + (size_t)b * NP + t) : Fr::zero();
       }
       // limbs: at most 7 normalized terms (< 2^29 each) between reductions
 #pragma unroll
@@ -417,6 +458,7 @@ struct ScState {
   uint32_t err;       // persistent-kernel barrier timeout flag
   uint32_t r29[9];    // last challenge * 2^261 mod p (< 2p), the fold multiplier
   uint32_t pad[1];
+  uint32_t claim[8];  // this round's claim h_{j-1}(r_{j-1}) at scale S (big rounds, j >= 1)
 };
 
 struct RoundOut {
@@ -565,12 +607,14 @@ __global__ void __launch_bounds__(SC_BLOCK)
     for (int i = 0; i < 9; i++) r.l[i] = ro.st->r29[i];
   }
   if (pending && blockIdx.x == 0 && tid >= 64 && tid < 128) {
-    // deferred absorb of round j-1's challenge bytes (wave 1 of block 0)
+    // deferred absorb of round j-1's challenge bytes (wave 1 of block 0),
+    // handed to the last block write-through (see k_sc_big)
     if (tid - 64 < 32) fs.ab[tid - 64] = tid - 64 < 20 ? ro.st->pend[tid - 64] : 0u;
     __builtin_amdgcn_s_waitcnt(0);
     __builtin_amdgcn_wave_barrier();
-    b3_hash_quad(fs.ab, 80, ro.st->state, 8);
-    __builtin_amdgcn_fence(__ATOMIC_RELEASE, "agent");
+    b3_hash_quad(fs.ab, 80, fs.chin, 8);
+    __builtin_amdgcn_wave_barrier();
+    if (tid - 64 < 8) st_sc1_u32(&ro.st->state[tid - 64], fs.chin[tid - 64]);
   }
   __syncthreads();
   constexpr uint32_t PB = SC_BLOCK / NP;
@@ -579,24 +623,26 @@ __global__ void __launch_bounds__(SC_BLOCK)
                                (size_t)gridDim.x * PB, acc);
   if (blockIdx.x == 0) SC_TR(tr + 1);
   block_reduce_pts<NP>(acc, h.np, red, res);
-  if (tid < h.np) partial[(size_t)blockIdx.x * NP + tid] = from29(canon29(res[tid]));
+  if (tid < h.np) st_sc1(partial + (size_t)blockIdx.x * NP + tid, from29(canon29(res[tid])));
+  drain_stores();
   __syncthreads();
   if (tid == 0) {
-    __builtin_amdgcn_fence(__ATOMIC_RELEASE, "agent");
-    const uint32_t old =
-        __hip_atomic_fetch_add(&ro.st->ticket, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+    const uint32_t old = __hip_atomic_fetch_add((gu32*)&ro.st->ticket, 1u, __ATOMIC_RELAXED,
+                                                __HIP_MEMORY_SCOPE_AGENT);
     last = old + 1 == gridDim.x;
-    if (last) __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "agent");
+    __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
   }
   __syncthreads();
   if (!last) return;
   SC_TR(tr + 2);
+  __shared__ uint32_t st_in[8];
+  if (tid < 8) st_in[tid] = ld_sc1_u32(&ro.st->state[tid]);
   acc = R29::zero();
   {
     const uint32_t t = tid % NP;
     if (t < h.np)
       for (uint32_t b = tid / NP; b < gridDim.x; b += SC_BLOCK / NP)
-        acc = red6p(add29(acc, to29(partial[(size_t)b * NP + t])));
+        acc = red6p(add29(acc, to29(ld_sc1(partial + (size_t)b * NP + t))));
   }
   block_reduce_pts<NP>(acc, h.np, red, res);
   if (tid == 0) ro.st->ticket = 0;
@@ -604,7 +650,7 @@ __global__ void __launch_bounds__(SC_BLOCK)
     if (tid < NP) loc[tid] = tid < h.np ? from29(canon29(res[tid])) : Fr::zero();
     return;
   }
-  finish_core<NP>(sp, h.np, res, ro, j, fs, ro.st->state, ro.st->pend, nullptr, tr);
+  finish_core<NP>(sp, h.np, res, ro, j, fs, st_in, ro.st->pend, nullptr, tr);
   if (tid < 9) ro.st->r29[tid] = fs.r.l[tid];
   SC_TR(tr + 7);
 }
@@ -698,7 +744,7 @@ struct AllBufs {
 template <int K, int NP, bool PURE, bool PF>
 QG_DEV void sweep_pairs(const AllBufs& tb, uint32_t j, bool fold, const R29& r, size_t npairs,
                         size_t p0, size_t stride, const SopLds<NP>& sp, const SopHdr& h,
-                        R29 (&acc)[NP]) {
+                        bool skip0, R29 (&acc)[NP]) {
   const uint32_t nslots = h.nslots, np = h.np;
   uint32_t cnt = 0;
   for (size_t p = p0; p < npairs; p += stride) {
@@ -717,6 +763,7 @@ QG_DEV void sweep_pairs(const AllBufs& tb, uint32_t j, bool fold, const R29& r, 
         const R29 d = norm29(sub29(hi, lo));
 #pragma unroll
         for (int t = 0; t < NP; t++) {
+          if (t == 0 && skip0) continue;  // h(0) = claim - h(1), by the finisher
           const R29 v = at_point<NP>(lo, d, t, sp);
           prod[t] = s == 0 ? v : mul29t(prod[t], v);
         }
@@ -728,7 +775,7 @@ QG_DEV void sweep_pairs(const AllBufs& tb, uint32_t j, bool fold, const R29& r, 
       // products of >= 2 factors are < 4p: three lazy additions stay below 16p
 #pragma unroll
       for (int t = 0; t < NP; t++)
-        if ((uint32_t)t < np) acc[t] = add29(acc[t], prod[t]);
+        if ((uint32_t)t < np && !(t == 0 && skip0)) acc[t] = add29(acc[t], prod[t]);
       if (++cnt == 3) {
 #pragma unroll
         for (int t = 0; t < NP; t++) acc[t] = red16p29<FrP>(acc[t]);
@@ -759,13 +806,15 @@ QG_DEV void sweep_pairs(const AllBufs& tb, uint32_t j, bool fold, const R29& r, 
             const R29 a = pick29<K>(lo, s), d = pick29<K>(dd, s);
 #pragma unroll
             for (int t = 0; t < NP; t++) {
+              if (t == 0 && skip0) continue;
               const R29 v = at_point<NP>(a, d, t, sp);
               prod[t] = q == 0 ? v : mul29t(prod[t], v);
             }
           }
           if (!sp.skip(m) || len == 1) {
 #pragma unroll
-            for (int t = 0; t < NP; t++) prod[t] = mul29t(prod[t], sp.c29[m]);
+            for (int t = 0; t < NP; t++)
+              if (!(t == 0 && skip0)) prod[t] = mul29t(prod[t], sp.c29[m]);
           }
         }
         f += len;
@@ -773,7 +822,7 @@ QG_DEV void sweep_pairs(const AllBufs& tb, uint32_t j, bool fold, const R29& r, 
         // multiplier): three lazy additions stay below 16p
 #pragma unroll
         for (int t = 0; t < NP; t++)
-          if ((uint32_t)t < np) acc[t] = add29(acc[t], prod[t]);
+          if ((uint32_t)t < np && !(t == 0 && skip0)) acc[t] = add29(acc[t], prod[t]);
         if (++cnt == 3) {
 #pragma unroll
           for (int t = 0; t < NP; t++) acc[t] = red16p29<FrP>(acc[t]);
@@ -793,7 +842,7 @@ QG_DEV void sweep_pairs(const AllBufs& tb, uint32_t j, bool fold, const R29& r, 
 template <int K, int NP, bool PURE, bool PF>
 __global__ void __launch_bounds__(SC_BLOCK)
     k_sc_big(AllBufs tb, uint32_t j, const SopDev* __restrict__ spg, SopHdr h, size_t npairs,
-             RoundOut ro, int pending, Fr* __restrict__ partial, Fr* __restrict__ loc) {
+             RoundOut ro, int pending, Fr* __restrict__ partial, Fr* __restrict__ loc, int skip0) {
   __shared__ SopLds<NP> sp;
   __shared__ R29 red[(SC_BLOCK / 64) * NP];
   __shared__ R29 res[NP];
@@ -811,12 +860,27 @@ __global__ void __launch_bounds__(SC_BLOCK)
     for (int i = 0; i < 9; i++) r.l[i] = ro.st->r29[i];
   }
   if (pending && blockIdx.x == 0 && tid >= 64 && tid < 128) {
-    // deferred absorb of round j-1's challenge bytes (wave 1 of block 0)
+    // deferred absorb of round j-1's challenge bytes (wave 1 of block 0); the
+    // new state is handed to the last block write-through (sc1) and drained
+    // before this block's ticket
     if (tid - 64 < 32) fs.ab[tid - 64] = tid - 64 < 20 ? ro.st->pend[tid - 64] : 0u;
     __builtin_amdgcn_s_waitcnt(0);
     __builtin_amdgcn_wave_barrier();
-    b3_hash_quad(fs.ab, 80, ro.st->state, 8);
-    __builtin_amdgcn_fence(__ATOMIC_RELEASE, "agent");
+    b3_hash_quad(fs.ab, 80, fs.chin, 8);
+    __builtin_amdgcn_wave_barrier();
+    if (tid - 64 < 8) st_sc1_u32(&ro.st->state[tid - 64], fs.chin[tid - 64]);
+  }
+  if (skip0 && blockIdx.x == 0 && tid == 128) {
+    // this round's claim h_{j-1}(r_{j-1}) at scale S, for the finisher's
+    // h(0) = claim - h(1): Horner over round j-1's Montgomery coefficients
+    // (wave 2 of block 0, beside the sweep; handed over write-through)
+    const Fr* c = ro.coeffs + (size_t)(j - 1) * ro.width;
+    R29 a = to29(c[h.np - 1]);
+    for (int t = (int)h.np - 2; t >= 0; t--) a = red6p(add29(mul29(a, r), to29(c[t])));
+    R29 cs;
+#pragma unroll
+    for (int i = 0; i < 9; i++) cs.l[i] = spg->cs29.v[i];
+    st_sc1(reinterpret_cast<Fr*>(ro.st->claim), from29(canon29(red6p(mul29(a, cs)))));
   }
   __syncthreads();
   const uint32_t np = h.np;
@@ -824,30 +888,36 @@ __global__ void __launch_bounds__(SC_BLOCK)
 #pragma unroll
   for (int t = 0; t < NP; t++) acc[t] = R29::zero();
   sweep_pairs<K, NP, PURE, PF>(tb, j, fold, r, npairs, (size_t)blockIdx.x * SC_BLOCK + tid,
-                           (size_t)gridDim.x * SC_BLOCK, sp, h, acc);
+                           (size_t)gridDim.x * SC_BLOCK, sp, h, skip0 != 0, acc);
   if (blockIdx.x == 0) SC_TR(tr + 1);
   SC_TB(j, 1);
   block_sums29<NP>(acc, np, red, res);
-  if (tid < np) partial[(size_t)blockIdx.x * NP + tid] = from29(canon29(res[tid]));
+  // publish: sc1 row stores, every storing wave drains, then one ticket add
+  if (tid < np) st_sc1(partial + (size_t)blockIdx.x * NP + tid, from29(canon29(res[tid])));
+  drain_stores();
   __syncthreads();
   if (tid == 0) {
-    __builtin_amdgcn_fence(__ATOMIC_RELEASE, "agent");
-    const uint32_t old =
-        __hip_atomic_fetch_add(&ro.st->ticket, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+    const uint32_t old = __hip_atomic_fetch_add((gu32*)&ro.st->ticket, 1u, __ATOMIC_RELAXED,
+                                                __HIP_MEMORY_SCOPE_AGENT);
     last = old + 1 == gridDim.x;
-    if (last) __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "agent");
+    __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");  // no instruction: loads stay below
   }
   __syncthreads();
   if (!last) return;
   SC_TR(tr + 2);
+  __shared__ uint32_t st_in[8];
+  if (tid < 8) st_in[tid] = ld_sc1_u32(&ro.st->state[tid]);
   sum_rows29<NP>(partial, gridDim.x, np, red, res);
   SC_TR(tr + 8);
   if (tid == 0) ro.st->ticket = 0;
-  if (loc) {
+  if (loc) {  // sharded: k_sc_finish applies the claim to the global sums
     if (tid < NP) loc[tid] = tid < np ? from29(canon29(res[tid])) : Fr::zero();
     return;
   }
-  finish_core<NP>(sp, np, res, ro, j, fs, ro.st->state, ro.st->pend, nullptr, tr);
+  if (skip0 && tid == 0)
+    res[0] = red6p(sub29(to29(ld_sc1(reinterpret_cast<const Fr*>(ro.st->claim))), res[1]));
+  __syncthreads();
+  finish_core<NP>(sp, np, res, ro, j, fs, st_in, ro.st->pend, nullptr, tr);
   if (tid < 9) ro.st->r29[tid] = fs.r.l[tid];
   SC_TR(tr + 7);
 }
@@ -856,7 +926,7 @@ __global__ void __launch_bounds__(SC_BLOCK)
 template <int NP>
 __global__ void __launch_bounds__(SC_BLOCK)
     k_sc_finish(const SopDev* __restrict__ spg, SopHdr h, const Fr* __restrict__ rows,
-                uint32_t nrows, RoundOut ro, uint32_t j) {
+                uint32_t nrows, RoundOut ro, uint32_t j, int skip0) {
   __shared__ SopLds<NP> sp;
   __shared__ R29 red[(SC_BLOCK / 64) * NP];
   __shared__ R29 res[NP];
@@ -874,53 +944,108 @@ __global__ void __launch_bounds__(SC_BLOCK)
   }
   __syncthreads();
   block_reduce_pts<NP>(acc, h.np, red, res);
+  if (skip0 && tid == 0)  // h(0) = claim - h(1) on the global sums
+    res[0] = red6p(sub29(to29(*reinterpret_cast<const Fr*>(ro.st->claim)), res[1]));
+  __syncthreads();
   finish_core<NP>(sp, h.np, res, ro, j, fs, st, nullptr, ro.st->state);
   if (tid < 9) ro.st->r29[tid] = fs.r.l[tid];
 }
 
-// Grid barrier among the first n blocks (monotonic per-round counter).  Every
-// wave drains its stores, thread 0 publishes with an agent-scope release and
-// acquires after the count completes (MI355X_MICROARCH.md, inter-workgroup
-// visibility).  The spin is bounded: on timeout the error flag is raised and
-// the kernel runs on to its end (the host reports QG_ERR_DEVICE).
+// Grid barrier among the first n blocks (monotonic per-round counter): every
+// wave drains its sc1 stores, one lane adds to the counter and polls it with
+// sc1 loads, the others wait at the workgroup barrier.  Everything handed
+// across it is stored and loaded sc1 (helpers above), so no fences.  The spin
+// is bounded: on timeout the error flag is raised and the kernel runs on to
+// its end (the host reports QG_ERR_DEVICE).
 QG_DEV void grid_barrier(uint32_t* ctr, uint32_t n, uint32_t* err) {
-  __builtin_amdgcn_s_waitcnt(0);
+  drain_stores();
   __syncthreads();
   if (threadIdx.x == 0) {
-    __builtin_amdgcn_fence(__ATOMIC_RELEASE, "agent");
-    __hip_atomic_fetch_add(ctr, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+    gu32* c = (gu32*)ctr;
+    __hip_atomic_fetch_add(c, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
     uint32_t spins = 0;
-    while (__hip_atomic_load(ctr, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) < n) {
+    while (__hip_atomic_load(c, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) < n) {
       __builtin_amdgcn_s_sleep(1);
       if (++spins > (1u << 26)) {
-        __hip_atomic_store(err, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+        st_sc1_u32(err, 1u);
         break;
       }
     }
-    __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "agent");
+    __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");  // no instruction: keeps loads below
   }
   __syncthreads();
 }
 
-// Rounds j0..nvars-1 in one persistent launch.  Round j keeps the first
-// nb_j = ceil(pairs / PB) blocks (the others retire: work only shrinks); each
-// block sweeps its pairs, publishes its per-point sums, meets the others at a
-// grid barrier, then every block sums all partials and runs the (identical)
-// transcript step itself, so no second barrier or broadcast is needed.  Block
-// 0 writes the proof outputs.  Once nb_j == 1, block 0 continues alone.  The
-// transcript state, the pending absorb and r stay in LDS between rounds, and
-// the code stays hot in the instruction cache (a fresh launch per small round
-// would refetch ~45 KB of code cold).  Final fold + claim by block 0.
-// bufs: ping-pong scratch per slot (a: size >= 2^(n-j0-1), b: >= 2^(n-j0-2)).
+// ---------------------------------------------------------------------------
+// Persistent tail: rounds j0..nvars-1 in ONE launch of TAIL_BLOCK-thread workgroups,
+// one per CU.  Round j keeps nb_j = ceil(pairs / PB) blocks (PB pairs per
+// block step; the others retire), each sweeps its pairs (phase F: fold into
+// the LDS staging array F and, while other blocks read them next round, into
+// HBM with sc1 stores; phase E: thread (pair, point) evaluates h), publishes
+// its per-point sums, meets the others at the grid barrier, then every block
+// sums the partials and runs the identical transcript step — no second
+// barrier, no broadcast.  Block 0 writes the proof outputs.
+// Once a round fits one block step (nb == 1, pairs <= PB) its folded table IS
+// the staging array, so from the next round on the tables never leave LDS:
+// F ping-pongs between two arrays (the second half as large: the table halves
+// every round), no HBM round trip, no barrier.  The deferred absorb of the
+// previous challenge runs on the block's LAST wave, which has no pair work in
+// the small rounds, beside the sweep.  Final fold + claim by block 0.
+// PB is chosen at run time from the slot count (tail_pb, shared with the
+// host's grid computation) so the two staging arrays fit TAIL_FBYTES.
+static constexpr int TAIL_BLOCK = 256;
+static constexpr uint32_t TAIL_FBYTES = 100 * 1024;  // LDS for the staging arrays
+// np: the kernel's point stride NP (threads per pair), not the expression's np
+QG_HD uint32_t tail_pb(uint32_t nslots, uint32_t np) {
+  // F0: nslots x 2 PB entries, F1: nslots x PB entries, 36 B each
+  const uint32_t per = nslots ? nslots * 108u : 108u;
+  uint32_t pb = 1;
+  while (pb * 2 * per <= TAIL_FBYTES && pb * 2 * np <= (uint32_t)TAIL_BLOCK) pb *= 2;
+  return pb;
+}
+
+template <int NP>
+QG_DEV void tail_eval(const R29* F, uint32_t ss, const SopLds<NP>& sp, const SopHdr& h,
+                      uint32_t pl, uint32_t t, R29& acc) {
+  R29 sum = R29::zero();
+  uint32_t f = 0;
+  for (uint32_t m = 0; m < h.nmono; m++) {
+    const uint32_t len = sp.mono_len(m);
+    R29 prod;
+    if (len == 0) {
+      prod = sp.c29[m];
+    } else {
+      for (uint32_t q = 0; q < len; q++) {
+        const uint32_t s = sp.fac(f + q);
+        const R29 lo = F[s * ss + 2 * pl], hi = F[s * ss + 2 * pl + 1];
+        R29 v;
+        if constexpr (NP <= 4) {
+          const R29 d = norm29(sub29(hi, lo));
+          R29 a = lo;
+          if (t & 1u) a = add29(a, d);
+          if (t & 2u) a = add29(a, add29(d, d));
+          v = norm29(a);
+        } else {
+          v = norm29(add29(lo, mul29(sub29(hi, lo), sp.t29[t])));
+        }
+        prod = q == 0 ? v : mul29(prod, v);
+      }
+      if (!sp.skip(m) || len == 1) prod = mul29(prod, sp.c29[m]);
+    }
+    f += len;
+    sum = red6p(add29(sum, prod));
+  }
+  acc = red6p(add29(acc, sum));
+}
+
 template <int K, int NP>
 __global__ void __launch_bounds__(TAIL_BLOCK)
-    k_sc_persist(TablePtrs tp0, TablePtrs bufA, TablePtrs bufB, const SopDev* __restrict__ spg,
-                 SopHdr h, uint32_t nvars, uint32_t j0, int fold0, int pending0, RoundOut ro,
-                 Fr* __restrict__ partial, uint32_t* __restrict__ bar, Fr* __restrict__ final_vals,
-                 Fr* __restrict__ evaluation) {
-  constexpr uint32_t PB = TAIL_BLOCK / NP;
+    k_sc_tail(TablePtrs tp0, TablePtrs bufA, TablePtrs bufB, const SopDev* __restrict__ spg,
+              SopHdr h, uint32_t nvars, uint32_t j0, int fold0, int pending0, RoundOut ro,
+              Fr* __restrict__ partial, uint32_t* __restrict__ bar, Fr* __restrict__ final_vals,
+              Fr* __restrict__ evaluation) {
   __shared__ SopLds<NP> sp;
-  __shared__ RoundLds<K, NP, TAIL_BLOCK> L;
+  __shared__ R29 Fbuf[TAIL_FBYTES / sizeof(R29)];
   __shared__ R29 red[(TAIL_BLOCK / 64) * NP];
   __shared__ R29 res[NP];
   __shared__ FinSmem fs;
@@ -928,7 +1053,13 @@ __global__ void __launch_bounds__(TAIL_BLOCK)
   __shared__ uint32_t pend[32];
   const uint32_t tid = threadIdx.x, blk = blockIdx.x;
   const uint32_t nslots = h.nslots, np = h.np;
+  const uint32_t PB = tail_pb(nslots, NP);  // (pair, point) threads: NP per pair
+  const uint32_t t = tid % NP, pl = tid / NP;
   const bool writer = blk == 0;
+  const bool last_wave = tid >= TAIL_BLOCK - 64;
+  // F0 (slot stride 2 PB) and F1 (slot stride PB)
+  R29* const F0 = Fbuf;
+  R29* const F1 = Fbuf + (size_t)(nslots ? nslots : 1) * 2 * PB;
   sop_load<NP>(sp, spg, h, true);
   if (tid < 8) st[tid] = ro.st->state[tid];
   if (tid < 32) pend[tid] = (pending0 && tid < 20) ? ro.st->pend[tid] : 0u;
@@ -937,43 +1068,66 @@ __global__ void __launch_bounds__(TAIL_BLOCK)
 #pragma unroll
     for (int i = 0; i < 9; i++) r.l[i] = ro.st->r29[i];
   }
+  __syncthreads();
   TablePtrs cur = tp0;
   int fold = fold0, pending = pending0;
+  // where this round's source lives: HBM (cur.src) or LDS (prev, slot stride ss_prev)
+  const R29* prev = nullptr;
+  uint32_t ss_prev = 0;
+  R29* wr = F0;
+  uint32_t ss_wr = 2 * PB;
   for (uint32_t j = j0; j < nvars; j++) {
     const size_t npairs = (size_t)1 << (nvars - 1 - j);
     const uint32_t nb = (uint32_t)std::min<size_t>(gridDim.x, (npairs + PB - 1) / PB);
     if (blk >= nb) return;  // retired: every later round has fewer pairs
-#pragma unroll
-    for (int i = 0; i < 8; i++) {
-      if (tid == (uint32_t)i) {
-        L.src[i] = cur.src[i];
-        L.dst[i] = cur.dst[i];
-      }
-    }
-    __syncthreads();
+    const bool single = nb == 1 && npairs <= PB;
     if (writer) SC_TR(16 * j + 0);
-    if (pending && tid >= 64 && tid < 128) b3_hash_quad(pend, 80, st, 8);  // wave 1
+    if (pending && last_wave) b3_hash_quad(pend, 80, st, 8);  // beside the sweep
+    // ---- phase F: fold (or copy) this round's table into the staging array
     R29 acc = R29::zero();
-    round_sweep<K, NP, TAIL_BLOCK>(L, sp, h, npairs, fold != 0, r, (size_t)blk * PB,
-                                   (size_t)nb * PB, acc);
+    const size_t stride = (size_t)nb * PB;
+    for (size_t base = (size_t)blk * PB; base < npairs; base += stride) {
+      const uint32_t cnt = (uint32_t)std::min<size_t>(PB, npairs - base);
+      const uint32_t per = 2 * cnt, nitems = nslots * per;
+      for (uint32_t it = tid; it < nitems; it += TAIL_BLOCK) {
+        const uint32_t s = it / per, e = it % per;
+        const size_t idx = 2 * base + e;  // entry of this round's (folded) table
+        R29 v;
+        if (prev) {  // LDS-resident source: entries 2e, 2e+1 of the previous table
+          const R29 x0 = prev[s * ss_prev + 2 * e], x1 = prev[s * ss_prev + 2 * e + 1];
+          v = red6p(add29(x0, mul29(sub29(x1, x0), r)));
+        } else if (fold) {
+          const Fr* src = cur.src[s] + 2 * idx;
+          const R29 x0 = to29(ld_sc1(src)), x1 = to29(ld_sc1(src + 1));
+          v = red6p(add29(x0, mul29(sub29(x1, x0), r)));
+          if (!single) st_sc1(cur.dst[s] + idx, from29(v));
+        } else {
+          v = to29(ld_sc1(cur.src[s] + idx));
+        }
+        wr[s * ss_wr + e] = v;
+      }
+      __syncthreads();
+      // ---- phase E: thread (pair pl, point t)
+      if (t < np && pl < cnt) tail_eval<NP>(wr, ss_wr, sp, h, pl, t, acc);
+      if (base + stride < npairs) __syncthreads();  // the staging array is refilled
+    }
     if (writer) SC_TR(16 * j + 1);
     block_reduce_pts<NP>(acc, np, red, res);
     if (writer) SC_TR(16 * j + 7);
     if (nb > 1) {
       Fr* part = partial + (size_t)(j & 1) * gridDim.x * NP;
-      if (tid < np) part[(size_t)blk * NP + tid] = from29(canon29(res[tid]));
+      if (tid < np) st_sc1(part + (size_t)blk * NP + tid, from29(canon29(res[tid])));
       grid_barrier(bar + j, nb, &ro.st->err);
       if (writer) SC_TR(16 * j + 8);
       acc = R29::zero();
-      const uint32_t t = tid % NP;
       if (t < np)
-        for (uint32_t b0 = tid / NP; b0 < nb; b0 += 4 * PB) {
+        for (uint32_t b0 = pl; b0 < nb; b0 += 4 * (TAIL_BLOCK / NP)) {
           // four partials in flight at once, then acc (< 2p) + 4 values (< p) < 6p
           Fr v[4];
 #pragma unroll
           for (int k = 0; k < 4; k++) {
-            const uint32_t b = b0 + k * PB;
-            v[k] = b < nb ? part[(size_t)b * NP + t] : Fr::zero();
+            const uint32_t b = b0 + k * (TAIL_BLOCK / NP);
+            v[k] = b < nb ? ld_sc1(part + (size_t)b * NP + t) : Fr::zero();
           }
 #pragma unroll
           for (int k = 0; k < 4; k++) acc = add29(acc, to29(v[k]));
@@ -986,25 +1140,34 @@ __global__ void __launch_bounds__(TAIL_BLOCK)
     __syncthreads();
     r = fs.r;
     pending = 1;
-    // the folded tables written this round become the next source
-    TablePtrs nxt;
-    const TablePtrs& w = ((j - j0) & 1) ? bufB : bufA;
-    for (int i = 0; i < 8; i++) {
-      nxt.src[i] = fold ? cur.dst[i] : cur.src[i];
-      nxt.dst[i] = w.dst[i];
+    // next round's source: the staging array just written when this round was a
+    // single block step, else the HBM tables this round folded into
+    if (single) {
+      prev = wr;
+      ss_prev = ss_wr;
+      const bool w0 = wr == F0;
+      wr = w0 ? F1 : F0;
+      ss_wr = w0 ? PB : 2 * PB;
+    } else {
+      TablePtrs nxt;
+      const TablePtrs& w = ((j - j0) & 1) ? bufB : bufA;
+      for (int i = 0; i < 8; i++) {
+        nxt.src[i] = fold ? cur.dst[i] : cur.src[i];
+        nxt.dst[i] = w.dst[i];
+      }
+      cur = nxt;
     }
-    // when round j did not fold (j == 0), its source stays the source
-    cur = nxt;
     fold = 1;
   }
-  // final fold with r_{n-1} on the 32-bit path: cur.src has 2 entries per slot
+  // final fold with r_{n-1} on the 32-bit path: the last round (one pair) is
+  // always a single block step, so its two folded entries per slot are in prev
   if (tid == 0) {
     const Fr rr = fs.r256;
     Fr val[K];
 #pragma unroll
     for (int i = 0; i < K; i++) {
       if ((uint32_t)i < nslots) {
-        const Fr a = lt_p(cur.src[i][0]), b = lt_p(cur.src[i][1]);
+        const Fr a = lt_p(from29(prev[i * ss_prev])), b = lt_p(from29(prev[i * ss_prev + 1]));
         val[i] = a + rr * (b - a);
         final_vals[i] = val[i];
       } else {
@@ -1014,7 +1177,7 @@ __global__ void __launch_bounds__(TAIL_BLOCK)
     *evaluation = sop_eval_final<K>(spg, h.nmono, val);
   }
   // absorb the last challenge bytes
-  if (pending && tid >= 64 && tid < 128) b3_hash_quad(pend, 80, ro.st->state, 8);
+  if (pending && tid < 64) b3_hash_quad(pend, 80, ro.st->state, 8);
 }
 
 // ---------------------------------------------------------------------------
@@ -1287,6 +1450,7 @@ static std::shared_ptr<const ScProgram> get_program(const qg_expr_op* prog, size
   d.cr29[1] = l9_of(pow2_mod_plain<FrP>(778));
   d.cr29[2] = l9_of(pow2_mod_plain<FrP>(517));
   d.cr29[3] = l9_of(pow2_mod_plain<FrP>(773));
+  d.cs29 = l9_of(pow2_mod_plain<FrP>((uint32_t)(261 - e)));
   bool pure = d.nmono == 1 && sp.is_one[0] && sp.mono_len[0] == d.nslots && d.nslots >= 2 &&
               d.nslots == sp.degree;
   for (uint32_t f = 0; pure && f < d.nfac; f++) pure = sp.fac[f] == f;
@@ -1311,7 +1475,7 @@ static unsigned persist_grid_cap(qg_ctx* ctx, size_t cus) {
   int occ = 0;
   if (it == ctx->memo.end()) {
     QG_HIP(hipOccupancyMaxActiveBlocksPerMultiprocessor(
-        &occ, reinterpret_cast<const void*>(&k_sc_persist<K, NP>), TAIL_BLOCK, 0));
+        &occ, reinterpret_cast<const void*>(&k_sc_tail<K, NP>), TAIL_BLOCK, 0));
     ctx->memo[key] = std::to_string(occ);
   } else {
     occ = std::stoi(it->second);
@@ -1334,13 +1498,20 @@ static unsigned sc_big_blocks(qg_ctx* ctx, size_t npairs) {
   return (unsigned)std::max<size_t>(1, std::min<size_t>(cap, div_up(npairs, SC_BLOCK)));
 }
 
+// returns -1 when the staged k_sc_round must run instead, else the skip0 flag used
 template <int K, int NP>
-static bool launch_big(qg_ctx* ctx, const std::vector<const Fr*>& src, Fr* X, Fr* Y, size_t N,
+static int launch_big(qg_ctx* ctx, const std::vector<const Fr*>& src, Fr* X, Fr* Y, size_t N,
                        uint32_t j, const SopDev* d_sp, SopHdr h, size_t npairs, RoundOut ro,
                        int pending, Fr* partial, Fr* loc) {
-  if (sc_use_staged() || NP > 4) return false;
+  // rounds j >= 1: h(0) = h_{j-1}(r_{j-1}) - h(1), exact by construction (the
+  // folded table's pair sums ARE the previous message at r); round 0 evaluates
+  // every point, so a wrong caller claim still yields the reference's bytes.
+  // QG_SC_NO_SKIP0=1 evaluates t = 0 in every round (A/B runs).
+  static const bool no_skip0 = getenv("QG_SC_NO_SKIP0") != nullptr;
+  const int skip0 = (j >= 1 && h.np >= 2 && !no_skip0) ? 1 : 0;
+  if (sc_use_staged() || NP > 4) return -1;
   const bool pure = (h.pad & SOP_PURE) != 0;
-  if (!pure && K > 4) return false;
+  if (!pure && K > 4) return -1;
   AllBufs tb{};
   for (uint32_t i = 0; i < 8; i++) tb.in.src[i] = i < src.size() ? src[i] : nullptr;
   tb.X = X;
@@ -1352,15 +1523,15 @@ static bool launch_big(qg_ctx* ctx, const std::vector<const Fr*>& src, Fr* X, Fr
   static const bool pf = getenv("QG_SC_PF") != nullptr;
   if (pure && pf)
     hipLaunchKernelGGL((k_sc_big<K, 4, true, true>), dim3(blocks), dim3(SC_BLOCK), 0, ctx->stream,
-                       tb, j, d_sp, h, npairs, ro, pending, partial, loc);
+                       tb, j, d_sp, h, npairs, ro, pending, partial, loc, skip0);
   else if (pure)
     hipLaunchKernelGGL((k_sc_big<K, 4, true, false>), dim3(blocks), dim3(SC_BLOCK), 0, ctx->stream,
-                       tb, j, d_sp, h, npairs, ro, pending, partial, loc);
+                       tb, j, d_sp, h, npairs, ro, pending, partial, loc, skip0);
   else
     hipLaunchKernelGGL((k_sc_big<4, 4, false, false>), dim3(blocks), dim3(SC_BLOCK), 0, ctx->stream,
-                       tb, j, d_sp, h, npairs, ro, pending, partial, loc);
+                       tb, j, d_sp, h, npairs, ro, pending, partial, loc, skip0);
   QG_LAUNCH_CHECK();
-  return true;
+  return skip0;
 }
 
 template <int K, int NP>
@@ -1396,7 +1567,7 @@ static void run_rounds(qg_ctx* ctx, uint32_t nvars, const std::vector<const Fr*>
         const TablePtrs& d = parity ? tY : tX;
         for (int i = 0; i < 8; i++) tp.dst[i] = d.dst[i];
       }
-      if (!launch_big<K, NP>(ctx, src, X, Y, N, j, d_sp, h, npairs, ro, pending, partial, nullptr))
+      if (launch_big<K, NP>(ctx, src, X, Y, N, j, d_sp, h, npairs, ro, pending, partial, nullptr) < 0)
         hipLaunchKernelGGL((k_sc_round<K, NP>), dim3(sc_round_blocks(ctx, npairs)), dim3(SC_BLOCK),
                            0, ctx->stream, tp, d_sp, h, npairs, fold, ro, j, pending, partial,
                            (Fr*)nullptr);
@@ -1429,12 +1600,12 @@ static void run_rounds(qg_ctx* ctx, uint32_t nvars, const std::vector<const Fr*>
     }
     // persistent launch: one block per CU at most (co-residency for the grid
     // barrier), fewer when the first persistent round has fewer pair groups
-    constexpr size_t PB = TAIL_BLOCK / NP;
+    const size_t PB = tail_pb(h.nslots, NP);
     const size_t pairs0 = (N >> j) / 2;
     const unsigned grid = (unsigned)std::max<size_t>(
         1, std::min<size_t>(persist_grid_cap<K, NP>(ctx, ctx->num_cus()), (pairs0 + PB - 1) / PB));
     Fr* ppart = ctx->scratch_as<Fr>("sc_ppartial", (size_t)2 * grid * NP);
-    hipLaunchKernelGGL((k_sc_persist<K, NP>), dim3(grid), dim3(TAIL_BLOCK), 0, ctx->stream, t0,
+    hipLaunchKernelGGL((k_sc_tail<K, NP>), dim3(grid), dim3(TAIL_BLOCK), 0, ctx->stream, t0,
                        bufA, bufB, d_sp, h, nvars, j, fold, pending, ro, ppart, bar, d_final,
                        d_eval);
     QG_LAUNCH_CHECK();
@@ -1502,13 +1673,16 @@ static void run_rounds_dist(qg_ctx* ctx, uint32_t nvars, const std::vector<const
         const TablePtrs& d = parity ? tY : tX;
         for (int i = 0; i < 8; i++) tp.dst[i] = d.dst[i];
       }
-      if (!launch_big<K, NP>(ctx, src, X, Y, NL, j, d_sp, h, npairs, ro, 0, partial, loc))
+      int skip0 = launch_big<K, NP>(ctx, src, X, Y, NL, j, d_sp, h, npairs, ro, 0, partial, loc);
+      if (skip0 < 0) {
+        skip0 = 0;
         hipLaunchKernelGGL((k_sc_round<K, NP>), dim3(sc_round_blocks(ctx, npairs)), dim3(SC_BLOCK),
                            0, ctx->stream, tp, d_sp, h, npairs, fold, ro, j, 0, partial, loc);
+      }
       QG_LAUNCH_CHECK();
       comm_allgather_bytes(ctx, loc, all, sizeof(Fr) * NP);
       hipLaunchKernelGGL((k_sc_finish<NP>), dim3(1), dim3(SC_BLOCK), 0, ctx->stream, d_sp, h, all,
-                         world, ro, j);
+                         world, ro, j, skip0);
       QG_LAUNCH_CHECK();
       if (fold) {
         for (int i = 0; i < 8; i++) cur.src[i] = tp.dst[i];
@@ -1555,7 +1729,7 @@ static void run_rounds_dist(qg_ctx* ctx, uint32_t nvars, const std::vector<const
         bufB.dst[i] = a;
       }
     }
-    constexpr size_t PB = TAIL_BLOCK / NP;
+    const size_t PB = tail_pb(h.nslots, NP);
     const size_t pairs0 = ((size_t)1 << nvars >> js) / 2;
     // co-residency of the grid barrier: with the in-process loopback every rank
     // shares one device, so each persistent grid takes a 1/world share of the CUs
@@ -1564,7 +1738,7 @@ static void run_rounds_dist(qg_ctx* ctx, uint32_t nvars, const std::vector<const
     const unsigned grid = (unsigned)std::max<size_t>(
         1, std::min<size_t>(persist_grid_cap<K, NP>(ctx, cus), (pairs0 + PB - 1) / PB));
     Fr* ppart = ctx->scratch_as<Fr>("sc_ppartial", (size_t)2 * grid * NP);
-    hipLaunchKernelGGL((k_sc_persist<K, NP>), dim3(grid), dim3(TAIL_BLOCK), 0, ctx->stream, t0,
+    hipLaunchKernelGGL((k_sc_tail<K, NP>), dim3(grid), dim3(TAIL_BLOCK), 0, ctx->stream, t0,
                        bufA, bufB, d_sp, h, nvars, js, js >= 1 ? 1 : 0, 0, ro, ppart, bar,
                        d_final, d_eval);
     QG_LAUNCH_CHECK();
@@ -1714,28 +1888,38 @@ void expr_table_device(qg_ctx* ctx, size_t n, uint32_t ntables, const std::vecto
 }
 
 // Sumcheck over the generic interpreter (see k_gen_eval); same transcript,
-// proof and claim as the fast path (sumcheck.rs:28-114)
+// proof and claim as the fast path (sumcheck.rs:28-114).  With a communicator
+// attached (world W = 2^lw) each rank holds the 2^(nvars - lw) block of every
+// table whose high index bits are its rank — the compiled path's decomposition:
+// rounds j < m = nvars - lw pair local entries only, each rank's np round sums
+// are allgathered and summed, and every rank runs the identical host transcript
+// step; then every rank folds its block by r_{m-1} to one value per slot,
+// allgathers those W x K values (the rank is the high index bits) and runs the
+// last lw rounds redundantly on the gathered W-entry tables.
 static void sumcheck_run_generic(qg_ctx* ctx, uint32_t nvars, uint32_t ntables,
                                  const std::vector<const Fr*>& d_tables, const qg_expr_op* prog,
                                  size_t prog_len, const uint64_t* consts, size_t nconsts,
                                  const uint64_t claimed_sum[4], uint8_t state[32],
                                  uint64_t* round_coeffs, uint32_t* round_lens, uint64_t* point,
                                  uint64_t evaluation[4]) {
-  QG_CHECK(ctx->world == 1, QG_ERR_UNSUPPORTED,
-           "generic (interpreted) sumcheck expressions run on one GPU");
+  const uint32_t world = (uint32_t)ctx->world;
+  uint32_t lw = 0;
+  while ((1u << lw) < world) lw++;
+  QG_CHECK((1u << lw) == world, QG_ERR_INVALID, "sharded sumcheck needs a power-of-two world");
+  QG_CHECK(nvars >= lw, QG_ERR_INVALID, "sharded sumcheck needs nvars >= log2(world)");
+  const uint32_t m = nvars - lw;  // rounds over local pairs
   const uint32_t width = expr_degree(prog, prog_len) + 1;
   const uint32_t np = width;
   QG_CHECK(np <= (uint32_t)GEN_NPMAX, QG_ERR_UNSUPPORTED, "expression degree above 31");
   const GenProg g = gen_prepare(prog, prog_len, consts, nconsts, ntables);
   const std::vector<uint32_t>& used = g.used;
   const uint32_t K = (uint32_t)used.size();
-  const size_t N = (size_t)1 << nvars;
+  const size_t NL = (size_t)1 << m;  // this rank's entries per table
   // t x 2^261 (plain integers, 29-bit limbs)
   std::vector<L9> t29(GEN_NPMAX);
   for (uint32_t t = 0; t < (uint32_t)GEN_NPMAX; t++)
     t29[t] = l9_of(plain_mul(from_u64_plain(t), pow2_mod_plain<FrP>(261)));
   const std::vector<Fr> V = vinv_general(np);
-  // device data: ops | consts | t | per-round slot pointers | fold scratch
   const auto dprog = gen_upload(ctx, g, "gen_prog");
   const GenOp* d_ops = dprog.first;
   const L9* d_c29 = dprog.second;
@@ -1743,20 +1927,22 @@ static void sumcheck_run_generic(qg_ctx* ctx, uint32_t nvars, uint32_t ntables,
   QG_HIP(hipMemcpyAsync(d_t29, t29.data(), sizeof(L9) * GEN_NPMAX, hipMemcpyHostToDevice,
                         ctx->stream));
   const size_t Ks = std::max<uint32_t>(K, 1);
-  Fr* X = ctx->scratch_as<Fr>("gen_x", std::max<size_t>(1, (N / 2) * Ks));
-  Fr* Y = ctx->scratch_as<Fr>("gen_y", std::max<size_t>(1, (N / 4) * Ks));
-  // round j's tables: inputs (j = 0), X (j odd), Y (j even >= 2)
-  std::vector<const Fr*> hp((size_t)nvars * Ks, nullptr);
-  for (uint32_t j = 0; j < nvars; j++)
-    for (uint32_t s2 = 0; s2 < K; s2++)
-      hp[(size_t)j * Ks + s2] = j == 0 ? d_tables[used[s2]]
-                                       : ((j & 1) ? X + (N / 2) * s2 : Y + std::max<size_t>(1, N / 4) * s2);
-  const Fr** d_ptrs = ctx->scratch_as<const Fr*>("gen_ptrs", hp.size());
-  QG_HIP(hipMemcpyAsync(d_ptrs, hp.data(), sizeof(Fr*) * hp.size(), hipMemcpyHostToDevice,
-                        ctx->stream));
+  // fold ping-pong (X: NL/2 per slot, Y: NL/4 per slot), gathered tables G
+  // (W per slot) and their fold ping-pong (GX, GY: W/2, W/4 per slot)
+  Fr* X = ctx->scratch_as<Fr>("gen_x", std::max<size_t>(1, (NL / 2) * Ks));
+  Fr* Y = ctx->scratch_as<Fr>("gen_y", std::max<size_t>(1, (NL / 4) * Ks));
+  Fr* G = ctx->scratch_as<Fr>("gen_g", (size_t)world * Ks);
+  Fr* GX = ctx->scratch_as<Fr>("gen_gx", std::max<size_t>(1, (world / 2) * Ks));
+  Fr* GY = ctx->scratch_as<Fr>("gen_gy", std::max<size_t>(1, (world / 4) * Ks));
+  Fr* one = ctx->scratch_as<Fr>("gen_one", Ks);  // each slot folded to one value (gather send)
+  // pointer arrays of the fold (src | dst) and of the evaluation, each its own
+  // pinned staging slot: both are enqueued within one round, before its sync
+  const Fr** d_ptrs_f = ctx->scratch_as<const Fr*>("gen_ptrs_f", 2 * Ks);
+  const Fr** d_ptrs_e = ctx->scratch_as<const Fr*>("gen_ptrs_e", Ks);
   ScState* d_st = ctx->scratch_as<ScState>("gen_st", 1);
   Fr* partial = ctx->scratch_as<Fr>("gen_partial", (size_t)1024 * GEN_NPMAX);
   Fr* d_out = ctx->scratch_as<Fr>("gen_out", GEN_NPMAX);
+  Fr* d_all = ctx->scratch_as<Fr>("gen_all", (size_t)world * std::max<size_t>(GEN_NPMAX, Ks));
   // transcript: append num_vars (usize) and claimed_sum (sumcheck.rs:35-36)
   {
     uint8_t b8[8], b32[32];
@@ -1767,27 +1953,100 @@ static void sumcheck_run_generic(qg_ctx* ctx, uint32_t nvars, uint32_t ntables,
   }
   uint32_t npp = 4;
   while (npp < np) npp <<= 1;
+  // per-slot table pointers of the current round's source
+  std::vector<const Fr*> cur(Ks, nullptr);
+  for (uint32_t s2 = 0; s2 < K; s2++) cur[s2] = d_tables[used[s2]];
+  size_t cur_n = NL;  // entries per table of the current source
+  auto upload_ptrs = [&](const Fr** d, const char* slot, const std::vector<const Fr*>& a,
+                         const std::vector<Fr*>* b) {
+    const size_t n = b ? 2 * Ks : Ks;
+    const Fr** hp = reinterpret_cast<const Fr**>(ctx->pinned_get(slot, sizeof(Fr*) * n));
+    for (size_t k = 0; k < Ks; k++) {
+      hp[k] = a[k];
+      if (b) hp[Ks + k] = (*b)[k];
+    }
+    QG_HIP(hipMemcpyAsync(d, hp, sizeof(Fr*) * n, hipMemcpyHostToDevice, ctx->stream));
+  };
+  // fold cur (cur_n entries per slot) by the challenge in d_st into dst[] (cur_n / 2 each)
+  auto fold_into = [&](const std::vector<Fr*>& dst) {
+    const size_t nq = cur_n / 2;
+    if (K > 0) {
+      upload_ptrs(d_ptrs_f, "gen_ptrs_f", cur, &dst);
+      hipLaunchKernelGGL(k_gen_fold, dim3(div_up(nq * K, 256)), dim3(256), 0, ctx->stream,
+                         d_ptrs_f, (Fr* const*)(d_ptrs_f + Ks), K, nq, d_st);
+      QG_LAUNCH_CHECK();
+      for (uint32_t s2 = 0; s2 < K; s2++) cur[s2] = dst[s2];
+    }
+    cur_n = nq;
+  };
   std::vector<Fr> ev(np);
   Fr r = Fr::zero();
+  bool pend_fold = false;  // the source still has to be folded by r
+  int par = 0;             // next fold destination in the current phase: 0 -> X/GX, 1 -> Y/GY
   QgTimed tm(ctx, "sumcheck_round");
   for (uint32_t j = 0; j < nvars; j++) {
-    const size_t half = N >> (j + 1);
-    if (j > 0 && K > 0) {
-      const size_t nq = 2 * half;
-      hipLaunchKernelGGL(k_gen_fold, dim3(div_up(nq * K, 256)), dim3(256), 0, ctx->stream,
-                         d_ptrs + (size_t)(j - 1) * Ks, (Fr* const*)(d_ptrs + (size_t)j * Ks), K, nq,
-                         d_st);
-      QG_LAUNCH_CHECK();
+    if (j == m && lw > 0) {
+      // gather: every slot folded to one value, allgathered; G[s][rank] = value
+      if (pend_fold) {
+        std::vector<Fr*> dst(Ks);
+        for (uint32_t s2 = 0; s2 < K; s2++) dst[s2] = one + s2;
+        fold_into(dst);
+      } else {
+        for (uint32_t s2 = 0; s2 < K; s2++)
+          QG_HIP(hipMemcpyAsync(one + s2, cur[s2], sizeof(Fr), hipMemcpyDeviceToDevice, ctx->stream));
+      }
+      std::vector<Fr> all((size_t)world * Ks);
+      if (K) {
+        comm_allgather_bytes(ctx, one, d_all, sizeof(Fr) * K);
+        QG_HIP(hipMemcpyAsync(all.data(), d_all, sizeof(Fr) * K * world, hipMemcpyDeviceToHost,
+                              ctx->stream));
+        ctx->sync();
+        std::vector<Fr> gt((size_t)world * K);
+        for (uint32_t rk = 0; rk < world; rk++)
+          for (uint32_t s2 = 0; s2 < K; s2++) gt[(size_t)s2 * world + rk] = all[(size_t)rk * K + s2];
+        QG_HIP(hipMemcpyAsync(G, gt.data(), sizeof(Fr) * gt.size(), hipMemcpyHostToDevice,
+                              ctx->stream));
+        ctx->sync();
+      }
+      for (uint32_t s2 = 0; s2 < K; s2++) cur[s2] = G + (size_t)world * s2;
+      cur_n = world;
+      pend_fold = false;
+      par = 0;
+    } else if (pend_fold) {
+      std::vector<Fr*> dst(Ks);
+      const bool gathered = j > m;  // rounds after the gather run on G
+      Fr* base = gathered ? (par ? GY : GX) : (par ? Y : X);
+      const size_t per = std::max<size_t>(1, gathered ? (par ? world / 4 : world / 2)
+                                                       : (par ? NL / 4 : NL / 2));
+      for (uint32_t s2 = 0; s2 < K; s2++) dst[s2] = base + per * s2;
+      fold_into(dst);
+      par ^= 1;
+      pend_fold = false;
     }
-    const Fr* const* dp = d_ptrs + (size_t)j * Ks;
+    const size_t half = cur_n / 2;
+    upload_ptrs(d_ptrs_e, "gen_ptrs_e", cur, nullptr);
     switch (npp) {
-      case 4: gen_round_kernels<4>(ctx, dp, half, np, d_ops, (uint32_t)prog_len, d_c29, d_t29, partial, d_out); break;
-      case 8: gen_round_kernels<8>(ctx, dp, half, np, d_ops, (uint32_t)prog_len, d_c29, d_t29, partial, d_out); break;
-      case 16: gen_round_kernels<16>(ctx, dp, half, np, d_ops, (uint32_t)prog_len, d_c29, d_t29, partial, d_out); break;
-      default: gen_round_kernels<32>(ctx, dp, half, np, d_ops, (uint32_t)prog_len, d_c29, d_t29, partial, d_out); break;
+      case 4: gen_round_kernels<4>(ctx, d_ptrs_e, half, np, d_ops, (uint32_t)prog_len, d_c29, d_t29, partial, d_out); break;
+      case 8: gen_round_kernels<8>(ctx, d_ptrs_e, half, np, d_ops, (uint32_t)prog_len, d_c29, d_t29, partial, d_out); break;
+      case 16: gen_round_kernels<16>(ctx, d_ptrs_e, half, np, d_ops, (uint32_t)prog_len, d_c29, d_t29, partial, d_out); break;
+      default: gen_round_kernels<32>(ctx, d_ptrs_e, half, np, d_ops, (uint32_t)prog_len, d_c29, d_t29, partial, d_out); break;
     }
-    QG_HIP(hipMemcpyAsync(ev.data(), d_out, sizeof(Fr) * np, hipMemcpyDeviceToHost, ctx->stream));
-    ctx->sync();
+    if (j < m && lw > 0) {
+      // this rank's sums of the local pairs -> the global round sums
+      comm_allgather_bytes(ctx, d_out, d_all, sizeof(Fr) * np);
+      std::vector<Fr> all((size_t)world * np);
+      QG_HIP(hipMemcpyAsync(all.data(), d_all, sizeof(Fr) * np * world, hipMemcpyDeviceToHost,
+                            ctx->stream));
+      ctx->sync();
+      for (uint32_t t = 0; t < np; t++) {
+        Fr a = Fr::zero();
+        for (uint32_t rk = 0; rk < world; rk++) a = a + all[(size_t)rk * np + t];
+        ev[t] = a;
+      }
+    } else {
+      QG_HIP(hipMemcpyAsync(ev.data(), d_out, sizeof(Fr) * np, hipMemcpyDeviceToHost, ctx->stream));
+      ctx->sync();
+    }
     // coefficients, trim, absorb (u64 length + canonical coefficients), draw r
     std::vector<Fr> co(np);
     uint32_t len = 0;
@@ -1812,13 +2071,14 @@ static void sumcheck_run_generic(qg_ctx* ctx, uint32_t nvars, uint32_t ntables,
     const L9 r29 = l9_of(plain_mul(from_mont(r), pow2_mod_plain<FrP>(261)));
     for (int k = 0; k < 9; k++) hs->r29[k] = r29.v[k];
     QG_HIP(hipMemcpyAsync(d_st, hs, sizeof(ScState), hipMemcpyHostToDevice, ctx->stream));
+    pend_fold = true;
   }
-  // final fold with r_{n-1} on the host and h at the point (sumcheck.rs:93-99)
+  // final fold with r_{n-1} on the host and h at the point (sumcheck.rs:93-99);
+  // the last round's source holds 2 entries per slot (identical on every rank)
   std::vector<Fr> fin(ntables, Fr::zero());
   for (uint32_t s2 = 0; s2 < K; s2++) {
     Fr ab[2];
-    QG_HIP(hipMemcpyAsync(ab, hp[(size_t)(nvars - 1) * Ks + s2], sizeof ab, hipMemcpyDeviceToHost,
-                          ctx->stream));
+    QG_HIP(hipMemcpyAsync(ab, cur[s2], sizeof ab, hipMemcpyDeviceToHost, ctx->stream));
     ctx->sync();
     for (Fr& x : ab) reduce_once<FrP>(x.v), reduce_once<FrP>(x.v);
     fin[used[s2]] = ab[0] + r * (ab[1] - ab[0]);

@@ -267,6 +267,17 @@ class Srs:
               self.dev.h)
         return g1_from_abi(xy, inf.value)
 
+    def commit_array(self, arr: np.ndarray, n=None):
+        """KZG::commit (kzg.rs:61-73) from host memory: `arr` is an (n, 4) uint64
+        array of Montgomery limbs (arkworks' in-memory Fr), passed to
+        qg_kzg_commit as is — the drop-in path a Rust caller takes."""
+        arr = np.ascontiguousarray(arr, dtype=np.uint64)
+        n = arr.shape[0] if n is None else n
+        xy = (C.c_uint64 * 8)()
+        inf = C.c_uint8()
+        check(lib().qg_kzg_commit(self.dev.h, self.h, u64p(arr), n, xy, C.byref(inf)), self.dev.h)
+        return g1_from_abi(xy, inf.value)
+
     def msm_dev(self, vec: DeviceVec, n=None):
         n = vec.n if n is None else n
         xy = (C.c_uint64 * 8)()

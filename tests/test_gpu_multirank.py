@@ -38,7 +38,7 @@ def run_ranks(world, fn):
     return out
 
 
-@pytest.mark.parametrize("world", [2, 4])
+@pytest.mark.parametrize("world", [2, 4, 8])
 def test_sharded_msm(world):
     import quill_amd as q
     rnd = random.Random(world)
@@ -55,7 +55,7 @@ def test_sharded_msm(world):
     assert all(r == exp for r in run_ranks(world, fn))
 
 
-@pytest.mark.parametrize("world,nv_local", [(2, 9), (4, 6), (2, 1)])
+@pytest.mark.parametrize("world,nv_local", [(2, 9), (4, 6), (2, 1), (8, 5), (8, 1)])
 def test_sharded_sumcheck(world, nv_local):
     import quill_amd as q
     from quill_amd.hyperplonk import VirtualPolyExpr as E, sumcheck_prove_tables
@@ -83,7 +83,7 @@ def test_sharded_sumcheck(world, nv_local):
         assert rp == proof.r_polys and pt == opt and ev == oev and s == ot.state
 
 
-@pytest.mark.parametrize("world", [2, 4])
+@pytest.mark.parametrize("world", [2, 4, 8])
 def test_sharded_zerocheck(world):
     import quill_amd as q
     from quill_amd.hyperplonk import VirtualPolyExpr as E, sumcheck_prove_tables
@@ -112,7 +112,8 @@ def test_sharded_zerocheck(world):
         assert rp == zp.sumcheck_proof.r_polys and pt == opt and ev == oev and s == ot.state
 
 
-@pytest.mark.parametrize("world,tail_zeros", [(2, 0), (4, 0), (4, 131), (2, 1)])
+@pytest.mark.parametrize("world,tail_zeros", [(2, 0), (4, 0), (4, 131), (2, 1), (8, 0), (8, 131),
+                                              (8, 300)])
 def test_sharded_mle_open(world, tail_zeros):
     """MLEvalProof::prove with the evaluations and the SRS sharded over ranks
     equals the single-context proof (and transcript state)."""
@@ -147,7 +148,8 @@ def test_sharded_mle_open(world, tail_zeros):
 
 
 @pytest.mark.parametrize("world,rows,which", [(2, 64, ("fib", "mod")), (4, 64, ("mod", "fib")),
-                                              (4, 16, ("fib",)), (2, 1024, ("mod",))])
+                                              (4, 16, ("fib",)), (2, 1024, ("mod",)),
+                                              (8, 64, ("fib", "mod")), (8, 256, ("mod",))])
 def test_sharded_hyperplonk(world, rows, which):
     """HyperPlonk::prove (proof.rs:239-301) sharded over `world` ranks: every
     rank holds its row block of each column, the full witness is exchanged by
@@ -187,7 +189,7 @@ def test_sharded_hyperplonk(world, rows, which):
         assert vt.state == state
 
 
-@pytest.mark.parametrize("world", [2, 4])
+@pytest.mark.parametrize("world", [2, 4, 8])
 def test_sharded_hyperplonk_bad_copy_constraint_across_blocks(world):
     """the copy constraint next(row) == current(row + 1) at a block boundary is
     checked with the neighbour rank's first row; every rank raises."""
@@ -217,7 +219,7 @@ def test_sharded_hyperplonk_bad_copy_constraint_across_blocks(world):
     assert all(o_ is not None and "Permutation" in o_ and f"row {RL - 1}" in o_ for o_ in outs), outs
 
 
-@pytest.mark.parametrize("world,nv", [(2, 17), (4, 18), (2, 19)])
+@pytest.mark.parametrize("world,nv", [(2, 17), (4, 18), (2, 19), (8, 19), (8, 20)])
 def test_sharded_sumcheck_early_gather_matches_single(world, nv):
     """nvars >= 17: the sharded prover runs nv - 15 rounds with per-round
     allgathers, then gathers the folded tables (2^16 global entries) and
@@ -248,3 +250,100 @@ def test_sharded_sumcheck_early_gather_matches_single(world, nv):
     for a, b in run_ranks(world, fn):
         assert a == ref
         assert b == zref
+
+
+@pytest.mark.parametrize("world,nv,kind", [(2, 6, "tables12"), (4, 7, "deg17"), (8, 8, "blowup"),
+                                           (4, 3, "tables12"), (8, 4, "deg31"), (2, 9, "deg17")])
+def test_sharded_sumcheck_generic(world, nv, kind):
+    """The interpreted (generic-expression) sumcheck sharded by the high index
+    bits (sumcheck_run_generic): per-round allgather of the local sums, then
+    the one-value-per-slot gather and the last log2(world) rounds redundantly.
+    Bit-exact against the oracle's reference-structured prover; nv = log2(world)
+    + 1 leaves one local round (the API needs nvars > log2(world), like the
+    compiled path)."""
+    import quill_amd as q
+    from quill_amd.hyperplonk import sumcheck_prove_tables
+    from test_gpu_generic import _exprs
+    rnd = random.Random(world * 1000 + nv)
+    me, oe, k = _exprs(kind)
+    lw = world.bit_length() - 1
+    NL = 1 << (nv - lw)
+    tabs = [[rnd.randrange(R) for _ in range(1 << nv)] for _ in range(k)]
+    ost = o.VirtualPolynomialStore(nv)
+    for tb in tabs:
+        ost.allocate_polynomial(tb)
+    oh = ost.new_virtual_from_expr(oe)
+    claimed = rnd.randrange(R)
+    ot = o.Transcript(b"generic-shard")
+    oproof, (opt, oev) = o.SumcheckProof.prove(nv, ost, oh, claimed, ot)
+
+    def fn(dev, rank, world):
+        t = q.Transcript(b"generic-shard")
+        rp, pt, ev = sumcheck_prove_tables(dev, nv, [tb[rank * NL:(rank + 1) * NL] for tb in tabs],
+                                           me, claimed, t)
+        return rp, pt, ev, t.state
+    for rp, pt, ev, s in run_ranks(world, fn):
+        assert rp == oproof.r_polys and pt == opt and ev == oev and s == ot.state
+
+
+@pytest.mark.parametrize("world", [2, 4])
+def test_sharded_zerocheck_generic(world):
+    """9 inputs + eq = 10 tables: the sharded zero-check's h * eq runs interpreted"""
+    import quill_amd as q
+    from quill_amd.hyperplonk import VirtualPolyExpr as E, sumcheck_prove_tables
+    nv = 7
+    lw = world.bit_length() - 1
+    NL = 1 << (nv - lw)
+    rnd = random.Random(77 + world)
+    tabs = [[rnd.randrange(R) for _ in range(1 << nv)] for _ in range(8)]
+    tabs.append([sum(tabs[2 * j][i] * tabs[2 * j + 1][i] for j in range(4)) % R
+                 for i in range(1 << nv)])
+    me = E.Input(0) * E.Input(1) + E.Input(2) * E.Input(3) + E.Input(4) * E.Input(5) + \
+        E.Input(6) * E.Input(7) - E.Input(8)
+    O = o.Expr
+    oe = O.input(0) * O.input(1) + O.input(2) * O.input(3) + O.input(4) * O.input(5) + \
+        O.input(6) * O.input(7) - O.input(8)
+    ost = o.VirtualPolynomialStore(nv)
+    for tb in tabs:
+        ost.allocate_polynomial(tb)
+    oh = ost.new_virtual_from_expr(oe)
+    ot = o.Transcript(b"zc-generic-shard")
+    ozp, (opt, oev) = o.ZeroCheckProof.prove(ost, oh, ot)
+
+    def fn(dev, rank, world):
+        t = q.Transcript(b"zc-generic-shard")
+        rp, pt, ev = sumcheck_prove_tables(dev, nv, [tb[rank * NL:(rank + 1) * NL] for tb in tabs],
+                                           me, 0, t, zerocheck=True)
+        return rp, pt, ev, t.state
+    for rp, pt, ev, s in run_ranks(world, fn):
+        assert rp == ozp.sumcheck_proof.r_polys and pt == opt and ev == oev and s == ot.state
+
+
+@pytest.mark.parametrize("world,rows", [(2, 32), (4, 32), (8, 64)])
+def test_sharded_hyperplonk_16_column(world, rows):
+    """The 16-column TransitionCircuit (23 tables, 330-term constraint: beyond
+    the compiled sumcheck image) proved sharded over `world` ranks; every
+    rank's proof equals the single-process oracle proof field by field."""
+    import hyperplonk_oracle as ho
+    import quill_amd as q
+    from test_gpu_generic import TAU as GTAU, _wide_circuit_device, _wide_circuit_oracle, \
+        _wide_witness
+    from test_gpu_hyperplonk import assert_same_proof, to_oracle
+    w = _wide_witness(rows)
+    oc_ = _wide_circuit_oracle(rows)
+    opcs = o.KZG(16 * rows, GTAU)
+    ohp = ho.HyperPlonk.preprocess([oc_], opcs)
+    oproof, ot = ohp.prove(opcs, [w])
+
+    def fn(dev, rank, world):
+        c = _wide_circuit_device(rows)
+        pcs = q.KZG.trusted_setup(16 * rows, GTAU, dev)
+        hp = q.HyperPlonk.preprocess([c], pcs)
+        proof = hp.prove(pcs, [w])
+        pcs.close()
+        return proof, hp.last_transcript.state
+    for proof, state in run_ranks(world, fn):
+        assert_same_proof(proof, oproof)
+        assert state == ot.state
+        vt = ho.hyperplonk_verify(to_oracle(proof), ohp.to_vk(), opcs)
+        assert vt.state == ot.state
