@@ -6,6 +6,8 @@
 //    XYZZ partial per rank, then EC additions (RCCL cannot add curve points).
 //  * sumcheck: ranks own the block of the hypercube selected by the high index
 //    bits; one allgather of the (d+1) round sums per round.
+//  * ML-PCS opening: the S polynomial's transform is split by frequency
+//    residue; one all-to-all delivers every rank its slice of S.
 #include <string.h>
 
 #include <condition_variable>
@@ -77,6 +79,40 @@ void comm_allgather_bytes(qg_ctx* ctx, const void* d_send, void* d_recv, size_t 
   }
   QG_CHECK(ctx->comm->comm, QG_ERR_COMM, "no communicator attached");
   QG_NCCL(ncclAllGather(d_send, d_recv, bytes, ncclUint8, ctx->comm->comm, ctx->stream));
+}
+
+// Personalised exchange: d_send holds world chunks of `bytes` (chunk d goes to
+// rank d), d_recv receives world chunks (chunk s came from rank s).  RCCL:
+// grouped point-to-point send/recv over xGMI (no reduction: the payload is
+// field elements, which RCCL cannot add); loopback: device copies.
+void comm_alltoall_bytes(qg_ctx* ctx, const void* d_send, void* d_recv, size_t bytes) {
+  if (ctx->world <= 1) {
+    QG_HIP(hipMemcpyAsync(d_recv, d_send, bytes, hipMemcpyDeviceToDevice, ctx->stream));
+    return;
+  }
+  QG_CHECK(ctx->comm, QG_ERR_COMM, "no communicator attached");
+  if (ctx->comm->lb) {
+    qg_loopback* lb = ctx->comm->lb;
+    QG_HIP(hipStreamSynchronize(ctx->stream));  // send buffer complete
+    lb->sends[ctx->rank] = d_send;
+    lb->barrier();
+    for (int r = 0; r < ctx->world; r++)
+      QG_HIP(hipMemcpyAsync((uint8_t*)d_recv + (size_t)r * bytes,
+                            (const uint8_t*)lb->sends[r] + (size_t)ctx->rank * bytes, bytes,
+                            hipMemcpyDeviceToDevice, ctx->stream));
+    QG_HIP(hipStreamSynchronize(ctx->stream));
+    lb->barrier();
+    return;
+  }
+  QG_CHECK(ctx->comm->comm, QG_ERR_COMM, "no communicator attached");
+  QG_NCCL(ncclGroupStart());
+  for (int r = 0; r < ctx->world; r++) {
+    QG_NCCL(ncclSend((const uint8_t*)d_send + (size_t)r * bytes, bytes, ncclUint8, r,
+                     ctx->comm->comm, ctx->stream));
+    QG_NCCL(ncclRecv((uint8_t*)d_recv + (size_t)r * bytes, bytes, ncclUint8, r, ctx->comm->comm,
+                     ctx->stream));
+  }
+  QG_NCCL(ncclGroupEnd());
 }
 
 // One contiguous piece of a sharded column-major full witness: rows [a, b) of

@@ -220,6 +220,7 @@ void expr_table_device(qg_ctx* ctx, size_t n, uint32_t ntables, const std::vecto
                        size_t nconsts, Fr* d_out);
 // RCCL helpers (comm.hip); no-ops when world == 1
 void comm_allgather_bytes(qg_ctx* ctx, const void* d_send, void* d_recv, size_t bytes);
+void comm_alltoall_bytes(qg_ctx* ctx, const void* d_send, void* d_recv, size_t bytes);
 void comm_release(qg_ctx* ctx);
 // true when the attached communicator is the in-process loopback (ranks share a device)
 bool comm_is_loopback(const qg_ctx* ctx);

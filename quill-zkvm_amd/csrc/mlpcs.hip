@@ -471,13 +471,14 @@ static Fr ml_plain_mul(const Fr& x, const Fr& y) { return from_mont(to_mont(x) *
 
 // twiddle tables w^k 2^261 (k < n/2) for w = root_of_unity(logn) and its
 // inverse, cached per transform size
-static void ntt_twiddles(qg_ctx* ctx, int logn, Fr** tw, Fr** twi) {
+static void ntt_twiddles(qg_ctx* ctx, int logn, Fr** tw, Fr** twi,
+                         const std::string& tag = "ntt_tw") {
   const size_t n = (size_t)1 << logn, h = std::max<size_t>(n / 2, 1);
-  *tw = ctx->scratch_as<Fr>("ntt_tw", h);
-  *twi = ctx->scratch_as<Fr>("ntt_twi", h);
+  *tw = ctx->scratch_as<Fr>(tag, h);
+  *twi = ctx->scratch_as<Fr>(tag + "i", h);
   const std::string memo = std::to_string(logn) + "@" + std::to_string((uintptr_t)*tw) + "," +
                            std::to_string((uintptr_t)*twi);
-  if (ctx->memo["ntt_tw"] == memo) return;
+  if (ctx->memo[tag] == memo) return;
   const Fr w = root_of_unity(logn), wi = finv(w);
   const int K = 64;
   const L9 c = F29P<FrP>::TO261;
@@ -491,7 +492,7 @@ static void ntt_twiddles(qg_ctx* ctx, int logn, Fr** tw, Fr** twi) {
   QG_LAUNCH_CHECK();
   hipLaunchKernelGGL(k_fr_to261, dim3(div_up(h, 256)), dim3(256), 0, ctx->stream, *twi, h, c);
   QG_LAUNCH_CHECK();
-  ctx->memo["ntt_tw"] = memo;
+  ctx->memo[tag] = memo;
 }
 
 // Transform of the eq table without an NTT.  g = eq(., z) over nz variables is
@@ -777,11 +778,226 @@ static void kzg_open_sharded(qg_ctx* ctx, const qg_srs* srs, const Fr* c, size_t
   g1_export(pi, out->proof_xy, &out->proof_inf);
 }
 
+// ---------------------------------------------------------------- sharded S polynomial
+// S = the window [M, 2M - 1) of h = IDFT_n(Hs), Hs[k] = w^{k(M-1)} / n (F[k] G[-k]
+// + F[-k] G[k]) (the replicated s_poly_device, n = 2M), split over W ranks by
+// frequency residue.  With k = k2 W + c and i = i1 B + i2 (B = n / W = 2L):
+//   F[k2 W + c] = DFT_B(u_c)[k2],  u_c[i2] = w^{i2 c} sum_{i1 < W/2} w_W^{i1 c} f[i1 B + i2]
+//   h[i1 B + i2] = sum_c w_W^{-i1 c} w^{-i2 c} IDFT_B(Hs[. W + c])[i2]
+// Rank r owns residue c = r: it transforms u_r and the mirror residue (-r mod W,
+// for the combine's F[-k] G[-k]), builds G at both residues from the eq
+// product formula restricted to the residue (k_eqdft_res), combines, runs one
+// B-point inverse, and sends every rank d the L values of h its slice
+// S[dL, (d+1)L) = h[M + dL + m] needs (i1 = W/2 + d/2, i2 = (d mod 2) L + m),
+// pre-multiplied by w_W^{-i1 c} w^{-i2 c}; one all-to-all, then each rank sums
+// the W vectors it received.  Work per rank: 2 B-point DIFs + 1 DIT against
+// the replicated path's two 2M-point transforms; the forward input f stays
+// the gathered vector (its pre-sum is W/2 multiplies per entry).
+// Bit orders as in s_poly_device: DIF outputs bit-reversed within the B block.
+
+// u[i2] = pw[i2] * sum_{i1 < h} cw[i1] f[i1 B + i2]   (cw: w_W^{i1 c} 2^261, pw: w^{i2 c} 2^261)
+static constexpr int SP_MAXW = 64;
+struct SpConsts {
+  L9 v[SP_MAXW];
+};
+__global__ void k_s_presum(const Fr* __restrict__ f, size_t B, uint32_t h, SpConsts cw,
+                           const Fr* __restrict__ pw, Fr* __restrict__ u) {
+  const size_t i2 = (size_t)blockIdx.x * blockDim.x + threadIdx.x;
+  if (i2 >= B) return;
+  R29 acc = R29::zero();
+  for (uint32_t i1 = 0; i1 < h; i1++)
+    acc = red2p29(add29(acc, mul29(to29(f[(size_t)i1 * B + i2]), R29::from_l9(cw.v[i1]))));
+  u[i2] = from29(canon29(mul29(acc, to29(pw[i2]))));
+}
+
+// G at residue c, bit-reversed within the block, one product-formula level per
+// launch (k_eqdft_level restricted to k = c mod W): level t has 2^(lb - t)
+// entries e (lb = log2 B), k2 = bitrev(e), factor a_t + z_t w^{(k2 W + c) 2^t}
+// = a_t + (z_t w^{c 2^t}) w_B^{k2 2^t}; Q_t[e] = factor Q_{t+1}[e >> 1].
+// twB: w_B^m 2^261 for m < B/2 (w_B^{B/2} = -1).
+__global__ void k_eqdft_res(const Fr* __restrict__ qnext, Fr q0, L9 a261, L9 zc261,
+                            const Fr* __restrict__ twB, int lb, int t, Fr* __restrict__ q) {
+  const int bits = lb - t;
+  const size_t len = (size_t)1 << bits;
+  const size_t e = (size_t)blockIdx.x * blockDim.x + threadIdx.x;
+  if (e >= len) return;
+  const size_t k2 = bits ? (size_t)(__brevll((unsigned long long)e) >> (64 - bits)) : 0;
+  const size_t m = k2 << t, half = (size_t)1 << (lb - 1);
+  R29 w = to29(twB[m & (half - 1)]);
+  if (m & half) w = sub29(R29::zero(), w);
+  const R29 fct = red6p29(add29(R29::from_l9(a261), mul29(R29::from_l9(zc261), w)));
+  const R29 qn = qnext ? to29(qnext[e >> 1]) : to29(q0);
+  q[e] = from29(canon29(mul29(fct, qn)));
+}
+
+// Hs at residue c in the bit-reversed block order: p -> k2 = bitrev(p); the
+// partner of -k is residue m = -c mod W at position ~p (c != 0) or, for c = 0,
+// the bit-reversed negation (k_s_combine_br's rule).  Hs = (-1)^c w^{-c} / n
+// w_B^{-k2} (F_c G_m' + F_m' G_c): twiB holds w_B^{-e} 2^261, cst the
+// per-residue constant x 2^266 (mul29 of the 2^251-scaled products lands in
+// arkworks form).
+__global__ void k_s_combine_res(const Fr* __restrict__ Fc, const Fr* __restrict__ Gc,
+                                const Fr* __restrict__ Fm, const Fr* __restrict__ Gm, int c,
+                                const Fr* __restrict__ twiB, int lb, L9 cst, Fr* __restrict__ H) {
+  const size_t B = (size_t)1 << lb;
+  const size_t p = (size_t)blockIdx.x * blockDim.x + threadIdx.x;
+  if (p >= B) return;
+  size_t pp;
+  if (c != 0) {
+    pp = ~p & (B - 1);
+  } else {
+    pp = 0;
+    if (p) {
+      const int hb = 63 - __clzll((unsigned long long)p);
+      pp = p ^ (((size_t)1 << hb) - 1);
+    }
+  }
+  const size_t k2 = (size_t)(__brevll((unsigned long long)p) >> (64 - lb));
+  const size_t half = B / 2;
+  R29 wi = to29(twiB[k2 & (half - 1)]);
+  if (k2 & half) wi = sub29(R29::zero(), wi);
+  const R29 v = red2p29(add29(mul29(to29(Fc[p]), to29(Gm[pp])), mul29(to29(Fm[pp]), to29(Gc[p]))));
+  H[p] = from29(canon29(mul29(mul29(v, red6p29(wi)), R29::from_l9(cst))));
+}
+
+// send[d L + m] = K[d] P[i2] Z[i2], i2 = (d mod 2) L + m   (K: x 2^261, P: x 2^261)
+__global__ void k_s_outgoing(const Fr* __restrict__ Z, const Fr* __restrict__ P, SpConsts K,
+                             size_t L, uint32_t W, Fr* __restrict__ send) {
+  const size_t i = (size_t)blockIdx.x * blockDim.x + threadIdx.x;
+  if (i >= (size_t)W * L) return;
+  const uint32_t d = (uint32_t)(i / L);
+  const size_t i2 = (size_t)(d & 1) * L + i % L;
+  send[i] = from29(canon29(mul29(mul29(to29(Z[i2]), to29(P[i2])), R29::from_l9(K.v[d]))));
+}
+
+// out[m] = sum_s recv[s L + m]
+__global__ void k_s_sum_parts(const Fr* __restrict__ recv, size_t L, uint32_t W,
+                              Fr* __restrict__ out) {
+  const size_t m = (size_t)blockIdx.x * blockDim.x + threadIdx.x;
+  if (m >= L) return;
+  R29 acc = R29::zero();
+  for (uint32_t s = 0; s < W; s++) acc = red2p29(add29(acc, to29(recv[(size_t)s * L + m])));
+  out[m] = from29(canon29(acc));
+}
+
+static L9 l9_x261(const Fr& mont) {  // Montgomery field element -> (value x 2^261) limbs
+  return l9_of29(ml_plain_mul(from_mont(mont), pow2_mod_plain<FrP>(261)));
+}
+
+// this rank's slice S[rank L, rank L + L) (L = M / W; the last entry of the last
+// slice is h[2M - 1] = 0, past S's M - 1 coefficients).  f: the gathered
+// evaluations (M entries, every rank), point: the eq variables (nvars).
+static void s_poly_sharded(qg_ctx* ctx, const Fr* f, size_t M, const uint64_t* point,
+                           size_t nvars, Fr* S_local) {
+  QgTimed tm(ctx, "s_polynomial");
+  const uint32_t W = (uint32_t)ctx->world, c = (uint32_t)ctx->rank;
+  QG_CHECK(W <= SP_MAXW && (W & (W - 1)) == 0 && M == ((size_t)1 << nvars) && M >= W,
+           QG_ERR_UNSUPPORTED, "sharded S polynomial geometry");
+  const size_t L = M / W, B = 2 * L;
+  int lb = 0;
+  while (((size_t)1 << lb) < B) lb++;
+  int logn = 0;
+  while (((size_t)1 << logn) < 2 * M) logn++;
+  QG_CHECK(logn <= 28, QG_ERR_UNSUPPORTED, "S-polynomial NTT beyond 2-adicity");
+  Fr *twB, *twiB;
+  ntt_twiddles(ctx, lb, &twB, &twiB, "sp_tw");
+  const Fr w = root_of_unity(logn), wi = finv(w);
+  const Fr wW = fpow_small(w, B);  // w_W = w^(n / W)
+  const Fr ninv = finv(from_u64<FrP>((uint64_t)2 * M));
+  const uint32_t cm = (W - c) % W;  // mirror residue (-c mod W)
+  const int nres = cm == c ? 1 : 2;
+  const uint32_t res[2] = {c, cm};
+  Fr* Fb = ctx->scratch_as<Fr>("sp_F", 2 * B);
+  Fr* Gb = ctx->scratch_as<Fr>("sp_G", 2 * B);
+  Fr* tmp = ctx->scratch_as<Fr>("sp_tmp", 2 * B);  // u / pw scratch, then G level ping-pong
+  const int K = 64;
+  for (int q = 0; q < nres; q++) {
+    const uint32_t cc = res[q];
+    Fr* Fq = Fb + (size_t)q * B;
+    Fr* Gq = Gb + (size_t)q * B;
+    // u_cc = w^{i2 cc} sum_i1 w_W^{i1 cc} f[i1 B + i2]
+    Fr* pw = tmp + B;
+    hipLaunchKernelGGL(k_powers_ml, dim3(div_up(div_up(B, (size_t)K), ML_BLOCK)), dim3(ML_BLOCK), 0,
+                       ctx->stream, fpow_small(w, cc), B, K, pw);
+    QG_LAUNCH_CHECK();
+    hipLaunchKernelGGL(k_fr_to261, dim3(div_up(B, ML_BLOCK)), dim3(ML_BLOCK), 0, ctx->stream, pw, B,
+                       F29P<FrP>::TO261);
+    QG_LAUNCH_CHECK();
+    SpConsts cw{};
+    Fr wk = Fr::one();
+    const Fr wWc = fpow_small(wW, cc);
+    for (uint32_t i1 = 0; i1 < W / 2; i1++) {
+      cw.v[i1] = l9_x261(wk);
+      wk = wk * wWc;
+    }
+    hipLaunchKernelGGL(k_s_presum, dim3(div_up(B, ML_BLOCK)), dim3(ML_BLOCK), 0, ctx->stream, f, B,
+                       W / 2, cw, pw, tmp);
+    QG_LAUNCH_CHECK();
+    ntt_run(ctx, true, tmp, B, Fq, twB, lb, 0, 0, nullptr);
+    // G at residue cc: levels above the block collapse into a host constant,
+    // then one launch per level t = lb - 1 .. 0 (ping-pong tmp / Gq; nz >= lb
+    // whenever W >= 2)
+    const size_t nz = nvars;
+    Fr q0 = Fr::one();
+    for (size_t t = nz; t-- > (size_t)lb;) {  // levels with a single entry (t >= lb)
+      const Fr zt = fr_import(point + 4 * t);
+      q0 = q0 * ((Fr::one() - zt) + zt * fpow_small(w, (uint64_t)cc << t));
+    }
+    const int top = (int)std::min<size_t>(nz, (size_t)lb);
+    const Fr* qn = nullptr;
+    for (int t = top - 1; t >= 0; t--) {
+      const Fr zt = fr_import(point + 4 * t);
+      const L9 a9 = l9_x261(Fr::one() - zt);
+      const L9 z9 = l9_x261(zt * fpow_small(w, (uint64_t)cc << t));
+      Fr* dst = (t & 1) == 0 ? Gq : tmp;
+      const size_t len = (size_t)1 << (lb - t);
+      hipLaunchKernelGGL(k_eqdft_res, dim3(div_up(len, ML_BLOCK)), dim3(ML_BLOCK), 0, ctx->stream,
+                         qn, q0, a9, z9, twB, lb, t, dst);
+      QG_LAUNCH_CHECK();
+      qn = dst;
+    }
+  }
+  // combine + inverse (own residue), pre-multiplied outgoing vectors, all-to-all, sum
+  Fr* H = tmp;
+  const Fr* Fm = nres == 2 ? Fb + B : Fb;
+  const Fr* Gm = nres == 2 ? Gb + B : Gb;
+  Fr cst = fpow_small(wi, c) * ninv;
+  if (c & 1) cst = fneg(cst);
+  const L9 cst9 = l9_of29(ml_plain_mul(from_mont(cst), pow2_mod_plain<FrP>(266)));
+  hipLaunchKernelGGL(k_s_combine_res, dim3(div_up(B, ML_BLOCK)), dim3(ML_BLOCK), 0, ctx->stream, Fb,
+                     Gb, Fm, Gm, (int)c, twiB, lb, cst9, H);
+  QG_LAUNCH_CHECK();
+  ntt_run(ctx, false, H, B, H, twiB, lb, 0, 0, nullptr);
+  Fr* P = tmp + B;
+  hipLaunchKernelGGL(k_powers_ml, dim3(div_up(div_up(B, (size_t)K), ML_BLOCK)), dim3(ML_BLOCK), 0,
+                     ctx->stream, fpow_small(wi, c), B, K, P);
+  QG_LAUNCH_CHECK();
+  hipLaunchKernelGGL(k_fr_to261, dim3(div_up(B, ML_BLOCK)), dim3(ML_BLOCK), 0, ctx->stream, P, B,
+                     F29P<FrP>::TO261);
+  QG_LAUNCH_CHECK();
+  SpConsts Kd{};
+  const Fr wWi = finv(wW);
+  for (uint32_t d = 0; d < W; d++) {
+    const uint64_t i1 = W / 2 + d / 2;
+    Kd.v[d] = l9_x261(fpow_small(wWi, (i1 * c) % W));
+  }
+  Fr* sendb = ctx->scratch_as<Fr>("sp_send", (size_t)W * L);
+  Fr* recvb = ctx->scratch_as<Fr>("sp_recv", (size_t)W * L);
+  hipLaunchKernelGGL(k_s_outgoing, dim3(div_up((size_t)W * L, ML_BLOCK)), dim3(ML_BLOCK), 0,
+                     ctx->stream, H, P, Kd, L, W, sendb);
+  QG_LAUNCH_CHECK();
+  comm_alltoall_bytes(ctx, sendb, recvb, L * sizeof(Fr));
+  hipLaunchKernelGGL(k_s_sum_parts, dim3(div_up(L, ML_BLOCK)), dim3(ML_BLOCK), 0, ctx->stream,
+                     recvb, L, W, S_local);
+  QG_LAUNCH_CHECK();
+}
+
 // MLEvalProof::prove with a communicator: this rank holds poly[rank L, (rank+1) L)
 // of the 2^nvars evaluations (L = 2^nvars / world) and the matching SRS shard.
-// eq table and the dot product per slice; the S polynomial needs whole vectors
-// (a correlation), so the slices are allgathered and S is computed on every
-// rank; its commitment and all four quotient commitments are sharded MSMs.
+// eq table and the dot product per slice; the S polynomial's transform is split
+// by frequency residue over the ranks (s_poly_sharded: the slices are
+// allgathered for its forward pre-sum, one all-to-all returns every rank its
+// slice of S); its commitment and all four quotient commitments are sharded MSMs.
 static void mle_open_sharded(qg_ctx* ctx, const qg_srs* srs, const Fr* dpoly, size_t L,
                              const uint64_t* point, size_t nvars, uint8_t state[32],
                              qg_mle_proof* out) {
@@ -800,17 +1016,28 @@ static void mle_open_sharded(qg_ctx* ctx, const qg_srs* srs, const Fr* dpoly, si
   allgather_host(ctx, &part, sizeof(Fr), parts.data());
   Fr evaluation = Fr::zero();
   for (const Fr& v : parts) evaluation = evaluation + v;
-  // S on every rank from the gathered vector
+  // S: this rank's slice from the residue-split transform (s_poly_sharded) or,
+  // with QG_S_REPLICATED=1 (A/B runs), the whole S on every rank
   comm_allgather_bytes(ctx, dpoly, dfull, L * sizeof(Fr));
-  Fr* dS = ctx->scratch_as<Fr>("mle_S", N > 1 ? N - 1 : 1);
+  static const bool replicated = getenv("QG_S_REPLICATED") != nullptr;
+  Fr* Sl = ctx->scratch_as<Fr>("mle_S_local", L);
   size_t Slen = 0;
   if (N > 1) {
-    s_poly_device(ctx, dfull, N, dpr, N, dS, point, nvars);
-    Slen = trimmed_len(ctx, dS, N - 1);
+    if (replicated) {
+      Fr* dS = ctx->scratch_as<Fr>("mle_S", N);
+      s_poly_device(ctx, dfull, N, dpr, N, dS, point, nvars);
+      QG_HIP(hipMemsetAsync(dS + N - 1, 0, sizeof(Fr), ctx->stream));  // h[2M - 1] = 0
+      QG_HIP(hipMemcpyAsync(Sl, dS + off, L * sizeof(Fr), hipMemcpyDeviceToDevice, ctx->stream));
+    } else {
+      s_poly_sharded(ctx, dfull, N, point, nvars, Sl);
+    }
+    Slen = trimmed_len_global(ctx, Sl, L, L);
+  } else {
+    QG_HIP(hipMemsetAsync(Sl, 0, L * sizeof(Fr), ctx->stream));
   }
   const size_t sloc = Slen > off ? std::min(L, Slen - off) : 0;
   QG_CHECK(sloc <= srs->n, QG_ERR_INVALID, "Polynomial degree exceeds max degree");
-  G1Affine s_comm = msm_device(ctx, srs, dS + off, sloc);
+  G1Affine s_comm = msm_device(ctx, srs, Sl, sloc);
   // transcript: point (Vec<Fr>), evaluation, s_comm; draw r (mlpcs.rs:100-107)
   std::vector<uint8_t> msg(8 + 32 * nvars);
   u64_to_bytes(nvars, msg.data());
@@ -829,8 +1056,8 @@ static void mle_open_sharded(qg_ctx* ctx, const qg_srs* srs, const Fr* dpoly, si
   const size_t Lt = trimmed_len_global(ctx, dpoly, L, L);
   kzg_open_sharded(ctx, srs, dpoly, L, Lt, r, &out->poly_opening);
   kzg_open_sharded(ctx, srs, dpoly, L, Lt, r_inv, &out->poly_opening_inv);
-  kzg_open_sharded(ctx, srs, dS + off, L, Slen, r, &out->s_opening);
-  kzg_open_sharded(ctx, srs, dS + off, L, Slen, r_inv, &out->s_opening_inv);
+  kzg_open_sharded(ctx, srs, Sl, L, Slen, r, &out->s_opening);
+  kzg_open_sharded(ctx, srs, Sl, L, Slen, r_inv, &out->s_opening_inv);
 }
 
 // MLEvalProof::prove (mlpcs.rs:83-124) on a device-resident evaluation vector

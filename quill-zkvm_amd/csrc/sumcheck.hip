@@ -487,9 +487,13 @@ struct FinSmem {
 // lanes (r * 2^261 for the fold and r * 2^256 for the output, each lo + hi).
 // Absorbing the 48 challenge bytes is deferred when pend_out != nullptr.
 template <int NP>
+// canon_out: the writer stores the CANONICAL coefficients (the transcript's) in
+// ro.coeffs right away and skips the Montgomery pass after the challenge (the
+// persistent tail: the host converts those rows, keeping ~1 us off every round)
 QG_DEV void finish_core(const SopLds<NP>& sp, uint32_t np, const R29* ev, const RoundOut& ro,
                         uint32_t j, FinSmem& fs, const uint32_t* state_in, uint32_t* pend_out,
-                        uint32_t* state_out, uint32_t tr = 4096, bool writer = true) {
+                        uint32_t* state_out, uint32_t tr = 4096, bool writer = true,
+                        bool canon_out = false) {
   constexpr uint32_t U = NP <= 8 ? NP : 4;  // lanes per coefficient
   const uint32_t tid = threadIdx.x;
   const bool w0 = tid < 64;
@@ -504,8 +508,10 @@ QG_DEV void finish_core(const SopLds<NP>& sp, uint32_t np, const R29* ev, const 
   cc = norm29(cc);
 #pragma unroll
   for (uint32_t m = 1; m < U; m <<= 1) cc = norm29(add29(cc, shfl_xor29(cc, m)));
-  const Fr ccw = from29(canon29(red128p(cc)));
+  // U <= 8 products < 2p each: < 16p
+  const Fr ccw = from29(canon29(red16p29<FrP>(cc)));
   const bool lead = w0 && cu == 0 && ct < np;
+  if (writer && canon_out && lead) ro.coeffs[(size_t)j * ro.width + ct] = ccw;
   if (writer) {
     for (uint32_t i = np + tid; i < ro.width; i += blockDim.x)
       ro.coeffs[(size_t)j * ro.width + i] = Fr::zero();
@@ -563,7 +569,7 @@ QG_DEV void finish_core(const SopLds<NP>& sp, uint32_t np, const R29* ev, const 
   __syncthreads();
   SC_TR(tr + 6);
   if (!pend_out && w0) b3_hash_quad(fs.ab, 80, state_out, 8);
-  if (writer) {
+  if (writer && !canon_out) {
     // Montgomery coefficients for the proof output (off the challenge path)
     R29 cm = R29::zero();
     if (w0 && ct < np) {
@@ -839,8 +845,8 @@ QG_DEV void sweep_pairs(const AllBufs& tb, uint32_t j, bool fold, const R29& r, 
 // (sweep_pairs), per-block partial rows, and the last block to publish
 // (ticket election) sums the rows and runs the transcript step (or, sharded,
 // writes this rank's local sums).
-template <int K, int NP, bool PURE, bool PF>
-__global__ void __launch_bounds__(SC_BLOCK)
+template <int K, int NP, bool PURE, bool PF, int WPE = 1>
+__global__ void __launch_bounds__(SC_BLOCK) __attribute__((amdgpu_waves_per_eu(WPE)))
     k_sc_big(AllBufs tb, uint32_t j, const SopDev* __restrict__ spg, SopHdr h, size_t npairs,
              RoundOut ro, int pending, Fr* __restrict__ partial, Fr* __restrict__ loc, int skip0) {
   __shared__ SopLds<NP> sp;
@@ -1004,6 +1010,24 @@ QG_HD uint32_t tail_pb(uint32_t nslots, uint32_t np) {
   return pb;
 }
 
+// Per-point sums when only the first `n` threads (n <= 64: wave 0) hold
+// values: a shuffle tree of exactly log2(n / NP) steps inside wave 0, no LDS
+// staging; else the block reduction.  res[t] (LDS, < 2p) on return.
+template <int NP>
+QG_DEV void tail_reduce(R29 acc, uint32_t n, uint32_t np, R29* red, R29* res) {
+  uint32_t n2 = NP;
+  while (n2 < n) n2 <<= 1;  // lanes past n hold zeros
+  if (n2 > 64) {
+    block_reduce_pts<NP>(acc, np, red, res);
+    return;
+  }
+  if (threadIdx.x < 64) {
+    for (uint32_t m = n2 / 2; m >= NP; m >>= 1) acc = norm29(add29(acc, shfl_xor29(acc, m)));
+    if (threadIdx.x < np) res[threadIdx.x] = red128p(acc);
+  }
+  __syncthreads();
+}
+
 template <int NP>
 QG_DEV void tail_eval(const R29* F, uint32_t ss, const SopLds<NP>& sp, const SopHdr& h,
                       uint32_t pl, uint32_t t, R29& acc) {
@@ -1112,7 +1136,12 @@ __global__ void __launch_bounds__(TAIL_BLOCK)
       if (base + stride < npairs) __syncthreads();  // the staging array is refilled
     }
     if (writer) SC_TR(16 * j + 1);
-    block_reduce_pts<NP>(acc, np, red, res);
+    {
+      // threads holding values: NP per pair of this block's (last) step
+      const size_t first = (size_t)blk * PB;
+      const uint32_t cnt = npairs > first ? (uint32_t)std::min<size_t>(PB, npairs - first) : 0u;
+      tail_reduce<NP>(acc, npairs > stride ? (uint32_t)TAIL_BLOCK : cnt * NP, np, red, res);
+    }
     if (writer) SC_TR(16 * j + 7);
     if (nb > 1) {
       Fr* part = partial + (size_t)(j & 1) * gridDim.x * NP;
@@ -1133,10 +1162,12 @@ __global__ void __launch_bounds__(TAIL_BLOCK)
           for (int k = 0; k < 4; k++) acc = add29(acc, to29(v[k]));
           acc = red6p(acc);
         }
-      block_reduce_pts<NP>(acc, np, red, res);
+      // rows of nb blocks: thread (row pl, point t) holds one when nb * NP <= 64
+      tail_reduce<NP>(acc, std::min<uint32_t>(nb, TAIL_BLOCK / NP) * NP, np, red, res);
     }
     if (writer) SC_TR(16 * j + 2);
-    finish_core<NP>(sp, np, res, ro, j, fs, st, pend, nullptr, writer ? 16 * j : 4096, writer);
+    finish_core<NP>(sp, np, res, ro, j, fs, st, pend, nullptr, writer ? 16 * j : 4096, writer,
+                    true);
     __syncthreads();
     r = fs.r;
     pending = 1;
@@ -1521,7 +1552,12 @@ static int launch_big(qg_ctx* ctx, const std::vector<const Fr*>& src, Fr* X, Fr*
   const unsigned blocks = sc_big_blocks(ctx, npairs);
   // QG_SC_PF=1: next slot's entries prefetched during the current slot (tuning)
   static const bool pf = getenv("QG_SC_PF") != nullptr;
-  if (pure && pf)
+  // QG_SC_WPE=4: the product sweep compiled for 4 waves per SIMD (<= 128 VGPRs; tuning)
+  static const bool wpe4 = getenv("QG_SC_WPE") != nullptr;
+  if (pure && wpe4)
+    hipLaunchKernelGGL((k_sc_big<K, 4, true, false, 4>), dim3(blocks), dim3(SC_BLOCK), 0,
+                       ctx->stream, tb, j, d_sp, h, npairs, ro, pending, partial, loc, skip0);
+  else if (pure && pf)
     hipLaunchKernelGGL((k_sc_big<K, 4, true, true>), dim3(blocks), dim3(SC_BLOCK), 0, ctx->stream,
                        tb, j, d_sp, h, npairs, ro, pending, partial, loc, skip0);
   else if (pure)
@@ -1534,8 +1570,10 @@ static int launch_big(qg_ctx* ctx, const std::vector<const Fr*>& src, Fr* X, Fr*
   return skip0;
 }
 
+// returns the first round of the persistent tail (its coefficient rows are
+// canonical words: k_sc_tail's finish_core canon_out)
 template <int K, int NP>
-static void run_rounds(qg_ctx* ctx, uint32_t nvars, const std::vector<const Fr*>& src,
+static uint32_t run_rounds(qg_ctx* ctx, uint32_t nvars, const std::vector<const Fr*>& src,
                        const SopDev* d_sp, SopHdr h, RoundOut ro, uint32_t* bar, Fr* d_final,
                        Fr* d_eval) {
 
@@ -1556,11 +1594,16 @@ static void run_rounds(qg_ctx* ctx, uint32_t nvars, const std::vector<const Fr*>
   int fold = 0, pending = 0;
   uint32_t j = 0;
   int parity = 0;  // next destination: 0 -> X, 1 -> Y
+  // QG_SC_PERS_LOG overrides where the persistent tail takes over (tuning)
+  static const int pers_log = [] {
+    const char* e = getenv("QG_SC_PERS_LOG");
+    return e ? atoi(e) : PERS_LOG;
+  }();
   {
     QgTimed tm(ctx, "sumcheck_round");
     for (; j < nvars; j++) {
       const size_t table = N >> j;  // entries per table evaluated in round j
-      if (table <= ((size_t)1 << PERS_LOG)) break;
+      if (table <= ((size_t)1 << pers_log)) break;
       const size_t npairs = table / 2;
       TablePtrs tp = cur;
       if (fold) {
@@ -1610,6 +1653,7 @@ static void run_rounds(qg_ctx* ctx, uint32_t nvars, const std::vector<const Fr*>
                        d_eval);
     QG_LAUNCH_CHECK();
   }
+  return j;
 }
 
 // gathered [rank][slot][e] (S entries per rank and slot) -> per-slot tables
@@ -1634,7 +1678,7 @@ __global__ void k_sc_gather_tables(const Fr* __restrict__ in, uint32_t world, ui
 static constexpr uint32_t SC_GATHER_LOG = 16;
 
 template <int K, int NP>
-static void run_rounds_dist(qg_ctx* ctx, uint32_t nvars, const std::vector<const Fr*>& src,
+static uint32_t run_rounds_dist(qg_ctx* ctx, uint32_t nvars, const std::vector<const Fr*>& src,
                             const SopDev* d_sp, SopHdr h, RoundOut ro, uint32_t* bar, Fr* d_final,
                             Fr* d_eval) {
   const uint32_t nslots = h.nslots;
@@ -1743,14 +1787,15 @@ static void run_rounds_dist(qg_ctx* ctx, uint32_t nvars, const std::vector<const
                        d_final, d_eval);
     QG_LAUNCH_CHECK();
   }
+  return js;
 }
 
 template <int K, int NP>
-static void run_rounds_any(qg_ctx* ctx, uint32_t nvars, const std::vector<const Fr*>& src,
-                           const SopDev* d_sp, SopHdr h, RoundOut ro, uint32_t* bar, Fr* d_final,
-                           Fr* d_eval) {
-  if (ctx->world > 1) run_rounds_dist<K, NP>(ctx, nvars, src, d_sp, h, ro, bar, d_final, d_eval);
-  else run_rounds<K, NP>(ctx, nvars, src, d_sp, h, ro, bar, d_final, d_eval);
+static uint32_t run_rounds_any(qg_ctx* ctx, uint32_t nvars, const std::vector<const Fr*>& src,
+                               const SopDev* d_sp, SopHdr h, RoundOut ro, uint32_t* bar,
+                               Fr* d_final, Fr* d_eval) {
+  if (ctx->world > 1) return run_rounds_dist<K, NP>(ctx, nvars, src, d_sp, h, ro, bar, d_final, d_eval);
+  return run_rounds<K, NP>(ctx, nvars, src, d_sp, h, ro, bar, d_final, d_eval);
 }
 
 // inverse Vandermonde on nodes 0..np-1 for any np <= GEN_NPMAX: V[t][u]
@@ -2147,14 +2192,15 @@ static void sumcheck_run(qg_ctx* ctx, uint32_t nvars, uint32_t ntables,
   const uint32_t np = P->hdr.np;
   const size_t nsrc = src.size();
   // (with no used slots, nslots = 0 and loads are skipped)
+  uint32_t tail0;
   if (np <= 4) {
-    if (nsrc <= 4) run_rounds_any<4, 4>(ctx, nvars, src, d_sp, P->hdr, ro, bar, d_final, d_eval);
-    else run_rounds_any<8, 4>(ctx, nvars, src, d_sp, P->hdr, ro, bar, d_final, d_eval);
+    if (nsrc <= 4) tail0 = run_rounds_any<4, 4>(ctx, nvars, src, d_sp, P->hdr, ro, bar, d_final, d_eval);
+    else tail0 = run_rounds_any<8, 4>(ctx, nvars, src, d_sp, P->hdr, ro, bar, d_final, d_eval);
   } else if (np <= 8) {
-    if (nsrc <= 4) run_rounds_any<4, 8>(ctx, nvars, src, d_sp, P->hdr, ro, bar, d_final, d_eval);
-    else run_rounds_any<8, 8>(ctx, nvars, src, d_sp, P->hdr, ro, bar, d_final, d_eval);
+    if (nsrc <= 4) tail0 = run_rounds_any<4, 8>(ctx, nvars, src, d_sp, P->hdr, ro, bar, d_final, d_eval);
+    else tail0 = run_rounds_any<8, 8>(ctx, nvars, src, d_sp, P->hdr, ro, bar, d_final, d_eval);
   } else {
-    run_rounds_any<8, 16>(ctx, nvars, src, d_sp, P->hdr, ro, bar, d_final, d_eval);
+    tail0 = run_rounds_any<8, 16>(ctx, nvars, src, d_sp, P->hdr, ro, bar, d_final, d_eval);
   }
 
   QG_HIP(hipMemcpyAsync(hio, io, io_bytes, hipMemcpyDeviceToHost, ctx->stream));
@@ -2165,7 +2211,9 @@ static void sumcheck_run(qg_ctx* ctx, uint32_t nvars, uint32_t ntables,
   memcpy(state, h.data(), 32);
   memcpy(round_lens, h.data() + o_lens, sizeof(uint32_t) * nvars);
   const Fr* hc = reinterpret_cast<const Fr*>(h.data() + o_coeffs);
-  for (size_t i = 0; i < (size_t)nvars * width; i++) fr_export(hc[i], round_coeffs + 4 * i);
+  // rows of the persistent tail hold canonical words (finish_core canon_out)
+  for (size_t i = 0; i < (size_t)nvars * width; i++)
+    fr_export(i / width >= tail0 ? to_mont(hc[i]) : hc[i], round_coeffs + 4 * i);
   const Fr* hp = reinterpret_cast<const Fr*>(h.data() + o_chal);
   for (uint32_t i = 0; i < nvars; i++) fr_export(hp[i], point + 4 * i);
   fr_export(reinterpret_cast<const Fr*>(h.data() + o_final)[8], evaluation);

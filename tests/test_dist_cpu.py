@@ -115,8 +115,9 @@ def sharded_mle_open(rank, world, poly, point, tau, domain):
     """mle_open_sharded + kzg_open_sharded (csrc/mlpcs.hip) restated: rank r
     holds poly[r L, (r+1) L) and SRS shard [tau^(rL + i)] g.
     * eq table, local dot -> allgather of the partial evaluations;
-    * allgather of the slices, S replicated (the transform needs whole
-      vectors), s_comm from per-rank partial MSMs over the SRS shard;
+    * allgather of the slices; S split by frequency residue (s_poly_sharded,
+      tests/test_s_poly_split.py) with one all-to-all; s_comm from per-rank
+      partial MSMs over the SRS shard;
     * per KZG opening: global trimmed length (allgather of per-rank maxima),
       local suffix-Horner s_i = c_i + x s_{i+1}, allgather of T_r = s_local[0],
       carry C_r = sum_{r' > r} T_r' x^((r'-r-1) L), s_i += x^(le - i) C,
@@ -143,9 +144,15 @@ def sharded_mle_open(rank, world, poly, point, tau, domain):
     evaluation = sum(_allgather_obj(sum(a * b for a, b in zip(mine, pr[off:off + L])) % R,
                                     world)) % R
     full = [v for sl in _allgather_obj(mine, world) for v in sl]
-    S = o.compute_s_polynomial(full, pr) if N > 1 else []
-    S_local = (S + [0] * (N - len(S)))[off:off + L]
-    s_comm = sum_points(_allgather_obj(msm_shard(S_local[:max(0, min(L, len(S) - off))]), world))
+    # S split by frequency residue (s_poly_sharded): this rank's outgoing
+    # vectors, an all-to-all (gloo: gather then pick), the sum of what arrived
+    from test_s_poly_split import rank_slice
+    sends = rank_slice(full, point, world, rank)
+    got = _allgather_obj(sends, world)
+    S_local = [sum(got[s_][rank][m] for s_ in range(world)) % R for m in range(L)]
+    nzs = [i for i, v in enumerate(S_local) if v]
+    Slen = max(_allgather_obj(off + nzs[-1] + 1 if nzs else 0, world))
+    s_comm = sum_points(_allgather_obj(msm_shard(S_local[:max(0, min(L, Slen - off))]), world))
     t = o.Transcript(domain)
     t.append_fr_vec(point)
     t.append_fr(evaluation)
