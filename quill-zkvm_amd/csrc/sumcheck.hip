@@ -1000,7 +1000,7 @@ QG_DEV void grid_barrier(uint32_t* ctr, uint32_t n, uint32_t* err) {
 // PB is chosen at run time from the slot count (tail_pb, shared with the
 // host's grid computation) so the two staging arrays fit TAIL_FBYTES.
 static constexpr int TAIL_BLOCK = 256;
-static constexpr uint32_t TAIL_FBYTES = 100 * 1024;  // LDS for the staging arrays
+static constexpr uint32_t TAIL_FBYTES = 32 * 1024;  // LDS for the staging arrays
 // np: the kernel's point stride NP (threads per pair), not the expression's np
 QG_HD uint32_t tail_pb(uint32_t nslots, uint32_t np) {
   // F0: nslots x 2 PB entries, F1: nslots x PB entries, 36 B each
@@ -1512,9 +1512,16 @@ static unsigned persist_grid_cap(qg_ctx* ctx, size_t cus) {
     occ = std::stoi(it->second);
   }
   QG_CHECK(occ >= 1, QG_ERR_DEVICE, "persistent sumcheck kernel cannot be resident");
-  // one block per CU at most even where more would fit: a CU-resident block per
-  // grid slot keeps the barrier safe next to other kernels' blocks
-  return (unsigned)std::max<size_t>(1, cus);
+  // bpc blocks per CU (QG_SC_TAIL_BPC, default 1), never more than the
+  // occupancy answer minus one: a spare block slot per CU keeps the barrier
+  // safe next to other kernels' blocks and under the gfx950 SGPR admission
+  // rule (MI355X_MICROARCH.md "Residency")
+  static const int bpc_env = [] {
+    const char* e = getenv("QG_SC_TAIL_BPC");
+    return e ? std::max(1, atoi(e)) : 1;
+  }();
+  const int bpc = std::max(1, std::min(bpc_env, occ - 1));
+  return (unsigned)std::max<size_t>(1, cus * (size_t)bpc);
 }
 
 // thread-per-pair round kernel (k_sc_big) for product expressions and for
