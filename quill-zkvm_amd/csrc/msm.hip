@@ -12,13 +12,14 @@
 //  * Bucketing is a counting sort: count (atomics) -> scan -> scatter (atomics).
 //    Digits are recomputed from the scalars in the scatter pass (32 B/scalar)
 //    instead of materializing n*W keys.
-//  * Accumulation is load-balanced: every bucket is split into chunks of
-//    E entries, one thread per chunk, so skewed digit distributions (small
-//    witness values, the short top window) do not serialize on one lane.
-//    Mixed XYZZ + affine additions (8M + 2S), no inversions.
-//  * Bucket reduction sum_j (j+1) B_j runs as independent running sums over
-//    segments of L buckets; segment s contributes acc_s + lo_s * run_s; blocks
-//    tree-reduce in LDS; one final block sums block results.
+//  * Accumulation is load-balanced: the bucket-sorted entries are cut into
+//    equal chunks (a whole number of waves of resident threads), one thread
+//    per chunk, so skewed digit distributions (small witness values, the
+//    short top window) do not serialize on one lane.  Mixed XYZZ + affine
+//    additions (8M + 2S), no inversions.
+//  * Bucket reduction sum_j (j+1) B_j: running sums over segments of S
+//    buckets, one per SIMD lane of the chip, then shuffle-only wave folds
+//    (suffix scan + tree) 64 elements at a time; no bucket array, no LDS.
 #include <stdlib.h>
 
 #include "common.h"
@@ -28,7 +29,7 @@ using namespace qg;
 
 namespace qg {
 
-static constexpr int MSM_COMBINE_SEQ = 64;  // partials a bucket's combine adds sequentially
+static constexpr uint32_t MSM_COMBINE_SEQ = 4;  // partials the reduction adds per bucket in a row
 static constexpr int MSM_BLOCK = 256;
 
 // Window size for an SRS of n bases.  Cost model in bucket-addition units:
@@ -464,14 +465,14 @@ static constexpr int SCAN_PER_THREAD = 8;
 static constexpr int SCAN_BLOCK = 256;
 static constexpr int SCAN_TILE = SCAN_PER_THREAD * SCAN_BLOCK;
 
-// entries per accumulation thread = 2^elog (chosen per call, see msm_device)
-__device__ __forceinline__ uint2 scan_val(const uint32_t* counts, size_t i, size_t nb, int elog) {
+// entries per accumulation thread = L (chosen per call, msm_accumulate_phase)
+__device__ __forceinline__ uint2 scan_val(const uint32_t* counts, size_t i, size_t nb, uint32_t L) {
   uint32_t c = i < nb ? counts[i] : 0u;
-  return make_uint2(c, (c + (1u << elog) - 1) >> elog);
+  return make_uint2(c, (c + L - 1) / L);
 }
 
 // per-tile exclusive scan; writes tile totals
-__global__ void k_scan_tiles(const uint32_t* __restrict__ counts, size_t nb, int elog,
+__global__ void k_scan_tiles(const uint32_t* __restrict__ counts, size_t nb, uint32_t L,
                              uint32_t* __restrict__ bstart, uint32_t* __restrict__ tstart,
                              uint2* __restrict__ tile_tot, uint32_t* __restrict__ max_tpb) {
   __shared__ uint2 sh[SCAN_BLOCK];
@@ -480,7 +481,7 @@ __global__ void k_scan_tiles(const uint32_t* __restrict__ counts, size_t nb, int
   uint2 tot = make_uint2(0, 0);
   uint32_t mx = 0;
   for (int k = 0; k < SCAN_PER_THREAD; k++) {
-    v[k] = scan_val(counts, base + k, nb, elog);
+    v[k] = scan_val(counts, base + k, nb, L);
     tot.x += v[k].x;
     tot.y += v[k].y;
     mx = max(mx, v[k].y);
@@ -652,121 +653,301 @@ QG_DEV uint32_t msm_slot_last(const uint32_t* bstart, uint32_t b, uint32_t L) {
   return (bstart[b + 1] - 1) / L + b;
 }
 
-// Segmented pairwise tree over the partial slots: after the steps s = 1, 2,
-// 4, ... slot_first(b) holds bucket b's sum.  Slots no thread wrote carry
-// owner == ~0 and are skipped.
+// stride between a bucket's partial slots after the tree steps: buckets with
+// more than MSM_COMBINE_SEQ slots (skewed digits: the short top window, small
+// scalars) are pre-summed pairwise until at most that many remain, so one lane
+// of the reduction never adds a long run of partials while the others wait
+QG_DEV uint32_t msm_slot_stride(uint32_t nslot) {
+  uint32_t st = 1;
+  while (nslot > MSM_COMBINE_SEQ * st) st <<= 1;
+  return st;
+}
+
+// Segmented pairwise tree over the partial slots of the skewed buckets: after
+// the steps s = 1, 2, 4, ... slot_first(b) + k st_b holds the sum of slots
+// [k st_b, (k + 1) st_b) of bucket b.  Slots no thread wrote carry owner == ~0
+// and are skipped.
 __global__ void __launch_bounds__(MSM_BLOCK)
     k_msm_tree_step(X29Raw* __restrict__ partial, const uint32_t* __restrict__ owner,
-                                const uint32_t* __restrict__ bstart, uint32_t L, uint32_t nslots,
-                                uint32_t s) {
+                    const uint32_t* __restrict__ bstart, uint32_t L, uint32_t nslots, uint32_t s) {
   const uint32_t i = blockIdx.x * blockDim.x + threadIdx.x;
   if (i >= nslots) return;
   const uint32_t b = owner[i];
   if (b == 0xffffffffu) return;
   const uint32_t f = msm_slot_first(bstart, b, L), l = msm_slot_last(bstart, b, L);
+  if (l - f + 1 <= MSM_COMBINE_SEQ * s) return;  // this bucket is done at this level
   const uint32_t off = i - f;
   if ((off & (2 * s - 1)) == 0 && i + s <= l)
     partial[i] = x29_raw(x29_add(msm_partial(partial, i), msm_partial(partial, i + s)));
 }
 
 // ---- reduction ------------------------------------------------------------
-// per-MSM inputs of the batched reduction kernels (blockIdx.y = MSM)
+// sum_j (j + 1) B_j over the nb buckets of every MSM of a batch:
+//  * k_msm_bsum: thread t folds buckets [t S, t S + S) from the top, each
+//    bucket summed from its partial slots on the fly (no bucket array):
+//    run_t = sum B_j, wsum_t = sum (j - t S + 1) B_j, so the total is
+//    sum_t wsum_t + S t run_t;
+//  * then groups of G lanes fold (msm_fold): for pairs (A_g, Y_g) with weight
+//    factor F,  sum_g A_g + F g Y_g = sum_g A_g + F sum_{g>=1} Suf_g  (Suf =
+//    suffix sums of Y over the group: a shuffle scan, then a shuffle tree),
+//    emitted as A' and Y' = G F sum_g Y_g, so the next level is again
+//    sum_w A'_w + w Y'_w (factor 1);
+//  * k_msm_wfold repeats the fold, 16 elements per wave on quads of lanes
+//    (quad-cooperative additions, below) until one element is left.
+// One wave per SIMD already saturates the VALU on an XYZZ addition (micro/
+// add_bench.hip: 7.9 us per addition per wave at 1, 2 and 4 waves per SIMD),
+// so the reduction's cost is its addition count - and its code size: an
+// inlined addition is ~47 KB of instructions, so every kernel here issues all
+// of its additions from ONE call site inside a loop (operands selected per
+// iteration); several inlined copies overflowed the instruction cache (the
+// first version of k_msm_bsum, 301 KB, ran 2.3x slower than its count).
+// 2^19 buckets: 65536 lanes (S = 8), groups of 16 -> 4096 -> 256 -> 16 -> 1.
 struct MsmRed {
   const X29Raw* partial;
   const uint32_t* bstart;
-  uint32_t L, step;
+  uint32_t L;
 };
 
-// B_j = sum of bucket j's partial slots at offsets 0, step, 2 step, ... (empty
-// bucket -> infinity); at most MSM_COMBINE_SEQ of them.  buckets: nb per MSM.
-__global__ void __launch_bounds__(MSM_BLOCK)
-    k_msm_combine(const MsmRed* __restrict__ runs, uint32_t nb, G1Xyzz* __restrict__ buckets) {
-  const uint32_t j = blockIdx.x * blockDim.x + threadIdx.x;
-  if (j >= nb) return;
-  const MsmRed rr = runs[blockIdx.y];
-  G1Xyzz* out = buckets + (size_t)blockIdx.y * nb;
-  const X29Raw* partial = rr.partial;
-  if (rr.bstart[j] == rr.bstart[j + 1]) {
-    out[j] = x29_store(x29_inf());
-    return;
-  }
-  const uint32_t f = msm_slot_first(rr.bstart, j, rr.L), l = msm_slot_last(rr.bstart, j, rr.L);
-  if (l - f < rr.step) {
-    out[j] = x29_store(msm_partial(partial, f));
-    return;
-  }
-  X29 acc = msm_partial(partial, f);
-  for (uint32_t t = f + rr.step; t <= l; t += rr.step) acc = x29_add(acc, msm_partial(partial, t));
-  out[j] = x29_store(acc);
+#if defined(__HIP_DEVICE_COMPILE__)
+__device__ __forceinline__ Q29 q29_shfl_down(const Q29& a, uint32_t d, int width) {
+  Q29 r;
+#pragma unroll
+  for (int i = 0; i < 9; i++) r.l[i] = __shfl_down(a.l[i], d, width);
+  return r;
+}
+__device__ __forceinline__ X29 x29_shfl_down(const X29& p, uint32_t d, int width) {
+  return {q29_shfl_down(p.X, d, width), q29_shfl_down(p.Y, d, width),
+          q29_shfl_down(p.ZZ, d, width), q29_shfl_down(p.ZZZ, d, width)};
 }
 
-// k doublings (k < 32)
-QG_DEV X29 x29_dbl_k(X29 p, int k) {
-  for (int i = 0; i < k; i++) p = x29_dbl(p);
-  return p;
+// ---- quad-cooperative point arithmetic (latency-bound levels) -------------
+// Every lane of a quad (4 lanes) holds both operands; the field products of
+// one XYZZ addition / doubling are spread over the quad in dependent stages
+// and the stage results broadcast back with DPP quad permutes, so every lane
+// returns the full result.  Same formulas and operand bounds as x29_add /
+// x29_dbl (curve29.h): 4 product stages per addition instead of 14 products
+// in a row, 3 per doubling instead of 9.  micro/add_bench.hip: 4.1 us per
+// addition and 2.6 us per doubling on one wave (7.9 / 4.3 us single-lane),
+// for the short chains at the top of the reduction where lanes are idle.
+template <int S>
+__device__ __forceinline__ Q29 q29_quad(const Q29& a) {
+  Q29 r;
+#pragma unroll
+  for (int i = 0; i < 9; i++)
+    r.l[i] = (uint32_t)__builtin_amdgcn_mov_dpp((int)a.l[i], S * 0x55, 0xf, 0xf, false);
+  return r;
 }
 
-// One level of the bucket reduction  sum_i Q_i + i P_i  over i in [0, m)
-// (Q = P when Q is null).  Thread t of block b folds its S = 2^slog consecutive
-// elements from the top (run = sum P, wsum = sum (i - lo) P: one running-sum
-// chain, no scalar multiplications); the block then needs
-//   A_b = sum_t [acc_t + t S run_t],  sum_t t run_t = sum_{k>=1} Suf_k
-// with Suf_k = sum_{t>=k} run_t: an LDS suffix scan and a tree sum.  Output
-//   A_b = sum_{i in block b} Q_i + (i - base_b) P_i,   R_b = 2^rlog sum_{i in b} P_i
-// with rlog = log2(T S), so sum_i Q_i + i P_i = sum_b A_b + b R_b: the same form
-// one level up (P' = R, Q' = A).  A single block's A_0 is the total.
-// Level 1 runs on the buckets with P = Q = B: sum_j (j + 1) B_j.
-__global__ void __launch_bounds__(MSM_BLOCK)
-    k_msm_wsum(const G1Xyzz* __restrict__ P, const G1Xyzz* __restrict__ Q, uint32_t m, int slog,
-               int rlog, G1Xyzz* __restrict__ A_out, G1Xyzz* __restrict__ R_out, size_t stride_in,
-               size_t stride_out) {
-  __shared__ G1Xyzz sh_r[MSM_BLOCK], sh_a[MSM_BLOCK];
-  const uint32_t t = threadIdx.x, T = blockDim.x;
-  // MSM blockIdx.y of a batch: inputs stride_in apart, outputs stride_out apart
-  P += blockIdx.y * stride_in;
-  if (Q) Q += blockIdx.y * stride_in;
-  A_out += blockIdx.y * stride_out;
-  if (R_out) R_out += blockIdx.y * stride_out;
-  const uint64_t lo = ((uint64_t)blockIdx.x * T + t) << slog;
-  X29 run = x29_inf(), acc = x29_inf();
-  if (lo < m) {
-    const uint32_t l = (uint32_t)lo;
-    const uint32_t hi = m - l < (1u << slog) ? m : l + (1u << slog);
-    X29 wsum = x29_inf(), qsum = x29_inf();
-    for (uint32_t i = hi - 1; i > l; i--) {
-      run = x29_add(run, x29_load(P[i]));
-      wsum = x29_add(wsum, run);
-      if (Q) qsum = x29_add(qsum, x29_load(Q[i]));
+__device__ __forceinline__ Q29 q29_sel(bool c, const Q29& a, const Q29& b) {
+  Q29 r;
+#pragma unroll
+  for (int i = 0; i < 9; i++) r.l[i] = c ? a.l[i] : b.l[i];
+  return r;
+}
+
+__device__ __forceinline__ X29 x29_sel(bool c, const X29& a, const X29& b) {
+  return {q29_sel(c, a.X, b.X), q29_sel(c, a.Y, b.Y), q29_sel(c, a.ZZ, b.ZZ), q29_sel(c, a.ZZZ, b.ZZZ)};
+}
+
+__device__ __forceinline__ X29 x29_add_q4(const X29& p, const X29& q) {
+  if (x29_is_inf(p)) return q;
+  if (x29_is_inf(q)) return p;
+  const uint32_t r = threadIdx.x & 3u;
+  const bool r0 = r == 0, r1 = r == 1, r2 = r == 2, odd = (r & 1u) != 0u;
+  // U1 = X1 ZZ2 | U2 = X2 ZZ1 | S1 = Y1 ZZZ2 | S2 = Y2 ZZZ1;  ZZ1 ZZ2 | ZZZ1 ZZZ2
+  const Q29 m0 = mul29(q29_sel(r0, p.X, q29_sel(r1, q.X, q29_sel(r2, p.Y, q.Y))),
+                       q29_sel(r0, q.ZZ, q29_sel(r1, p.ZZ, q29_sel(r2, q.ZZZ, p.ZZZ))));
+  const Q29 m1 = mul29(q29_sel(odd, p.ZZZ, p.ZZ), q29_sel(odd, q.ZZZ, q.ZZ));
+  const Q29 U1 = q29_quad<0>(m0), U2 = q29_quad<1>(m0), S1 = q29_quad<2>(m0), S2 = q29_quad<3>(m0);
+  const Q29 ZZ12 = q29_quad<0>(m1), ZZZ12 = q29_quad<1>(m1);
+  const Q29 P = normfull29(sub29(U2, U1));
+  const Q29 R = normfull29(sub29(S2, S1));
+  if (is_zero_mod29_fast<FqP, 8>(P)) return x29_add(p, q);  // doubling / cancellation (quad-uniform)
+  // PP = P^2 | RR = R^2
+  const Q29 sq = sqr29(q29_sel(odd, R, P));
+  const Q29 PP = q29_quad<0>(sq), RR = q29_quad<1>(sq);
+  // PPP = P PP | Q = U1 PP | ZZ3 = ZZ1 ZZ2 PP
+  const Q29 m3 = mul29(q29_sel(r0, P, q29_sel(r1, U1, ZZ12)), PP);
+  const Q29 PPP = q29_quad<0>(m3), Q = q29_quad<1>(m3), ZZ3 = q29_quad<2>(m3);
+  const Q29 X3 = red16p29(sub29(sub29(sub29(RR, PPP), Q), Q));
+  // Y3 = R (Q - X3) - S1 PPP | ZZZ3 = ZZZ1 ZZZ2 PPP (- 0 0)
+  const Q29 z = Q29::zero();
+  const Q29 m4 = red6p29(mulsub29(q29_sel(r0, R, ZZZ12), q29_sel(r0, norm29(sub29(Q, X3)), PPP),
+                                  q29_sel(r0, S1, z), q29_sel(r0, PPP, z)));
+  return {X3, q29_quad<0>(m4), ZZ3, q29_quad<1>(m4)};
+}
+
+__device__ __forceinline__ X29 x29_dbl_q4(const X29& p) {
+  if (x29_is_inf(p)) return p;
+  const uint32_t r = threadIdx.x & 3u;
+  const bool r0 = r == 0, r1 = r == 1, r2 = r == 2;
+  const Q29 U = normfull29(add29(p.Y, p.Y));
+  // V = U^2 | X2 = X^2
+  const Q29 s1 = sqr29(q29_sel((r & 1u) != 0u, p.X, U));
+  const Q29 V = q29_quad<0>(s1), X2 = q29_quad<1>(s1);
+  const Q29 M = normfull29(add29(add29(X2, X2), X2));
+  // W = U V | S = X V | ZZ3 = ZZ V | M^2
+  const Q29 m2 = mul29(q29_sel(r0, U, q29_sel(r1, p.X, q29_sel(r2, p.ZZ, M))), q29_sel(r < 3, V, M));
+  const Q29 W = q29_quad<0>(m2), S = q29_quad<1>(m2), ZZ3 = q29_quad<2>(m2), MM = q29_quad<3>(m2);
+  const Q29 X3 = red16p29(sub29(sub29(MM, S), S));
+  // Y3 = M (S - X3) - W Y | ZZZ3 = W ZZZ (- 0 0)
+  const Q29 z = Q29::zero();
+  const Q29 m3 = red6p29(mulsub29(q29_sel(r0, M, W), q29_sel(r0, norm29(sub29(S, X3)), p.ZZZ),
+                                  q29_sel(r0, W, z), q29_sel(r0, p.Y, z)));
+  return {X3, q29_quad<0>(m3), ZZ3, q29_quad<1>(m3)};
+}
+
+template <bool Q4>
+__device__ __forceinline__ X29 red_add(const X29& a, const X29& b) {
+  if constexpr (Q4) return x29_add_q4(a, b);
+  else return x29_add(a, b);
+}
+template <bool Q4>
+__device__ __forceinline__ X29 red_dbl(const X29& a) {
+  if constexpr (Q4) return x29_dbl_q4(a);
+  else return x29_dbl(a);
+}
+
+// Group fold: element g (< mv <= 2^gl, on lane stride ES = 4 for quads, 1
+// otherwise) holds (A_g, Y_g); elements >= mv hold infinity.  Afterwards
+// element 0 holds A = sum_g A_g + 2^flog sum_g g Y_g and Yw = 2^ylog sum_g Y_g.
+// mv is uniform over the wave; one addition and one doubling call site.
+template <bool Q4>
+__device__ __forceinline__ void msm_fold(X29& A, X29 Y, int gl, uint32_t mv, int flog, int ylog,
+                                         X29& Yw) {
+  constexpr uint32_t ES = Q4 ? 4 : 1;
+  const int width = (int)(ES << gl);
+  const uint32_t g = ((threadIdx.x & 63u) % (uint32_t)width) / ES;
+  int ns = 0;
+  while ((1u << ns) < mv) ns++;  // scan / tree steps
+  X29 Yd = Y;
+  for (int s = 0; s < 2 * ns + 1; s++) {
+    if (s == ns) {  // suffix sums done: the doublings (one site)
+      Yw = Y;
+      Yd = Y;
+      X29 t = Y;
+      const int nd = flog > ylog ? flog : ylog;
+      for (int i = 1; i <= nd; i++) {
+        t = red_dbl<Q4>(t);
+        if (i == flog) Yd = t;
+        if (i == ylog) Yw = t;
+      }
     }
-    run = x29_add(run, x29_load(P[l]));
-    if (Q) qsum = x29_add(qsum, x29_load(Q[l]));
-    acc = x29_add(wsum, Q ? qsum : run);
+    uint32_t d;
+    bool live;
+    X29 a, o;
+    if (s < ns) {  // inclusive suffix sums of Y
+      d = 1u << s;
+      o = x29_shfl_down(Y, d * ES, width);
+      a = Y;
+      live = g + d < mv;
+    } else if (s == ns) {  // + sum_{g>=1} Suf_g = sum_g g Y_g
+      o = Yd;
+      a = A;
+      live = g != 0 && g < mv;
+    } else {  // tree sum of A
+      d = (1u << ns) >> (s - ns);
+      o = x29_shfl_down(A, d * ES, width);
+      a = A;
+      live = g < d;
+    }
+    const X29 r = red_add<Q4>(a, x29_sel(live, o, x29_inf()));
+    if (s < ns) Y = r;
+    else A = r;
   }
-  // inclusive suffix scan of run over the block (Hillis-Steele, double sync)
-  sh_r[t] = x29_store(run);
-  __syncthreads();
-  for (uint32_t off = 1; off < T; off <<= 1) {
-    X29 v = run;
-    if (t + off < T) v = x29_add(run, x29_load(sh_r[t + off]));
-    __syncthreads();
-    sh_r[t] = x29_store(v);
-    run = v;
-    __syncthreads();
+}
+#endif
+
+// level 1 (grid.y = MSM of the batch): fold group w (2^gl lanes) writes
+// A_out[w], Y_out[w] with sum_j (j + 1) B_j = sum_w A_w + w Y_w
+__global__ void __launch_bounds__(MSM_BLOCK)
+    k_msm_bsum(const MsmRed* __restrict__ runs, uint32_t nb, int slog, int gl,
+               G1Xyzz* __restrict__ A_out, G1Xyzz* __restrict__ Y_out, size_t ostride) {
+#if defined(__HIP_DEVICE_COMPILE__)
+  const uint32_t t = blockIdx.x * blockDim.x + threadIdx.x;
+  const MsmRed rr = runs[blockIdx.y];
+  X29 run = x29_inf(), wsum = x29_inf(), B = x29_inf();
+  const uint64_t lo64 = (uint64_t)t << slog;
+  const uint32_t lo = lo64 < nb ? (uint32_t)lo64 : nb;
+  uint32_t j = nb - lo < (1u << slog) ? nb : lo + (1u << slog);
+  // one addition per iteration: stage 1 = bucket j += next partial slot,
+  // 2 = run += B_j, 3 = wsum += run; stage 0 starts the next bucket down
+  int stage = 0;
+  uint32_t slot = 0, last = 0, step = 1;
+  for (;;) {
+    if (stage == 0) {
+      if (j == lo) break;
+      j--;
+      const uint32_t s0 = rr.bstart[j], s1 = rr.bstart[j + 1];
+      if (s0 == s1) {
+        B = x29_inf();
+        stage = 2;
+      } else {
+        const uint32_t f = s0 / rr.L + j;
+        last = (s1 - 1) / rr.L + j;
+        B = msm_partial(rr.partial, f);
+        step = msm_slot_stride(last - f + 1);
+        slot = f + step;
+        stage = slot <= last ? 1 : 2;
+      }
+    }
+    X29 a, b;
+    if (stage == 1) {
+      a = B;
+      b = msm_partial(rr.partial, slot);
+    } else {
+      a = stage == 2 ? run : wsum;
+      b = stage == 2 ? B : run;
+    }
+    const X29 r = x29_add(a, b);
+    if (stage == 1) {
+      B = r;
+      slot += step;
+      if (slot > last) stage = 2;
+    } else if (stage == 2) {
+      run = r;
+      stage = 3;
+    } else {
+      wsum = r;
+      stage = 0;
+    }
   }
-  const X29 total_run = x29_load(sh_r[0]);
-  // one tree sum of y_t = acc_t + S Suf_t (t >= 1), acc_0
-  const X29 y = t ? x29_add(acc, x29_dbl_k(run, slog)) : acc;
-  __syncthreads();
-  sh_a[t] = x29_store(y);
-  __syncthreads();
-  for (uint32_t s = T / 2; s > 0; s >>= 1) {
-    if (t < s) sh_a[t] = x29_store(x29_add(x29_load(sh_a[t]), x29_load(sh_a[t + s])));
-    __syncthreads();
+  X29 Yw;
+  msm_fold<false>(wsum, run, gl, 1u << gl, slog, gl + slog, Yw);
+  if ((t & ((1u << gl) - 1)) == 0) {
+    const size_t w = (size_t)blockIdx.y * ostride + (t >> gl);
+    A_out[w] = x29_store(wsum);
+    Y_out[w] = x29_store(Yw);
   }
-  if (t == 0) {
-    A_out[blockIdx.x] = sh_a[0];
-    if (R_out) R_out[blockIdx.x] = x29_store(x29_dbl_k(total_run, rlog));
+#endif
+}
+
+// next levels: m elements (A_e, Y_e), total sum_e A_e + e Y_e; group w (16
+// elements on quads, or 64 single-lane elements) writes (A'_w, Y'_w) of the
+// same form, or only A'_w (the total) when Y_out is null
+template <bool Q4>
+__global__ void __launch_bounds__(64)
+    k_msm_wfold(const G1Xyzz* __restrict__ A_in, const G1Xyzz* __restrict__ Y_in, uint32_t m,
+                size_t istride, G1Xyzz* __restrict__ A_out, G1Xyzz* __restrict__ Y_out,
+                size_t ostride) {
+#if defined(__HIP_DEVICE_COMPILE__)
+  constexpr uint32_t ES = Q4 ? 4 : 1, G = 64 / ES;
+  const uint32_t e0 = blockIdx.x * G, e = e0 + threadIdx.x / ES;
+  const uint32_t mv = m - e0 < G ? m - e0 : G;
+  X29 A = x29_inf(), Y = x29_inf();
+  if (e < m) {
+    A = x29_load(A_in[(size_t)blockIdx.y * istride + e]);
+    Y = x29_load(Y_in[(size_t)blockIdx.y * istride + e]);
   }
+  const int gl = Q4 ? 4 : 6;
+  X29 Yw;
+  msm_fold<Q4>(A, Y, gl, mv, 0, Y_out ? gl : 0, Yw);
+  if (threadIdx.x == 0) {
+    const size_t w = (size_t)blockIdx.y * ostride + blockIdx.x;
+    A_out[w] = x29_store(A);
+    if (Y_out) Y_out[w] = x29_store(Yw);
+  }
+#endif
 }
 
 // R = 2^261 XYZZ words -> R = 2^256 Montgomery XYZZ (canonical) for the host
@@ -971,15 +1152,24 @@ static MsmRun msm_accumulate_phase(qg_ctx* ctx, const qg_srs* srs, const Fr* d_s
     const int ntiles = (int)div_up(nb, SCAN_TILE);
     uint2* tile_tot = ctx->scratch_as<uint2>("msm_tiles", ntiles);
     // entries per accumulation thread (flat chunks, k_msm_accumulate): 64, or
-    // 128 for the largest MSMs, fewer while that would leave < 8 waves of
-    // threads per resident slot (256 CUs x 12 waves)
-    // (128 from 2^27 entries on: 2^24 x 13 windows measured 19.92 vs 20.03 ms,
-    // fewer partials for the reduction; 2^22 is faster at 64)
-    int elog = max_entries >= ((size_t)1 << 27) ? 7 : 6;
-    while (elog > 2 && (max_entries >> elog) < (size_t)ctx->num_cus() * 16 * 64 * 3) elog--;
-    if (const char* ov = getenv("QG_MSM_ELOG")) elog = atoi(ov);  // tuning experiments
-    QG_CHECK(elog >= 0 && elog <= 12, QG_ERR_INVALID, "QG_MSM_ELOG out of range");
-    const uint32_t L = 1u << elog;
+    // 128 for the largest MSMs, fewer while that would leave < 3 waves of
+    // threads per resident slot (256 CUs x 16 waves).  Measured against equal
+    // splits into 1 / 2 / 3 whole waves of the chip (QG_MSM_ROUNDS, which also
+    // leave fewer partials for the reduction): the accumulate loses 0.3-0.5 ms
+    // at 2^24 with 1-2 waves, and 3 waves is no faster than 128 entries.
+    uint32_t L;
+    if (const char* ov = getenv("QG_MSM_ROUNDS")) {  // tuning experiments
+      const int rounds = atoi(ov);
+      QG_CHECK(rounds >= 1 && rounds <= 64, QG_ERR_INVALID, "QG_MSM_ROUNDS out of range");
+      const size_t resident = (size_t)ctx->num_cus() * 16 * 64;
+      L = (uint32_t)((div_up(max_entries, resident * rounds) + 3) & ~(size_t)3);
+    } else {
+      int elog = max_entries >= ((size_t)1 << 27) ? 7 : 6;
+      while (elog > 2 && (max_entries >> elog) < (size_t)ctx->num_cus() * 16 * 64 * 3) elog--;
+      L = 1u << elog;
+    }
+    if (const char* ov = getenv("QG_MSM_ELOG")) L = 1u << atoi(ov);  // tuning experiments
+    QG_CHECK(L >= 1 && L <= 65536, QG_ERR_INVALID, "MSM chunk length out of range");
     const size_t max_threads = div_up(max_entries, L);
     const size_t nslots = max_threads + nb + 1;  // partial slot of (thread t, bucket b): t + b
     X29Raw* partial = ctx->scratch_as<X29Raw>("msm_partial" + sfx, nslots);
@@ -1041,7 +1231,7 @@ static MsmRun msm_accumulate_phase(qg_ctx* ctx, const qg_srs* srs, const Fr* d_s
                          cbase, chist, LO, nb, counts);
       QG_LAUNCH_CHECK();
       hipLaunchKernelGGL(k_scan_tiles, dim3(ntiles), dim3(SCAN_BLOCK), 0, ctx->stream, counts,
-                         (size_t)nb, elog, bstart, tstart, tile_tot, misc + 1);
+                         (size_t)nb, L, bstart, tstart, tile_tot, misc + 1);
       QG_LAUNCH_CHECK();
       hipLaunchKernelGGL(k_scan_top, dim3(1), dim3(1024), 0, ctx->stream, tile_tot, ntiles,
                          bstart, tstart, (size_t)nb);
@@ -1101,23 +1291,31 @@ static void msm_reduce_phase(qg_ctx* ctx, const qg_srs* srs, const std::vector<M
   QG_HIP(hipMemcpyAsync(mx.data(), d_mx, kl * sizeof(uint32_t), hipMemcpyDeviceToHost,
                         ctx->stream));
   QG_HIP(hipStreamSynchronize(ctx->stream));
-  int slog1 = nb >= 8u * MSM_BLOCK ? 3 : 0;
+  // level 1: S = 2^slog1 buckets per thread, as many threads as the chip has
+  // SIMD lanes (one wave per SIMD) over the whole batch; folds of 2^gl1 lanes
+  const size_t lanes = (size_t)ctx->num_cus() * 4 * 64;
+  int slog1 = 0;
+  while (slog1 < 12 && ((size_t)kl * nb >> (slog1 + 1)) >= lanes) slog1++;
   if (const char* ov = getenv("QG_MSM_SLOG1")) slog1 = atoi(ov);  // tuning experiments
-  QG_CHECK(slog1 >= 0 && slog1 <= 8, QG_ERR_INVALID, "QG_MSM_SLOG1 out of range");
-  const uint32_t nred = div_up(nb, (size_t)MSM_BLOCK << slog1);
-  int slog2 = 0;
-  while (((size_t)MSM_BLOCK << slog2) < nred) slog2++;
-  QG_CHECK(slog2 <= 12, QG_ERR_UNSUPPORTED, "bucket count too large");
-  G1Xyzz* buckets = ctx->scratch_as<G1Xyzz>("msm_buckets", (size_t)kl * nb);
-  const size_t rstride = 2 * (size_t)nred + 1;  // per MSM: A[nred] | R[nred] | total
-  G1Xyzz* red = ctx->scratch_as<G1Xyzz>("msm_red", (size_t)kl * rstride);
+  QG_CHECK(slog1 >= 0 && slog1 <= 12, QG_ERR_INVALID, "QG_MSM_SLOG1 out of range");
+  int gl1 = 4;
+  if (const char* ov = getenv("QG_MSM_GL1")) gl1 = atoi(ov);  // tuning experiments
+  QG_CHECK(gl1 >= 0 && gl1 <= 6, QG_ERR_INVALID, "QG_MSM_GL1 out of range");
+  const uint32_t g1 = div_up(div_up(nb, (size_t)1 << slog1), MSM_BLOCK);
+  const uint32_t m1 = g1 * (MSM_BLOCK >> gl1);  // level-1 groups per MSM
+  const uint32_t m2 = div_up(m1, 16);
+  G1Xyzz* A1 = ctx->scratch_as<G1Xyzz>("msm_redA1", (size_t)kl * m1);
+  G1Xyzz* Y1 = ctx->scratch_as<G1Xyzz>("msm_redY1", (size_t)kl * m1);
+  G1Xyzz* A2 = ctx->scratch_as<G1Xyzz>("msm_redA2", (size_t)kl * m2);
+  G1Xyzz* Y2 = ctx->scratch_as<G1Xyzz>("msm_redY2", (size_t)kl * m2);
+  G1Xyzz* fin = ctx->scratch_as<G1Xyzz>("msm_red_total", kl);
   G1Xyzz* d_out = ctx->scratch_as<G1Xyzz>("msm_out", kl);
   MsmRed* d_runs = ctx->scratch_as<MsmRed>("msm_runs", kl);
   std::vector<MsmRed> h_runs(kl);
   {
     QgTimed tm(ctx, "msm_reduce");
     // tree steps only until every bucket has <= MSM_COMBINE_SEQ partials left;
-    // the combine adds those sequentially.  A bucket of count c spans at most
+    // level 1 adds those sequentially.  A bucket of count c spans at most
     // ceil(c / L) + 1 slots.
     for (uint32_t q = 0; q < kl; q++) {
       const MsmRun& r = runs[live[q]];
@@ -1129,26 +1327,37 @@ static void msm_reduce_phase(qg_ctx* ctx, const qg_srs* srs, const std::vector<M
         QG_LAUNCH_CHECK();
         st <<= 1;
       }
-      h_runs[q] = {r.partial, r.bstart, r.L, st};
+      h_runs[q] = {r.partial, r.bstart, r.L};
     }
     QG_HIP(hipMemcpyAsync(d_runs, h_runs.data(), kl * sizeof(MsmRed), hipMemcpyHostToDevice,
                           ctx->stream));
-    hipLaunchKernelGGL(k_msm_combine, dim3(div_up(nb, MSM_BLOCK), kl), dim3(MSM_BLOCK), 0,
-                       ctx->stream, d_runs, nb, buckets);
+    hipLaunchKernelGGL(k_msm_bsum, dim3(g1, kl), dim3(MSM_BLOCK), 0, ctx->stream, d_runs, nb,
+                       slog1, gl1, A1, Y1, (size_t)m1);
     QG_LAUNCH_CHECK();
-    // level 1: A = red[0, nred), R = red[nred, 2 nred); level 2: red[2 nred]
-    hipLaunchKernelGGL(k_msm_wsum, dim3(nred, kl), dim3(MSM_BLOCK), 0, ctx->stream, buckets,
-                       (const G1Xyzz*)nullptr, nb, slog1, 8 + slog1, red, red + nred, (size_t)nb,
-                       rstride);
-    QG_LAUNCH_CHECK();
-    const uint32_t t2 = div_up(nred, (size_t)1 << slog2);
-    hipLaunchKernelGGL(k_msm_wsum, dim3(1, kl), dim3(t2 < 64 ? 64 : t2), 0, ctx->stream,
-                       red + nred, red, nred, slog2, 0, red + 2 * nred, (G1Xyzz*)nullptr, rstride,
-                       rstride);
+    // wave folds, 64 elements per wave, until one element per MSM is left
+    G1Xyzz *Ai = A1, *Yi = Y1, *Ao = A2, *Yo = Y2;
+    size_t istride = m1;
+    uint32_t m = m1;
+    // (quad-cooperative folds of 16 by default: the lanes are idle up here)
+    bool q4 = true;
+    if (const char* ov = getenv("QG_MSM_Q4")) q4 = atoi(ov) != 0;  // A/B experiments
+    const uint32_t per = q4 ? 16 : 64;
+    auto fold = q4 ? k_msm_wfold<true> : k_msm_wfold<false>;
+    while (m > per) {
+      const uint32_t mo = div_up(m, per);
+      hipLaunchKernelGGL(fold, dim3(mo, kl), dim3(64), 0, ctx->stream, Ai, Yi, m, istride, Ao, Yo,
+                         (size_t)mo);
+      QG_LAUNCH_CHECK();
+      std::swap(Ai, Ao);
+      std::swap(Yi, Yo);
+      istride = mo;
+      m = mo;
+    }
+    hipLaunchKernelGGL(fold, dim3(1, kl), dim3(64), 0, ctx->stream, Ai, Yi, m, istride, fin,
+                       (G1Xyzz*)nullptr, (size_t)1);
     QG_LAUNCH_CHECK();
   }
-  hipLaunchKernelGGL(k_msm_export, dim3(1), dim3(1024), 0, ctx->stream, red + 2 * nred, rstride, kl,
-                     d_out);
+  hipLaunchKernelGGL(k_msm_export, dim3(1), dim3(1024), 0, ctx->stream, fin, (size_t)1, kl, d_out);
   QG_LAUNCH_CHECK();
   std::vector<G1Xyzz> h(kl);
   QG_HIP(hipMemcpyAsync(h.data(), d_out, kl * sizeof(G1Xyzz), hipMemcpyDeviceToHost, ctx->stream));
