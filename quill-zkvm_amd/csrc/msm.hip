@@ -29,7 +29,6 @@ using namespace qg;
 
 namespace qg {
 
-static constexpr uint32_t MSM_COMBINE_SEQ = 4;  // partials the reduction adds per bucket in a row
 static constexpr int MSM_BLOCK = 256;
 
 // Window size for an SRS of n bases.  Cost model in bucket-addition units:
@@ -547,8 +546,13 @@ __global__ void k_scan_top(uint2* __restrict__ tile_tot, int ntiles, uint32_t* _
   }
 }
 
+// final bucket starts; misc[2] / misc[3] = first / last partial slot of the
+// buckets with more than T partial slots (msm_combine_run: the reduction's
+// tree steps run over that range only)
 __global__ void k_scan_add(const uint2* __restrict__ tile_off, size_t nb, uint32_t* __restrict__ bstart,
-                           uint32_t* __restrict__ tstart, uint32_t* __restrict__ cursor) {
+                           uint32_t* __restrict__ tstart, uint32_t* __restrict__ cursor,
+                           const uint32_t* __restrict__ counts, uint32_t L, uint32_t T,
+                           uint32_t* __restrict__ misc) {
   size_t i = (size_t)blockIdx.x * blockDim.x + threadIdx.x;
   if (i >= nb) return;
   uint2 off = tile_off[i / SCAN_TILE];
@@ -556,6 +560,14 @@ __global__ void k_scan_add(const uint2* __restrict__ tile_off, size_t nb, uint32
   bstart[i] = b;
   cursor[i] = b;
   tstart[i] += off.y;
+  const uint32_t c = counts[i];
+  if (c > (T - 1) * L) {  // may span more than T slots
+    const uint32_t f = b / L + (uint32_t)i, l = (b + c - 1) / L + (uint32_t)i;
+    if (l - f + 1 > T) {
+      atomicMin(misc + 2, f);
+      atomicMax(misc + 3, l);
+    }
+  }
 }
 
 // ---- accumulation ---------------------------------------------------------
@@ -654,12 +666,13 @@ QG_DEV uint32_t msm_slot_last(const uint32_t* bstart, uint32_t b, uint32_t L) {
 }
 
 // stride between a bucket's partial slots after the tree steps: buckets with
-// more than MSM_COMBINE_SEQ slots (skewed digits: the short top window, small
-// scalars) are pre-summed pairwise until at most that many remain, so one lane
-// of the reduction never adds a long run of partials while the others wait
-QG_DEV uint32_t msm_slot_stride(uint32_t nslot) {
+// more than T slots (skewed digits: the short top window, small scalars) are
+// pre-summed pairwise until at most T remain, so one lane of the reduction
+// never adds a long run of partials while the others wait.  T = the typical
+// slot count + 1 (msm_combine_run): the tree steps touch only skewed buckets.
+QG_DEV uint32_t msm_slot_stride(uint32_t nslot, uint32_t T) {
   uint32_t st = 1;
-  while (nslot > MSM_COMBINE_SEQ * st) st <<= 1;
+  while (nslot > T * st) st <<= 1;
   return st;
 }
 
@@ -669,13 +682,14 @@ QG_DEV uint32_t msm_slot_stride(uint32_t nslot) {
 // and are skipped.
 __global__ void __launch_bounds__(MSM_BLOCK)
     k_msm_tree_step(X29Raw* __restrict__ partial, const uint32_t* __restrict__ owner,
-                    const uint32_t* __restrict__ bstart, uint32_t L, uint32_t nslots, uint32_t s) {
-  const uint32_t i = blockIdx.x * blockDim.x + threadIdx.x;
-  if (i >= nslots) return;
+                    const uint32_t* __restrict__ bstart, uint32_t L, uint32_t T, uint32_t s_lo,
+                    uint32_t s_end, uint32_t s) {
+  const uint32_t i = s_lo + blockIdx.x * blockDim.x + threadIdx.x;
+  if (i >= s_end) return;
   const uint32_t b = owner[i];
   if (b == 0xffffffffu) return;
   const uint32_t f = msm_slot_first(bstart, b, L), l = msm_slot_last(bstart, b, L);
-  if (l - f + 1 <= MSM_COMBINE_SEQ * s) return;  // this bucket is done at this level
+  if (l - f + 1 <= T * s) return;  // this bucket is done at this level
   const uint32_t off = i - f;
   if ((off & (2 * s - 1)) == 0 && i + s <= l)
     partial[i] = x29_raw(x29_add(msm_partial(partial, i), msm_partial(partial, i + s)));
@@ -705,7 +719,7 @@ __global__ void __launch_bounds__(MSM_BLOCK)
 struct MsmRed {
   const X29Raw* partial;
   const uint32_t* bstart;
-  uint32_t L;
+  uint32_t L, T;
 };
 
 #if defined(__HIP_DEVICE_COMPILE__)
@@ -886,7 +900,7 @@ __global__ void __launch_bounds__(MSM_BLOCK)
         const uint32_t f = s0 / rr.L + j;
         last = (s1 - 1) / rr.L + j;
         B = msm_partial(rr.partial, f);
-        step = msm_slot_stride(last - f + 1);
+        step = msm_slot_stride(last - f + 1, rr.T);
         slot = f + step;
         stage = slot <= last ? 1 : 2;
       }
@@ -1098,7 +1112,7 @@ static qg_srs* srs_alloc(qg_ctx* ctx, size_t n) {
 // bucket offsets (per-slot scratch, so a batch's reductions run together).
 struct MsmRun {
   bool empty = true;
-  uint32_t L = 1;
+  uint32_t L = 1, T = 4;  // chunk length; partials per bucket the reduction adds in a row
   size_t nslots = 0;
   X29Raw* partial = nullptr;
   uint32_t* owner = nullptr;
@@ -1169,6 +1183,10 @@ static MsmRun msm_accumulate_phase(qg_ctx* ctx, const qg_srs* srs, const Fr* d_s
       L = 1u << elog;
     }
     if (const char* ov = getenv("QG_MSM_ELOG")) L = 1u << atoi(ov);  // tuning experiments
+    // partial slots a bucket's sum adds in a row in the reduction: the typical
+    // count + 1 (a bucket of c entries spans ceil(c / L) or one more slots);
+    // skewed buckets beyond it are pre-summed by tree steps
+    const uint32_t T = std::max<uint32_t>(4, (uint32_t)div_up(div_up(max_entries, nb), L) + 2);
     QG_CHECK(L >= 1 && L <= 65536, QG_ERR_INVALID, "MSM chunk length out of range");
     const size_t max_threads = div_up(max_entries, L);
     const size_t nslots = max_threads + nb + 1;  // partial slot of (thread t, bucket b): t + b
@@ -1220,6 +1238,7 @@ static MsmRun msm_accumulate_phase(qg_ctx* ctx, const qg_srs* srs, const Fr* d_s
       QG_LAUNCH_CHECK();
       // pass B: sort every group by the low bits, in chunks
       QG_HIP(hipMemsetAsync(misc, 0, 4 * sizeof(uint32_t), ctx->stream));
+      QG_HIP(hipMemsetAsync(misc + 2, 0xff, sizeof(uint32_t), ctx->stream));  // slot range: empty
       hipLaunchKernelGGL(k_sort_chunks, dim3(1), dim3(1024), 0, ctx->stream, goff, nblk, H,
                          gstart, cbase, cgroup, misc);
       QG_LAUNCH_CHECK();
@@ -1237,7 +1256,7 @@ static MsmRun msm_accumulate_phase(qg_ctx* ctx, const qg_srs* srs, const Fr* d_s
                          bstart, tstart, (size_t)nb);
       QG_LAUNCH_CHECK();
       hipLaunchKernelGGL(k_scan_add, dim3(div_up(nb, 256)), dim3(256), 0, ctx->stream, tile_tot,
-                         (size_t)nb, bstart, tstart, cursor);
+                         (size_t)nb, bstart, tstart, cursor, counts, L, T, misc);
       QG_LAUNCH_CHECK();
       hipLaunchKernelGGL(k_sort_chunk_offsets, dim3(div_up(nb, 256)), dim3(256), 0, ctx->stream,
                          cbase, chist, LO, nb, bstart, coff);
@@ -1257,6 +1276,7 @@ static MsmRun msm_accumulate_phase(qg_ctx* ctx, const qg_srs* srs, const Fr* d_s
     }
     run.empty = n == 0;
     run.L = L;
+    run.T = T;
     run.nslots = nslots;
     run.partial = partial;
     run.owner = owner;
@@ -1282,13 +1302,14 @@ static void msm_reduce_phase(qg_ctx* ctx, const qg_srs* srs, const std::vector<M
   QG_CHECK(live.size() <= 1024, QG_ERR_UNSUPPORTED, "MSM batch too large");
   const uint32_t kl = (uint32_t)live.size();
   const uint32_t nb = 1u << (srs->c - 1);
-  // max accumulation threads per bucket of every MSM (one transfer)
-  uint32_t* d_mx = ctx->scratch_as<uint32_t>("msm_maxtpb", kl);
+  // per MSM (one transfer): max accumulation threads per bucket, and the
+  // partial-slot range of the buckets the tree steps pre-sum
+  uint32_t* d_mx = ctx->scratch_as<uint32_t>("msm_maxtpb", 3 * (size_t)kl);
   for (uint32_t q = 0; q < kl; q++)
-    QG_HIP(hipMemcpyAsync(d_mx + q, runs[live[q]].misc + 1, sizeof(uint32_t),
+    QG_HIP(hipMemcpyAsync(d_mx + 3 * q, runs[live[q]].misc + 1, 3 * sizeof(uint32_t),
                           hipMemcpyDeviceToDevice, ctx->stream));
-  std::vector<uint32_t> mx(kl);
-  QG_HIP(hipMemcpyAsync(mx.data(), d_mx, kl * sizeof(uint32_t), hipMemcpyDeviceToHost,
+  std::vector<uint32_t> mx(3 * (size_t)kl);
+  QG_HIP(hipMemcpyAsync(mx.data(), d_mx, 3 * kl * sizeof(uint32_t), hipMemcpyDeviceToHost,
                         ctx->stream));
   QG_HIP(hipStreamSynchronize(ctx->stream));
   // level 1: S = 2^slog1 buckets per thread, as many threads as the chip has
@@ -1314,20 +1335,22 @@ static void msm_reduce_phase(qg_ctx* ctx, const qg_srs* srs, const std::vector<M
   std::vector<MsmRed> h_runs(kl);
   {
     QgTimed tm(ctx, "msm_reduce");
-    // tree steps only until every bucket has <= MSM_COMBINE_SEQ partials left;
+    // tree steps only until every bucket has <= T partials left;
     // level 1 adds those sequentially.  A bucket of count c spans at most
     // ceil(c / L) + 1 slots.
     for (uint32_t q = 0; q < kl; q++) {
       const MsmRun& r = runs[live[q]];
-      const uint32_t max_slots = mx[q] + 1;
+      const uint32_t max_slots = mx[3 * q] + 1, s_lo = mx[3 * q + 1], s_hi = mx[3 * q + 2];
       uint32_t st = 1;
-      while ((size_t)st * MSM_COMBINE_SEQ < max_slots) {
-        hipLaunchKernelGGL(k_msm_tree_step, dim3(div_up(r.nslots, MSM_BLOCK)), dim3(MSM_BLOCK), 0,
-                           ctx->stream, r.partial, r.owner, r.bstart, r.L, (uint32_t)r.nslots, st);
+      while (s_lo <= s_hi && (size_t)st * r.T < max_slots) {
+        QG_CHECK(s_hi < r.nslots, QG_ERR_ASSERT, "MSM partial-slot range");
+        hipLaunchKernelGGL(k_msm_tree_step, dim3(div_up(s_hi - s_lo + 1, MSM_BLOCK)), dim3(MSM_BLOCK),
+                           0, ctx->stream, r.partial, r.owner, r.bstart, r.L, r.T, s_lo, s_hi + 1,
+                           st);
         QG_LAUNCH_CHECK();
         st <<= 1;
       }
-      h_runs[q] = {r.partial, r.bstart, r.L};
+      h_runs[q] = {r.partial, r.bstart, r.L, r.T};
     }
     QG_HIP(hipMemcpyAsync(d_runs, h_runs.data(), kl * sizeof(MsmRed), hipMemcpyHostToDevice,
                           ctx->stream));
