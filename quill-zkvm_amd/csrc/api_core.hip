@@ -184,6 +184,7 @@ int qg_ctx_destroy(qg_ctx* ctx) {
   if (!ctx) return QG_OK;
   (void)hipSetDevice(ctx->device);
   if (ctx->stream) (void)hipStreamSynchronize(ctx->stream);
+  if (ctx->copy_stream) (void)hipStreamSynchronize(ctx->copy_stream);
   comm_release(ctx);
   for (auto& kv : ctx->scratch) (void)hipFree(kv.second.first);
   for (auto& kv : ctx->pinned) (void)hipHostFree(kv.second.first);
@@ -193,6 +194,7 @@ int qg_ctx_destroy(qg_ctx* ctx) {
   }
   for (auto e : ctx->event_pool) (void)hipEventDestroy(e);
   if (ctx->stream) (void)hipStreamDestroy(ctx->stream);
+  if (ctx->copy_stream) (void)hipStreamDestroy(ctx->copy_stream);
   delete ctx;
   return QG_OK;
 }

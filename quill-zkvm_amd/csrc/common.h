@@ -44,6 +44,7 @@ struct qg_comm_state;  // RCCL (comm.hip)
 struct qg_ctx {
   int device = 0;
   hipStream_t stream = nullptr;
+  hipStream_t copy_stream = nullptr;  // host-to-device uploads overlapped with kernels (msm_host)
   std::string last_error;
   // grow-only scratch arena, one slot per purpose
   std::map<std::string, std::pair<void*, size_t>> scratch;

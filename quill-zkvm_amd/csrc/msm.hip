@@ -191,7 +191,8 @@ __device__ __forceinline__ int lds_upper(const uint32_t* off, int n, uint32_t p)
 // The block's counts and global offsets are contiguous rows (hrow / orow).
 // Output per digit: the table entry (u32) and the bucket's low LO bits (u16).
 __global__ void __launch_bounds__(SORT_BLOCK)
-    k_sortA_scatter(const Fr* __restrict__ canon, size_t n, size_t N, int c, int W, int LO, int H,
+    k_sortA_scatter(const Fr* __restrict__ canon, size_t n, size_t N, size_t off, int c, int W, int LO,
+                    int H,
                     uint32_t nblk, uint32_t tile, const uint32_t* __restrict__ hrow,
                     const uint32_t* __restrict__ orow, uint32_t* __restrict__ tmp_e,
                     uint16_t* __restrict__ tmp_l) {
@@ -228,7 +229,7 @@ __global__ void __launch_bounds__(SORT_BLOCK)
     for_each_digit(sv[j], c, W, [&](int w, uint32_t b, bool neg) {
       const uint32_t g = b >> LO;
       const uint32_t slot = loff[g] + atomicAdd(&cur[g], 1u);
-      ent[slot] = (uint32_t)((size_t)w * N + i) | (neg ? 0x80000000u : 0u);
+      ent[slot] = (uint32_t)((size_t)w * N + off + i) | (neg ? 0x80000000u : 0u);
       bkt[slot] = b;
     });
   }
@@ -1120,10 +1121,11 @@ struct MsmRun {
   uint32_t* misc = nullptr;  // [0] nchunks, [1] max accumulation threads per bucket
 };
 
-// bucketing (two-pass radix sort) + bucket accumulation of MSM `slot` of a batch
+// bucketing (two-pass radix sort) + bucket accumulation of MSM `slot` of a
+// batch: sum_i d_scalars[i] * base[srs_off + i]
 static MsmRun msm_accumulate_phase(qg_ctx* ctx, const qg_srs* srs, const Fr* d_scalars, size_t n,
-                                   int slot) {
-  QG_CHECK(n <= srs->n, QG_ERR_INVALID, "MSM length exceeds the SRS");
+                                   int slot, size_t srs_off = 0) {
+  QG_CHECK(srs_off <= srs->n && n <= srs->n - srs_off, QG_ERR_INVALID, "MSM length exceeds the SRS");
   MsmRun run;
   const std::string sfx = "#" + std::to_string(slot);
   if (n > 0) {
@@ -1234,7 +1236,7 @@ static MsmRun msm_accumulate_phase(qg_ctx* ctx, const qg_srs* srs, const Fr* d_s
         ctx->memo["msm_lds_attr"] = "1";
       }
       hipLaunchKernelGGL(k_sortA_scatter, dim3(nblk), dim3(SORT_BLOCK), smemA, ctx->stream,
-                         canon, n, srs->n, c, W, LO, H, nblk, tile, hrow, orow, tmp_e, tmp_l);
+                         canon, n, srs->n, srs_off, c, W, LO, H, nblk, tile, hrow, orow, tmp_e, tmp_l);
       QG_LAUNCH_CHECK();
       // pass B: sort every group by the low bits, in chunks
       QG_HIP(hipMemsetAsync(misc, 0, 4 * sizeof(uint32_t), ctx->stream));
@@ -1388,6 +1390,24 @@ static void msm_reduce_phase(qg_ctx* ctx, const qg_srs* srs, const std::vector<M
   for (uint32_t q = 0; q < kl; q++) out[live[q]] = h[q];
 }
 
+// per-rank XYZZ partial -> the MSM over all ranks, affine (allgather + host EC
+// adds: RCCL cannot add curve points)
+static G1Affine msm_finish_ranks(qg_ctx* ctx, G1Xyzz acc) {
+  if (ctx->world > 1) {
+    G1Xyzz* d_send = ctx->scratch_as<G1Xyzz>("msm_comm_send", 1);
+    G1Xyzz* d_recv = ctx->scratch_as<G1Xyzz>("msm_comm_recv", ctx->world);
+    QG_HIP(hipMemcpyAsync(d_send, &acc, sizeof(G1Xyzz), hipMemcpyHostToDevice, ctx->stream));
+    comm_allgather_bytes(ctx, d_send, d_recv, sizeof(G1Xyzz));
+    std::vector<G1Xyzz> all(ctx->world);
+    QG_HIP(hipMemcpyAsync(all.data(), d_recv, sizeof(G1Xyzz) * ctx->world, hipMemcpyDeviceToHost,
+                          ctx->stream));
+    ctx->sync();
+    acc = G1Xyzz::infinity();
+    for (int r = 0; r < ctx->world; r++) acc = xyzz_add(acc, all[r]);
+  }
+  return xyzz_to_affine(acc);
+}
+
 // k MSMs over the same SRS (KZG openings of one proof); results per MSM,
 // summed over the RCCL ranks when a communicator is attached
 std::vector<G1Affine> msm_device_batch(qg_ctx* ctx, const qg_srs* srs,
@@ -1400,24 +1420,45 @@ std::vector<G1Affine> msm_device_batch(qg_ctx* ctx, const qg_srs* srs,
   std::vector<G1Xyzz> local;
   msm_reduce_phase(ctx, srs, runs, local);
   std::vector<G1Affine> res(local.size());
-  for (size_t i = 0; i < local.size(); i++) {
-    G1Xyzz acc = local[i];
-    if (ctx->world > 1) {
-      // sum of the per-rank partial MSMs (allgather + host EC adds; RCCL cannot add points)
-      G1Xyzz* d_send = ctx->scratch_as<G1Xyzz>("msm_comm_send", 1);
-      G1Xyzz* d_recv = ctx->scratch_as<G1Xyzz>("msm_comm_recv", ctx->world);
-      QG_HIP(hipMemcpyAsync(d_send, &acc, sizeof(G1Xyzz), hipMemcpyHostToDevice, ctx->stream));
-      comm_allgather_bytes(ctx, d_send, d_recv, sizeof(G1Xyzz));
-      std::vector<G1Xyzz> all(ctx->world);
-      QG_HIP(hipMemcpyAsync(all.data(), d_recv, sizeof(G1Xyzz) * ctx->world,
-                            hipMemcpyDeviceToHost, ctx->stream));
-      ctx->sync();
-      acc = G1Xyzz::infinity();
-      for (int r = 0; r < ctx->world; r++) acc = xyzz_add(acc, all[r]);
-    }
-    res[i] = xyzz_to_affine(acc);
-  }
+  for (size_t i = 0; i < local.size(); i++) res[i] = msm_finish_ranks(ctx, local[i]);
   return res;
+}
+
+// MSM of host-resident scalars (qg_kzg_commit / qg_msm_g1): the scalars go up
+// in P pieces on a copy stream and piece k's bucketing + accumulation, queued
+// before the host starts the (host-blocking, pageable) copy of piece k + 1,
+// runs under that copy; the pieces share one batched reduction and their
+// partial sums are added.  P = n / 2^21 pieces, at most 8 (2^24 on MI355X:
+// 33.0 ms with the whole copy first, 25.8 / 23.8 / 23.5 ms in 2 / 4 / 8
+// pieces; profiles/r03_host_commit_pieces.txt); QG_MSM_PIECES overrides.
+static G1Affine msm_host(qg_ctx* ctx, const qg_srs* srs, const uint64_t* h, size_t n) {
+  Fr* d = ctx->scratch_as<Fr>("msm_scalars", n ? n : 1);
+  int P = (int)std::min<size_t>(8, std::max<size_t>(1, n >> 21));
+  if (const char* ov = getenv("QG_MSM_PIECES")) P = atoi(ov);  // tuning experiments
+  QG_CHECK(P >= 1 && P <= 64, QG_ERR_INVALID, "QG_MSM_PIECES out of range");
+  if (P == 1 || n < (size_t)P) {
+    fr_upload(ctx, d, h, n);
+    return msm_device(ctx, srs, d, n);
+  }
+  if (!ctx->copy_stream) QG_HIP(hipStreamCreateWithFlags(&ctx->copy_stream, hipStreamNonBlocking));
+  std::vector<MsmRun> runs;
+  const size_t per = div_up(n, (size_t)P);
+  for (int k = 0; k < P; k++) {
+    const size_t off = (size_t)k * per, len = std::min(per, n - std::min(n, off));
+    if (len == 0) break;
+    QG_HIP(hipMemcpyAsync(d + off, h + 4 * off, len * sizeof(Fr), hipMemcpyHostToDevice,
+                          ctx->copy_stream));
+    hipEvent_t ev = ctx->ev_get();
+    QG_HIP(hipEventRecord(ev, ctx->copy_stream));
+    QG_HIP(hipStreamWaitEvent(ctx->stream, ev, 0));
+    ctx->event_pool.push_back(ev);
+    runs.push_back(msm_accumulate_phase(ctx, srs, d + off, len, k, off));
+  }
+  std::vector<G1Xyzz> part;
+  msm_reduce_phase(ctx, srs, runs, part);
+  G1Xyzz acc = G1Xyzz::infinity();
+  for (const G1Xyzz& q : part) acc = xyzz_add(acc, q);
+  return msm_finish_ranks(ctx, acc);
 }
 
 G1Affine msm_device(qg_ctx* ctx, const qg_srs* srs, const Fr* d_scalars, size_t n) {
@@ -1675,9 +1716,7 @@ int qg_msm_g1(qg_ctx* ctx, const qg_srs* srs, const uint64_t* scalars, size_t n,
     QG_HIP(hipSetDevice(ctx->device));
     // msm_unchecked truncates to min(len(bases), len(scalars))
     size_t m = n < srs->n ? n : srs->n;
-    Fr* d = ctx->scratch_as<Fr>("msm_scalars", m ? m : 1);
-    fr_upload(ctx, d, scalars, m);
-    G1Affine r = msm_device(ctx, srs, d, m);
+    G1Affine r = msm_host(ctx, srs, scalars, m);
     g1_export(r, out_xy, out_inf);
   });
 }
@@ -1688,9 +1727,7 @@ int qg_kzg_commit(qg_ctx* ctx, const qg_srs* srs, const uint64_t* poly, size_t n
   return qg_guard(ctx, [&] {
     QG_CHECK(n <= srs->n, QG_ERR_INVALID, "Polynomial degree exceeds max degree");
     QG_HIP(hipSetDevice(ctx->device));
-    Fr* d = ctx->scratch_as<Fr>("msm_scalars", n ? n : 1);
-    fr_upload(ctx, d, poly, n);
-    G1Affine r = msm_device(ctx, srs, d, n);
+    G1Affine r = msm_host(ctx, srs, poly, n);
     g1_export(r, out_xy, out_inf);
   });
 }

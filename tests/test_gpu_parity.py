@@ -98,6 +98,27 @@ def test_kzg_commit_trapdoor(dev, n):
     assert kzg.commit(poly[: n // 2]) == o.g1_mul(o.G1_GEN, o.poly_eval(poly[: n // 2], tau))
 
 
+@pytest.mark.parametrize("pieces", [2, 3, 7])
+def test_host_commit_in_pieces(dev, pieces, monkeypatch):
+    """qg_kzg_commit / qg_msm_g1 from host memory with the upload split into
+    pieces overlapped with the pieces' accumulation (QG_MSM_PIECES; 4 by
+    default from 2^22 scalars): same point as the single-piece path, ragged
+    last piece and msm_unchecked truncation included."""
+    from quill_amd import KZG, Srs
+    rnd = random.Random(pieces)
+    tau = rnd.randrange(R)
+    n = 1000
+    kzg = KZG.trusted_setup(n - 1, tau, dev)
+    poly = [rnd.randrange(R) for _ in range(n)]
+    want = o.g1_mul(o.G1_GEN, o.poly_eval(poly, tau))
+    monkeypatch.setenv("QG_MSM_PIECES", str(pieces))
+    assert kzg.commit(poly) == want
+    assert kzg.commit(poly[:333]) == o.g1_mul(o.G1_GEN, o.poly_eval(poly[:333], tau))
+    srs = Srs.upload(dev, [o.g1_mul(o.G1_GEN, pow(tau, i, R)) for i in range(50)])
+    sc = [rnd.randrange(R) for _ in range(80)]  # longer than the bases: truncated
+    assert srs.msm(sc) == o.g1_mul(o.G1_GEN, o.poly_eval(sc[:50], tau))
+
+
 def test_kzg_commit_rejects_oversize(dev):
     from quill_amd import KZG, QuillGpuError
     kzg = KZG.trusted_setup(4, 5, dev)
