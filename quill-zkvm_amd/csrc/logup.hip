@@ -50,6 +50,7 @@ static constexpr int LG_MAXT = 64;                 // distinct tables referenced
 // device image of the two compiled expressions: [0] = beta + h, [1] = m
 struct LgDev {
   uint32_t nm[2];
+  uint32_t unit[2][LG_MAXM];  // coefficient is 2^261 (mul29 by it is the identity)
   uint32_t mlen[2][LG_MAXM];
   uint32_t fstart[2][LG_MAXM];
   L9 coef[2][LG_MAXM];
@@ -62,9 +63,16 @@ QG_DEV R29 lg_eval(const LgDev* __restrict__ g, int w, size_t row) {
   R29 acc = R29::zero();
   const uint32_t nm = g->nm[w];
   for (uint32_t m = 0; m < nm; m++) {
-    R29 t = R29::from_l9(g->coef[w][m]);
     const uint32_t len = g->mlen[w][m], fs = g->fstart[w][m];
-    for (uint32_t j = 0; j < len; j++) t = mul29(t, to29(g->tab[g->fac[fs + j]][row]));
+    uint32_t j = 0;
+    R29 t;
+    if (g->unit[w][m]) {  // c 2^(base + 5f) = 2^261: the first factor as loaded (< p)
+      t = to29(g->tab[g->fac[fs]][row]);
+      j = 1;
+    } else {
+      t = R29::from_l9(g->coef[w][m]);
+    }
+    for (; j < len; j++) t = mul29(t, to29(g->tab[g->fac[fs + j]][row]));
     acc = red2p29(add29(acc, t));
   }
   return acc;
@@ -96,18 +104,23 @@ QG_DEV void lds_put(uint32_t* vs, int k, int tid, const R29& v) {
 
 // Phase 1: per row v = beta + h(row) (x 2^261), stored (< 2p) into the output
 // buffer; the block's product of all its rows -> bprod[block].  A zero
-// denominator makes the product zero (flagged).
-__global__ __launch_bounds__(LG_BLOCK) void k_logup_den(const LgDev* __restrict__ g, size_t n,
-                                                        Fr* __restrict__ out, Fr* __restrict__ bprod,
-                                                        uint32_t* __restrict__ err) {
-  __shared__ uint32_t wtot[LG_BLOCK / 64][9];
+// denominator makes the product zero (flagged).  128 threads x 16 rows per
+// 2048-row block: 4096 waves at 2^22 rows, all resident in one round (256
+// threads x 8 rows was 8192 waves for 6144 slots at 77 VGPRs: 1.33 rounds).
+static constexpr int LG_DEN_BLOCK = 128;
+static constexpr int LG_DEN_K = LG_ROWS / LG_DEN_BLOCK;
+__global__ __launch_bounds__(LG_DEN_BLOCK) void k_logup_den(const LgDev* __restrict__ g, size_t n,
+                                                            Fr* __restrict__ out,
+                                                            Fr* __restrict__ bprod,
+                                                            uint32_t* __restrict__ err) {
+  __shared__ uint32_t wtot[LG_DEN_BLOCK / 64][9];
   const int tid = threadIdx.x, lane = tid & 63, wv = tid >> 6;
   const size_t base = (size_t)blockIdx.x * LG_ROWS + tid;
   const R29 one = R29::from_l9(F29P<FrP>::ONE);
   R29 T = one;
   bool zero = false;
-  for (int k = 0; k < LG_K; k++) {
-    const size_t row = base + (size_t)k * LG_BLOCK;
+  for (int k = 0; k < LG_DEN_K; k++) {
+    const size_t row = base + (size_t)k * LG_DEN_BLOCK;
     if (row >= n) break;
     const R29 v = canon29(lg_eval(g, 0, row));
     zero |= is_zero29(v);
@@ -125,7 +138,7 @@ __global__ __launch_bounds__(LG_BLOCK) void k_logup_den(const LgDev* __restrict_
   __syncthreads();
   if (tid == 0) {
     R29 p = one;
-    for (int w = 0; w < LG_BLOCK / 64; w++) {
+    for (int w = 0; w < LG_DEN_BLOCK / 64; w++) {
       R29 t;
 #pragma unroll
       for (int i = 0; i < 9; i++) t.l[i] = wtot[w][i];
@@ -136,85 +149,52 @@ __global__ __launch_bounds__(LG_BLOCK) void k_logup_den(const LgDev* __restrict_
 }
 
 // Phase 2 (one block): exclusive prefix and suffix products of the nb block
-// products, and their total (the single value the host inverts).
-static constexpr int LG_SCAN = 1024;
+// products, and their total (the single value the host inverts).  256 threads,
+// one contiguous segment each (sequential products), wave shuffle scans of the
+// segment products and the four wave totals: ~20 dependent products per
+// thread at one wave per SIMD (a 1024-thread Hillis-Steele scan through LDS
+// took 49 us at 2^22 rows).
+static constexpr int LG_SCAN = 256;
 __global__ __launch_bounds__(LG_SCAN) void k_logup_scan(const Fr* __restrict__ bprod, uint32_t nb,
                                                         Fr* __restrict__ pre, Fr* __restrict__ suf,
                                                         Fr* __restrict__ total) {
-  __shared__ uint32_t sh[2][9][LG_SCAN];
-  const uint32_t tid = threadIdx.x;
-  const uint32_t per = (nb + LG_SCAN - 1) / LG_SCAN, lo = tid * per;
+  __shared__ uint32_t wtot[LG_SCAN / 64][9];
+  const uint32_t tid = threadIdx.x, lane = tid & 63, wv = tid >> 6;
+  const uint32_t per = (nb + LG_SCAN - 1) / LG_SCAN;
+  const uint32_t lo = tid * per < nb ? tid * per : nb, hi = lo + per < nb ? lo + per : nb;
   const R29 one = R29::from_l9(F29P<FrP>::ONE);
   R29 tp = one;  // product of this thread's segment
-  for (uint32_t i = lo; i < lo + per && i < nb; i++) tp = mul29(tp, to29(bprod[i]));
+  for (uint32_t i = lo; i < hi; i++) tp = mul29(tp, to29(bprod[i]));
+  R29 ip = tp, is = tp;  // inclusive in-wave prefix / suffix
+  for (int d = 1; d < 64; d <<= 1) {
+    const R29 a = shfl_up29(ip, d), b = shfl_down29(is, d);
+    if (lane >= (uint32_t)d) ip = mul29(a, ip);
+    if (lane + d < 64) is = mul29(is, b);
+  }
+  if (lane == 63)
 #pragma unroll
-  for (int i = 0; i < 9; i++) sh[0][i][tid] = tp.l[i];
+    for (int i = 0; i < 9; i++) wtot[wv][i] = ip.l[i];
+  R29 ep = shfl_up29(ip, 1), es = shfl_down29(is, 1);
+  if (lane == 0) ep = one;
+  if (lane == 63) es = one;
   __syncthreads();
-  // Hillis-Steele inclusive scan of the segment products (ping-pong)
-  int cur = 0;
-  for (uint32_t off = 1; off < LG_SCAN; off <<= 1) {
-    R29 a, bb;
+  R29 tot = one;
+  for (uint32_t w = 0; w < LG_SCAN / 64; w++) {
+    R29 t;
 #pragma unroll
-    for (int i = 0; i < 9; i++) a.l[i] = sh[cur][i][tid];
-    if (tid >= off) {
-#pragma unroll
-      for (int i = 0; i < 9; i++) bb.l[i] = sh[cur][i][tid - off];
-      a = mul29(bb, a);
-    }
-#pragma unroll
-    for (int i = 0; i < 9; i++) sh[cur ^ 1][i][tid] = a.l[i];
-    cur ^= 1;
-    __syncthreads();
-  }
-  R29 incl, excl = one, tot;
-#pragma unroll
-  for (int i = 0; i < 9; i++) {
-    incl.l[i] = sh[cur][i][tid];
-    tot.l[i] = sh[cur][i][LG_SCAN - 1];
-  }
-  if (tid > 0)
-#pragma unroll
-    for (int i = 0; i < 9; i++) excl.l[i] = sh[cur][i][tid - 1];
-  (void)incl;
-  // exclusive prefix within the segment
-  R29 run = excl;
-  for (uint32_t i = lo; i < lo + per && i < nb; i++) {
-    pre[i] = from29(canon29(run));
-    run = mul29(run, to29(bprod[i]));
+    for (int i = 0; i < 9; i++) t.l[i] = wtot[w][i];
+    if (w < wv) ep = mul29(ep, t);
+    if (w > wv) es = mul29(es, t);
+    if (tid == 0) tot = mul29(tot, t);
   }
   if (tid == 0) *total = from29(canon29(tot));
-  __syncthreads();
-  // suffix: the same over the reversed order
-#pragma unroll
-  for (int i = 0; i < 9; i++) sh[0][i][LG_SCAN - 1 - tid] = tp.l[i];
-  __syncthreads();
-  cur = 0;
-  for (uint32_t off = 1; off < LG_SCAN; off <<= 1) {
-    R29 a, bb;
-#pragma unroll
-    for (int i = 0; i < 9; i++) a.l[i] = sh[cur][i][tid];
-    if (tid >= off) {
-#pragma unroll
-      for (int i = 0; i < 9; i++) bb.l[i] = sh[cur][i][tid - off];
-      a = mul29(bb, a);
-    }
-#pragma unroll
-    for (int i = 0; i < 9; i++) sh[cur ^ 1][i][tid] = a.l[i];
-    cur ^= 1;
-    __syncthreads();
-  }
-  // reversed position of this thread's segment: LG_SCAN - 1 - tid; exclusive = entry before it
-  const uint32_t rp = LG_SCAN - 1 - tid;
-  R29 sx = one;
-  if (rp > 0)
-#pragma unroll
-    for (int i = 0; i < 9; i++) sx.l[i] = sh[cur][i][rp - 1];
-  run = sx;
-  for (uint32_t k = per; k-- > 0;) {
-    const uint32_t i = lo + k;
-    if (i >= nb) continue;
-    suf[i] = from29(canon29(run));
-    run = mul29(run, to29(bprod[i]));
+  R29 rp = ep, rs = es;
+  for (uint32_t k = 0; k < hi - lo; k++) {  // prefix up, suffix down, interleaved
+    const uint32_t i = lo + k, j = hi - 1 - k;
+    pre[i] = from29(canon29(rp));
+    suf[j] = from29(canon29(rs));
+    rp = mul29(rp, to29(bprod[i]));
+    rs = mul29(rs, to29(bprod[j]));
   }
 }
 
@@ -413,7 +393,9 @@ static void lg_compile(LgDev& d, int w, const SopProgram& sp, const Fr& add_cons
       }
       d.fac[nfac++] = slot;
     }
-    d.coef[w][m] = lg_l9(lg_plain_mul(from_mont(coeff[m]), pow2_mod_plain<FrP>(base + 5 * mlen[m])));
+    const Fr cf = lg_plain_mul(from_mont(coeff[m]), pow2_mod_plain<FrP>(base + 5 * mlen[m]));
+    d.coef[w][m] = lg_l9(cf);
+    d.unit[w][m] = mlen[m] >= 1 && cf == pow2_mod_plain<FrP>(261) ? 1u : 0u;
   }
 }
 
@@ -486,7 +468,7 @@ static Fr logup_run(qg_ctx* ctx, uint32_t nvars, uint32_t ntables, const std::ve
   {
     // kernel time only: the timed region closes before the D2H copies and the sync
     QgTimed tm(ctx, "logup_column");
-    hipLaunchKernelGGL(k_logup_den, dim3(nb), dim3(LG_BLOCK), 0, ctx->stream, d_img, n, d_out,
+    hipLaunchKernelGGL(k_logup_den, dim3(nb), dim3(LG_DEN_BLOCK), 0, ctx->stream, d_img, n, d_out,
                        d_bp, d_err);
     QG_LAUNCH_CHECK();
     hipLaunchKernelGGL(k_logup_scan, dim3(1), dim3(LG_SCAN), 0, ctx->stream, d_bp, nb, d_pre,
