@@ -614,22 +614,27 @@ def bench_logup(q, dev, args, barrier_sync, max_over_ranks, rank=0, world=1, tra
     dt = max_over_ranks(time.perf_counter() - t0)
     kms, kn = dev.kernel_time("logup_column")
     dev.enable_timing(False)
-    # device time per column (both timed regions: denominators + block scan, then
-    # the inverses; the host's single finv in between is outside them)
+    # device time per column: denominators + block scan, then the inverses (the
+    # host's single finv in between is outside the timed regions); with
+    # QG_LOGUP_FUSED=1 the one-pass kernel + the block-sum kernel
     kern_ms = max_over_ranks(kms / max(args.steps, 1))
     nbytes = LOGUP_BYTES_PER_ROW * n
+    lg_kernels = ("k_logup_fused", "k_logup_den", "k_logup")
+    lg_traffic = [_kernel_traffic(traffic, k) for k in lg_kernels]
+    fused = os.environ.get("QG_LOGUP_FUSED", "0") != "0"
     res = {"metric": f"Logup column rows/s at 2^{k} rows per GPU (m / (beta + t0 + a t1))",
            "value": world * n * args.steps / dt, "unit": "rows/s", "higher_is_better": True,
            "ms": dt / args.steps * 1e3, "kernel_ms": kern_ms,
            "roofline": {"bound": "hbm", "kernel": "logup_column", "achieved":
                         nbytes / (kern_ms * 1e-3) / 1e9, "peak": HBM_PEAK_GBPS, "unit": "GB/s",
                         "frac": nbytes / (kern_ms * 1e-3) / 1e9 / HBM_PEAK_GBPS,
-                        "traffic": (None if _kernel_traffic(traffic, "k_logup") is None else
-                                    sum(_kernel_traffic(traffic, k) or 0
-                                        for k in ("k_logup_den", "k_logup"))),
+                        "traffic": (None if all(t is None for t in lg_traffic) else
+                                    sum(t or 0 for t in lg_traffic)),
                         "algorithmic_bytes": nbytes,
-                        "note": "3 table reads + 1 column write of 32 B per row; the kernels "
-                                "also write and re-read the denominators (+64 B/row)"},
+                        "note": ("3 table reads + 1 column write of 32 B per row, one pass "
+                                 "(a binary-GCD inversion per 2048-row block)" if fused else
+                                 "3 table reads + 1 column write of 32 B per row; the kernels "
+                                 "also write and re-read the denominators (+64 B/row)")},
            "column_sum_low64": hex(s & ((1 << 64) - 1))}
     if rank == 0 and not args.no_cpu_baseline:
         res["cpu_baseline"] = cpu_baseline_logup(args, tabs, out)

@@ -378,6 +378,12 @@ int qg_microbench_fq_mul(qg_ctx* ctx, double* mul_per_s);
 int qg_microbench_fetch(qg_ctx* ctx, size_t rows, size_t gathers, double* gather_ms,
                         double* stream_ms);
 int qg_ctx_kernel_time(const qg_ctx* ctx, const char* name, double* total_ms, uint32_t* launches);
+/* Self-test of the binary-GCD field inversion the Logup column uses per block
+ * (csrc/bingcd.h): out[i] = in[i]^-1 (plain canonical integers, 4 x u64 LE;
+ * 0 -> 0) in Fr (field = 0) or Fq (field = 1), on the host (ctx may be NULL)
+ * or, with on_device, in a device kernel on ctx. */
+int qg_selftest_inverse(qg_ctx* ctx, int field, int on_device, const uint64_t* in, uint64_t* out,
+                        size_t n);
 
 #ifdef __cplusplus
 }

@@ -30,6 +30,7 @@
 
 #include <vector>
 
+#include "bingcd.h"
 #include "common.h"
 #include "expr.h"
 #include "field29.h"
@@ -56,6 +57,8 @@ struct LgDev {
   L9 coef[2][LG_MAXM];
   uint32_t fac[LG_MAXF];
   const Fr* tab[LG_MAXT];
+  L9 kinv;    // k_logup_fused: 2^778 mod r, mul29(P^-1, kinv) = block inverse (see there)
+  L9 one256;  // 2^256 mod r: a padding row's denominator in the x 2^256 domain
 };
 
 // one expression at one row; < 2p, normalized
@@ -102,7 +105,7 @@ QG_DEV void lds_put(uint32_t* vs, int k, int tid, const R29& v) {
   for (int i = 0; i < 9; i++) vs[(k * 9 + i) * LG_BLOCK + tid] = v.l[i];
 }
 
-// Phase 1: per row v = beta + h(row) (x 2^261), stored (< 2p) into the output
+// Phase 1: per row v = beta + h(row) (x 2^256), stored (< p) into the output
 // buffer; the block's product of all its rows -> bprod[block].  A zero
 // denominator makes the product zero (flagged).  128 threads x 16 rows per
 // 2048-row block: 4096 waves at 2^22 rows, all resident in one round (256
@@ -304,6 +307,143 @@ __global__ __launch_bounds__(LG_BLOCK) void k_logup(const LgDev* __restrict__ g,
   }
 }
 
+// One pass (default): k_logup with the denominators evaluated from the tables
+// instead of re-read, and 1 / (block product) from ONE binary-GCD inversion
+// per 2048-row block (csrc/bingcd.h, wave 0 on the scalar unit) instead of a
+// column-wide product inverted on the host: 96 B/row read + 32 B/row written,
+// no scan kernel, no host round trip.
+// Domains: the denominators stay in arkworks' x 2^256 form (the raw table
+// entries add in without a conversion multiply; beta + t0 + a t1 costs one
+// multiply).  Every mul29 takes 2^261 off, so a product of m such values
+// carries 2^(261 - 5m); each 1 / v_k below is a product tree over binv and the
+// block's other N - 1 rows, whatever its position, so with the block product P
+// = (prod v) 2^(261 - 5N) inverted as a plain integer and binv = mul29(P^-1,
+// 2^778) every 1 / v_k comes out as (1 / v_k) 2^261 - the multiplier's domain
+// then gives the output in arkworks form.  (Padding rows are 2^256, i.e. 1.)
+__global__ __launch_bounds__(LG_BLOCK) void k_logup_fused(const LgDev* __restrict__ g, size_t n,
+                                                          Fr* __restrict__ out, Fr* __restrict__ bsum,
+                                                          uint32_t* __restrict__ err) {
+  __shared__ uint32_t vs[LG_K * 9 * LG_BLOCK];  // row denominators, [k][limb][thread]
+  __shared__ uint32_t wtot[LG_BLOCK / 64][9];
+  __shared__ uint32_t wsum[LG_BLOCK / 64][9];
+  __shared__ uint32_t binv_sh[9];
+  const int tid = threadIdx.x, lane = tid & 63, wv = tid >> 6;
+  const size_t base = (size_t)blockIdx.x * LG_ROWS + tid;
+  const R29 one = R29::from_l9(F29P<FrP>::ONE);
+
+  // 1. denominators (x 2^261) into LDS, the running prefix of this thread's rows
+  bool zero = false;
+  for (int k = 0; k < LG_K; k++) {
+    const size_t row = base + (size_t)k * LG_BLOCK;
+    R29 v = R29::from_l9(g->one256);
+    if (row < n) {
+      v = canon29(lg_eval(g, 0, row));
+      zero |= is_zero29(v);
+    }
+    lds_put(vs, k, tid, v);
+  }
+  if (zero) atomicOr(err, 1u);
+  static_assert(LG_K == 8, "prefix chain is written out for 8 rows");
+  R29 pre_r[LG_K];
+  pre_r[0] = lds_row(vs, 0, tid);
+  pre_r[1] = mul29(pre_r[0], lds_row(vs, 1, tid));
+  pre_r[2] = mul29(pre_r[1], lds_row(vs, 2, tid));
+  pre_r[3] = mul29(pre_r[2], lds_row(vs, 3, tid));
+  pre_r[4] = mul29(pre_r[3], lds_row(vs, 4, tid));
+  pre_r[5] = mul29(pre_r[4], lds_row(vs, 5, tid));
+  pre_r[6] = mul29(pre_r[5], lds_row(vs, 6, tid));
+  pre_r[7] = mul29(pre_r[6], lds_row(vs, 7, tid));
+  const R29 T = pre_r[LG_K - 1];
+
+  // 2. exclusive prefix / suffix products of T across the block
+  R29 ip = T, is = T;
+  for (int d = 1; d < 64; d <<= 1) {
+    const R29 a = shfl_up29(ip, d), b = shfl_down29(is, d);
+    if (lane >= d) ip = mul29(a, ip);
+    if (lane + d < 64) is = mul29(is, b);
+  }
+  if (lane == 63)
+#pragma unroll
+    for (int i = 0; i < 9; i++) wtot[wv][i] = ip.l[i];
+  R29 ep = shfl_up29(ip, 1), es = shfl_down29(is, 1);
+  if (lane == 0) ep = one;
+  if (lane == 63) es = one;
+  __syncthreads();
+  if (wv == 0) {  // block inverse: one binary-GCD inversion, wave-uniform (scalar unit)
+    R29 P = one;
+    for (int w = 0; w < LG_BLOCK / 64; w++) {
+      R29 t;
+#pragma unroll
+      for (int i = 0; i < 9; i++) t.l[i] = wtot[w][i];
+      P = mul29(P, t);
+    }
+    Fr pc = from29(canon29(P));
+#pragma unroll
+    for (int i = 0; i < 8; i++) pc.v[i] = __builtin_amdgcn_readfirstlane(pc.v[i]);
+    const Fr ipl = inv_bingcd<FrP>(pc);  // 0 if some denominator was 0
+    const R29 b = mul29(to29(ipl), R29::from_l9(g->kinv));
+    if (lane == 0)
+#pragma unroll
+      for (int i = 0; i < 9; i++) binv_sh[i] = b.l[i];
+  }
+  for (int w = 0; w < LG_BLOCK / 64; w++) {  // wave products straight from LDS (uniform loop)
+    R29 t;
+#pragma unroll
+    for (int i = 0; i < 9; i++) t.l[i] = wtot[w][i];
+    if (w < wv) ep = mul29(ep, t);
+    if (w > wv) es = mul29(es, t);
+  }
+  __syncthreads();
+  R29 binv;
+#pragma unroll
+  for (int i = 0; i < 9; i++) binv.l[i] = binv_sh[i];
+  R29 inv_run = mul29(mul29(binv, ep), es);  // 1 / T
+
+  // 3. back-substitution: 1 / v_k overwrites v_k in LDS (own slots only)
+#define LG_BACK(k)                                        \
+  {                                                       \
+    const R29 x = mul29(inv_run, pre_r[k - 1]);           \
+    inv_run = mul29(inv_run, lds_row(vs, k, tid));        \
+    lds_put(vs, k, tid, x);                               \
+  }
+  LG_BACK(7) LG_BACK(6) LG_BACK(5) LG_BACK(4) LG_BACK(3) LG_BACK(2) LG_BACK(1)
+#undef LG_BACK
+  lds_put(vs, 0, tid, inv_run);
+
+  // 4. multiplier, store, block sum
+  R29 acc = R29::zero();
+  for (int k = 0; k < LG_K; k++) {
+    const size_t row = base + (size_t)k * LG_BLOCK;
+    if (row >= n) break;
+    const R29 x = lds_row(vs, k, tid);
+    const R29 m = lg_eval(g, 1, row);  // M x 2^256
+    const R29 y = canon29(mul29(x, m));
+    out[row] = from29(y);
+    acc = red2p29(add29(acc, y));
+  }
+  for (int d = 32; d >= 1; d >>= 1) {
+    R29 o;
+#pragma unroll
+    for (int i = 0; i < 9; i++) o.l[i] = __shfl_xor(acc.l[i], d, 64);
+    acc = red2p29(add29(acc, o));
+  }
+  if (lane == 0)
+#pragma unroll
+    for (int i = 0; i < 9; i++) wsum[wv][i] = acc.l[i];
+  __syncthreads();
+  if (tid == 0) {
+    R29 s = R29::zero();
+#pragma unroll
+    for (int w = 0; w < LG_BLOCK / 64; w++) {
+      R29 t;
+#pragma unroll
+      for (int i = 0; i < 9; i++) t.l[i] = wsum[w][i];
+      s = red2p29(add29(s, t));
+    }
+    bsum[blockIdx.x] = from29(canon29(s));
+  }
+}
+
 // sum of the per-block sums (one block)
 __global__ __launch_bounds__(256) void k_logup_sum(const Fr* __restrict__ bsum, uint32_t nb,
                                                    Fr* __restrict__ res) {
@@ -331,6 +471,44 @@ __global__ __launch_bounds__(256) void k_logup_sum(const Fr* __restrict__ bsum, 
     }
     *res = from29(canon29(s));
   }
+}
+
+// qg_selftest_inverse's device path: one inversion per thread
+template <class C>
+__global__ void k_inv_selftest(const Fp<C>* __restrict__ in, Fp<C>* __restrict__ out, size_t n) {
+  const size_t i = (size_t)blockIdx.x * blockDim.x + threadIdx.x;
+  if (i < n) out[i] = inv_bingcd<C>(in[i]);
+}
+
+template <class C>
+static void inv_selftest(qg_ctx* ctx, bool dev, const uint64_t* in, uint64_t* out, size_t n) {
+  std::vector<Fp<C>> h(n);
+  for (size_t i = 0; i < n; i++)
+    for (int l = 0; l < 4; l++) {
+      h[i].v[2 * l] = (uint32_t)in[4 * i + l];
+      h[i].v[2 * l + 1] = (uint32_t)(in[4 * i + l] >> 32);
+    }
+  for (size_t i = 0; i < n; i++) {
+    Fp<C> t = h[i];
+    reduce_full<C>(t.v);
+    QG_CHECK(t == h[i], QG_ERR_INVALID, "inverse self-test input not canonical");
+  }
+  if (dev) {
+    QG_CHECK(ctx, QG_ERR_INVALID, "device self-test needs a context");
+    QG_HIP(hipSetDevice(ctx->device));
+    Fp<C>* d = ctx->scratch_as<Fp<C>>("inv_selftest", 2 * n + 2);
+    QG_HIP(hipMemcpyAsync(d, h.data(), n * sizeof(Fp<C>), hipMemcpyHostToDevice, ctx->stream));
+    hipLaunchKernelGGL(k_inv_selftest<C>, dim3(div_up(n ? n : 1, 64)), dim3(64), 0, ctx->stream, d, d + n,
+                       n);
+    QG_LAUNCH_CHECK();
+    QG_HIP(hipMemcpyAsync(h.data(), d + n, n * sizeof(Fp<C>), hipMemcpyDeviceToHost, ctx->stream));
+    ctx->sync();
+  } else {
+    for (size_t i = 0; i < n; i++) h[i] = inv_bingcd<C>(h[i]);
+  }
+  for (size_t i = 0; i < n; i++)
+    for (int l = 0; l < 4; l++)
+      out[4 * i + l] = (uint64_t)h[i].v[2 * l] | ((uint64_t)h[i].v[2 * l + 1] << 32);
 }
 
 // first row whose expression value (slot 0, no beta) is nonzero; atomicMin
@@ -408,6 +586,53 @@ static size_t lg_local_size(const qg_ctx* ctx, uint32_t nvars) {
   return (size_t)1 << (nvars - lw);
 }
 
+// the 3-kernel path (default) or the one-pass kernel (QG_LOGUP_FUSED=1): one
+// pass moves 128 instead of 192 B/row but idles the block during its
+// inversion; the column is VALU-bound, so the 3 kernels are faster
+// (profiles/r03_logup_ab.txt)
+static bool logup_fused() {
+  const char* ov = getenv("QG_LOGUP_FUSED");
+  return ov && atoi(ov) != 0;
+}
+
+// the column sum (d_res) and the zero-denominator flag (d_err) of this rank,
+// summed / or-ed over all ranks; QG_ERR_ASSERT when any rank had a zero
+static Fr logup_total(qg_ctx* ctx, const Fr* d_res, const uint32_t* d_err) {
+  struct {
+    Fr res;
+    uint32_t err;
+  } h;
+  QG_HIP(hipMemcpyAsync(&h.err, d_err, 4, hipMemcpyDeviceToHost, ctx->stream));
+  QG_HIP(hipMemcpyAsync(&h.res, d_res, sizeof(Fr), hipMemcpyDeviceToHost, ctx->stream));
+  ctx->sync();
+  if (h.err) h.res = Fr::zero();
+  // every rank learns whether any rank hit a zero denominator, and the global sum
+  struct {
+    Fr s;
+    uint32_t err, pad[7];
+  } mine{h.res, h.err, {}};
+  Fr total = Fr::zero();
+  uint32_t any_err = 0;
+  if (ctx->world > 1) {
+    uint8_t* d_g = ctx->scratch_as<uint8_t>("lg_gather", sizeof(mine) * (ctx->world + 1));
+    QG_HIP(hipMemcpyAsync(d_g, &mine, sizeof(mine), hipMemcpyHostToDevice, ctx->stream));
+    comm_allgather_bytes(ctx, d_g, d_g + sizeof(mine), sizeof(mine));
+    std::vector<decltype(mine)> all(ctx->world);
+    QG_HIP(hipMemcpyAsync(all.data(), d_g + sizeof(mine), sizeof(mine) * ctx->world,
+                          hipMemcpyDeviceToHost, ctx->stream));
+    ctx->sync();
+    for (auto& a : all) {
+      total = total + a.s;
+      any_err |= a.err;
+    }
+  } else {
+    total = h.res;
+    any_err = h.err;
+  }
+  QG_CHECK(!any_err, QG_ERR_ASSERT, "logup denominator beta + h(x) is zero (reference: inverse().unwrap())");
+  return total;
+}
+
 // out[x] = m(x) / (beta + h(x)) over this rank's rows; returns sum_x out[x]
 // over all ranks (Fr, i.e. arkworks Montgomery words)
 static Fr logup_run(qg_ctx* ctx, uint32_t nvars, uint32_t ntables, const std::vector<const Fr*>& tabs,
@@ -422,7 +647,9 @@ static Fr logup_run(qg_ctx* ctx, uint32_t nvars, uint32_t ntables, const std::ve
   uint32_t nfac = 0;
   try {
     const SopProgram sh = compile_program(hp, hl, hc, hn, ntables);
-    lg_compile(img, 0, sh, fr_import(beta), true, 261, used, nfac);
+    // denominators in arkworks' x 2^256 form (raw t0 adds without a multiply;
+    // the mul29 drift is one fixed power of two per output, see k_logup_fused)
+    lg_compile(img, 0, sh, fr_import(beta), true, 256, used, nfac);
     if (mp && ml) {
       const SopProgram sm = compile_program(mp, ml, mc, mn, ntables);
       lg_compile(img, 1, sm, Fr::zero(), false, 256, used, nfac);
@@ -459,8 +686,21 @@ static Fr logup_run(qg_ctx* ctx, uint32_t nvars, uint32_t ntables, const std::ve
   Fr* d_suf = d_pre + nb;
   Fr* d_tot = d_suf + nb;
   Fr* d_tinv = d_tot + 1;
+  img.kinv = lg_l9(pow2_mod_plain<FrP>(778));
+  img.one256 = lg_l9(pow2_mod_plain<FrP>(256));
   QG_HIP(hipMemcpyAsync(d_img, &img, sizeof(img), hipMemcpyHostToDevice, ctx->stream));
   QG_HIP(hipMemsetAsync(d_err, 0, 4, ctx->stream));
+  if (logup_fused()) {
+    {
+      QgTimed tm(ctx, "logup_column");
+      hipLaunchKernelGGL(k_logup_fused, dim3(nb), dim3(LG_BLOCK), 0, ctx->stream, d_img, n, d_out,
+                         d_bsum, d_err);
+      QG_LAUNCH_CHECK();
+      hipLaunchKernelGGL(k_logup_sum, dim3(1), dim3(256), 0, ctx->stream, d_bsum, nb, d_res);
+      QG_LAUNCH_CHECK();
+    }
+    return logup_total(ctx, d_res, d_err);
+  }
   struct {
     Fr tot;
     uint32_t err;
@@ -479,12 +719,14 @@ static Fr logup_run(qg_ctx* ctx, uint32_t nvars, uint32_t ntables, const std::ve
   QG_HIP(hipMemcpyAsync(&ht.err, d_err, 4, hipMemcpyDeviceToHost, ctx->stream));
   ctx->sync();
   // one inversion for the whole column, of the product of every denominator:
-  // tot = P 2^261 (plain)  ->  (1 / P) 2^261 = 2^522 / tot
+  // with N rows in the x 2^256 domain, tot = P 2^(261 - 5N) (plain); each
+  // 1 / v_k of k_logup is a product tree over tinv and the other N - 1 rows,
+  // so tinv = tot^-1 2^517 gives every 1 / v_k as (1 / v_k) 2^261
   Fr tinv = Fr::zero();
   if (!ht.err) {
     const Fr tot_plain = ht.tot;  // nonzero: no denominator was zero
     const Fr inv_plain = from_mont(finv(to_mont(tot_plain)));
-    tinv = lg_plain_mul(inv_plain, pow2_mod_plain<FrP>(522));
+    tinv = lg_plain_mul(inv_plain, pow2_mod_plain<FrP>(517));
   }
   if (!ht.err) {
     QG_HIP(hipMemcpyAsync(d_tinv, &tinv, sizeof(Fr), hipMemcpyHostToDevice, ctx->stream));
@@ -495,40 +737,7 @@ static Fr logup_run(qg_ctx* ctx, uint32_t nvars, uint32_t ntables, const std::ve
     hipLaunchKernelGGL(k_logup_sum, dim3(1), dim3(256), 0, ctx->stream, d_bsum, nb, d_res);
     QG_LAUNCH_CHECK();
   }
-  struct {
-    Fr res;
-    uint32_t err;
-  } h;
-  h.res = Fr::zero();
-  h.err = ht.err;
-  if (!ht.err)
-    QG_HIP(hipMemcpyAsync(&h.res, d_res, sizeof(Fr), hipMemcpyDeviceToHost, ctx->stream));
-  ctx->sync();
-  // every rank learns whether any rank hit a zero denominator, and the global sum
-  struct {
-    Fr s;
-    uint32_t err, pad[7];
-  } mine{h.res, h.err, {}};
-  Fr total = Fr::zero();
-  uint32_t any_err = 0;
-  if (ctx->world > 1) {
-    uint8_t* d_g = ctx->scratch_as<uint8_t>("lg_gather", sizeof(mine) * (ctx->world + 1));
-    QG_HIP(hipMemcpyAsync(d_g, &mine, sizeof(mine), hipMemcpyHostToDevice, ctx->stream));
-    comm_allgather_bytes(ctx, d_g, d_g + sizeof(mine), sizeof(mine));
-    std::vector<decltype(mine)> all(ctx->world);
-    QG_HIP(hipMemcpyAsync(all.data(), d_g + sizeof(mine), sizeof(mine) * ctx->world,
-                          hipMemcpyDeviceToHost, ctx->stream));
-    ctx->sync();
-    for (auto& a : all) {
-      total = total + a.s;
-      any_err |= a.err;
-    }
-  } else {
-    total = h.res;
-    any_err = h.err;
-  }
-  QG_CHECK(!any_err, QG_ERR_ASSERT, "logup denominator beta + h(x) is zero (reference: inverse().unwrap())");
-  return total;
+  return logup_total(ctx, d_res, d_err);
 }
 
 }  // namespace qg
@@ -579,6 +788,16 @@ int qg_logup_column_dev(qg_ctx* ctx, uint32_t nvars, uint32_t ntables, const qg_
     const Fr s = logup_run(ctx, nvars, ntables, tabs, h_prog, h_len, h_consts, h_nconsts, m_prog,
                            m_len, m_consts, m_nconsts, beta, out->d);
     if (out_sum) fr_export(s, out_sum);
+  });
+}
+
+int qg_selftest_inverse(qg_ctx* ctx, int field, int on_device, const uint64_t* in, uint64_t* out,
+                        size_t n) {
+  if ((!in || !out) && n) return QG_ERR_INVALID;
+  if (field != 0 && field != 1) return QG_ERR_INVALID;
+  return qg_guard(ctx, [&] {
+    if (field == 0) inv_selftest<FrP>(ctx, on_device != 0, in, out, n);
+    else inv_selftest<FqP>(ctx, on_device != 0, in, out, n);
   });
 }
 
