@@ -7,21 +7,26 @@
 //
 //  * Both expressions are compiled on the host into sums of monomials
 //    (expr.h).  The coefficient of a monomial with f factors is pre-scaled by
-//    2^(261 + 5f) (denominator) or 2^(256 + 5f) (multiplier), so multiplying
-//    raw arkworks table entries (x 2^256) with mul29 (x 2^-261) lands the
-//    denominator in the R = 2^261 domain and the multiplier in arkworks form
-//    with no conversion multiplies.
+//    2^(256 + 5f), so multiplying raw arkworks table entries (x 2^256) with
+//    mul29 (x 2^-261) keeps both the denominator and the multiplier in
+//    arkworks form; a coefficient that comes out as 2^261 (a bare table
+//    entry) skips its multiply.
 //  * Batch inversion (Montgomery's trick) at four levels, ONE field inversion
 //    per column: phase 1 (k_logup_den) stores every row's beta + h(x) in the
 //    output buffer and multiplies each block's rows together; phase 2
 //    (k_logup_scan, one block) forms the exclusive prefix / suffix products of
-//    the block products and their total, which the host inverts (one finv);
-//    phase 3 (k_logup) gives each block 1/(its product) = 1/total x prefix x
-//    suffix, then within the block as before: each thread's running prefix of
+//    the block products and their total, which the host inverts (binary GCD,
+//    bingcd.h; on the device's scalar unit it took 50 us, more than the round
+//    trip); phase 3 (k_logup) gives each block 1/(its product) = 1/total x
+//    prefix x suffix, then within the block: each thread's running prefix of
 //    its LG_K rows in registers (row values in LDS), wave shuffle scans of the
-//    thread products, back-substitution.  (A per-block Fermat inversion, ~330
-//    dependent multiplies on one wave per 2048 rows, bounded the one-pass
-//    version at 0.42 TB/s.)
+//    thread products, back-substitution.  mul29 drifts the power of two by -5
+//    per product; every output is a product tree over the inverse and all other
+//    rows, so one constant fixes all of them.
+//  * k_logup_fused (QG_LOGUP_FUSED=1) is the one-pass alternative: one
+//    binary-GCD inversion per 2048-row block, 128 instead of 192 B/row of HBM,
+//    but slower - the column is VALU-bound and the block idles while wave 0
+//    inverts (profiles/r03_logup_ab.txt).
 //  * A zero denominator makes the block product zero: the kernel flags it and
 //    the call returns QG_ERR_ASSERT (the reference panics in unwrap()).
 //  * Per-block sums of the outputs feed SetInclusionProof's claimed sums
@@ -725,7 +730,7 @@ static Fr logup_run(qg_ctx* ctx, uint32_t nvars, uint32_t ntables, const std::ve
   Fr tinv = Fr::zero();
   if (!ht.err) {
     const Fr tot_plain = ht.tot;  // nonzero: no denominator was zero
-    const Fr inv_plain = from_mont(finv(to_mont(tot_plain)));
+    const Fr inv_plain = inv_bingcd<FrP>(tot_plain);
     tinv = lg_plain_mul(inv_plain, pow2_mod_plain<FrP>(517));
   }
   if (!ht.err) {
