@@ -136,6 +136,8 @@ PROTOTYPES = {
                                             C.POINTER(C.c_int64)]),
     "qg_ctx_enable_timing": (C.c_int, [P, C.c_int]),
     "qg_microbench_fq_mul": (C.c_int, [P, C.POINTER(C.c_double)]),
+    "qg_selftest_inverse": (C.c_int, [P, C.c_int, C.c_int, C.POINTER(C.c_uint64),
+                                      C.POINTER(C.c_uint64), C.c_size_t]),
     "qg_microbench_fetch": (C.c_int, [P, C.c_size_t, C.c_size_t, C.POINTER(C.c_double),
                                       C.POINTER(C.c_double)]),
     "qg_ctx_kernel_time": (C.c_int, [P, C.c_char_p, C.POINTER(C.c_double), U32P]),
