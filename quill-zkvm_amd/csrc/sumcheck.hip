@@ -60,7 +60,21 @@ __device__ unsigned long long g_sc_trace[2048 + 4 * 1536];
       if ((k) == 0) g_sc_trace[2048 + (j) * 1536 + 3 * blockIdx.x + 2] = __smid();    \
     }                                                                                 \
   } while (0)
+// per-wave (sweep end, HW_ID) of big rounds 0..3, blocks < 512, waves < 8
+__device__ unsigned long long g_sc_wtrace[4 * 512 * 8 * 2];
+#define SC_TW(j)                                                                          \
+  do {                                                                                    \
+    if ((threadIdx.x & 63) == 0 && (j) < 4 && blockIdx.x < 512 && (threadIdx.x >> 6) < 8) { \
+      const size_t o = (((size_t)(j) * 512 + blockIdx.x) * 8 + (threadIdx.x >> 6)) * 2;    \
+      g_sc_wtrace[o] = wall_clock64();                                                    \
+      g_sc_wtrace[o + 1] = __builtin_amdgcn_s_getreg(63492) /* HW_REG_HW_ID */          \
+                           | ((unsigned long long)__builtin_amdgcn_s_getreg(6164) << 32); /* XCC_ID */ \
+    }                                                                                     \
+  } while (0)
 #else
+#define SC_TW(j) \
+  do {           \
+  } while (0)
 #define SC_TR(idx) \
   do {             \
   } while (0)
@@ -313,7 +327,7 @@ QG_DEV void round_sweep(RoundLds<K, NP, BLOCK>& L, const SopLds<NP>& sp, const S
           const Fr* src = L.src[s] + 4 * p + 2 * (e & 1);
           const R29 x0 = to29(src[0]), x1 = to29(src[1]);
           // x0 + r (x1 - x0): x1 - x0 + 4p (lazy) times r (< 2p) -> < 2p; + x0 -> < 4p
-          v = red6p(add29(x0, mul29(sub29(x1, x0), r)));
+          v = red2p29<FrP>(add29(x0, mul29(sub29(x1, x0), r)));
           L.dst[s][2 * p + (e & 1)] = from29(v);
         } else {
           v = to29(L.src[s][2 * p + (e & 1)]);
@@ -685,6 +699,21 @@ __global__ void __launch_bounds__(SC_BLOCK)
 //    sums them and runs the transcript step.
 // ---------------------------------------------------------------------------
 // lo + t (hi - lo + 4p) for point t (d = norm29(hi - lo + 4p) < 6p)
+// the same value left lazy (limbs < 2^31 + 32, value < 20p) for NP <= 4: a
+// multiplier operand next to a normalized one (< 2p) keeps every column below
+// 2^64 and the product below 1.3p, so only the first factor needs the carry pass
+template <int NP>
+QG_DEV R29 at_point_lazy(const R29& lo, const R29& d, int t, const SopLds<NP>& sp) {
+  if constexpr (NP <= 4) {
+    R29 v = lo;
+    if (t & 1) v = add29(v, d);
+    if (t & 2) v = add29(v, add29(d, d));
+    return v;
+  } else {
+    return norm29(add29(lo, mul29t(d, sp.t29[t])));
+  }
+}
+
 template <int NP>
 QG_DEV R29 at_point(const R29& lo, const R29& d, int t, const SopLds<NP>& sp) {
   if constexpr (NP <= 4) {
@@ -697,12 +726,14 @@ QG_DEV R29 at_point(const R29& lo, const R29& d, int t, const SopLds<NP>& sp) {
   }
 }
 
-// fold x0..x3 -> (lo, hi) < 2p and store them (round j >= 1), or take x0, x1
+// fold x0..x3 -> (lo, hi) < 2p and store them (round j >= 1), or take x0, x1.
+// Bounds: x < 2p, x1 - x0 + 4p < 6p, r < 2p: the product is < 12p^2/2^261 + p
+// < 1.1p, so x0 + it < 3.1p and one conditional subtraction of 2p suffices.
 QG_DEV void fold_pair(const Fr (&w)[4], bool fold, const R29& r, Fr* dst, R29& lo, R29& hi) {
   if (fold) {
     const R29 x0 = to29(w[0]), x1 = to29(w[1]), x2 = to29(w[2]), x3 = to29(w[3]);
-    lo = red6p(add29(x0, mul29t(sub29(x1, x0), r)));
-    hi = red6p(add29(x2, mul29t(sub29(x3, x2), r)));
+    lo = red2p29<FrP>(add29(x0, mul29t(sub29(x1, x0), r)));
+    hi = red2p29<FrP>(add29(x2, mul29t(sub29(x3, x2), r)));
     dst[0] = from29(lo);
     dst[1] = from29(hi);
   } else {
@@ -753,9 +784,10 @@ QG_DEV void sweep_pairs(const AllBufs& tb, uint32_t j, bool fold, const R29& r, 
                         bool skip0, R29 (&acc)[NP]) {
   const uint32_t nslots = h.nslots, np = h.np;
   uint32_t cnt = 0;
-  for (size_t p = p0; p < npairs; p += stride) {
-    R29 prod[NP];
-    if constexpr (PURE) {
+  if constexpr (PURE) {
+    // one pair: fold the slots, multiply the points, accumulate lazily
+    auto body = [&](size_t p) {
+      R29 prod[NP];
       Fr w[4], wn[4];
       if constexpr (PF) load_pair(tb.src(j, 0) + (fold ? 4 : 2) * p, fold, w);
       for (uint32_t s = 0; s < nslots; s++) {
@@ -770,8 +802,10 @@ QG_DEV void sweep_pairs(const AllBufs& tb, uint32_t j, bool fold, const R29& r, 
 #pragma unroll
         for (int t = 0; t < NP; t++) {
           if (t == 0 && skip0) continue;  // h(0) = claim - h(1), by the finisher
-          const R29 v = at_point<NP>(lo, d, t, sp);
-          prod[t] = s == 0 ? v : mul29t(prod[t], v);
+          if (s == 0)
+            prod[t] = at_point<NP>(lo, d, t, sp);
+          else
+            prod[t] = mul29t(prod[t], at_point_lazy<NP>(lo, d, t, sp));
         }
         if constexpr (PF) {
 #pragma unroll
@@ -787,7 +821,13 @@ QG_DEV void sweep_pairs(const AllBufs& tb, uint32_t j, bool fold, const R29& r, 
         for (int t = 0; t < NP; t++) acc[t] = red16p29<FrP>(acc[t]);
         cnt = 0;
       }
-    } else {
+    };
+    for (size_t p = p0; p < npairs; p += stride) body(p);
+
+  } else {
+  for (size_t p = p0; p < npairs; p += stride) {
+    R29 prod[NP];
+    {
       static_assert(PURE || K <= 4, "generic sweep keeps <= 4 slots in registers");
       R29 lo[K], hi[K], dd[K];
 #pragma unroll
@@ -836,6 +876,7 @@ QG_DEV void sweep_pairs(const AllBufs& tb, uint32_t j, bool fold, const R29& r, 
         }
       }
     }
+  }
   }
 #pragma unroll
   for (int t = 0; t < NP; t++) acc[t] = red16p29<FrP>(acc[t]);
@@ -894,9 +935,10 @@ __global__ void __launch_bounds__(SC_BLOCK) __attribute__((amdgpu_waves_per_eu(W
 #pragma unroll
   for (int t = 0; t < NP; t++) acc[t] = R29::zero();
   sweep_pairs<K, NP, PURE, PF>(tb, j, fold, r, npairs, (size_t)blockIdx.x * SC_BLOCK + tid,
-                           (size_t)gridDim.x * SC_BLOCK, sp, h, skip0 != 0, acc);
+                               (size_t)gridDim.x * SC_BLOCK, sp, h, skip0 != 0, acc);
   if (blockIdx.x == 0) SC_TR(tr + 1);
   SC_TB(j, 1);
+  SC_TW(j);
   block_sums29<NP>(acc, np, red, res);
   // publish: sc1 row stores, every storing wave drains, then one ticket add
   if (tid < np) st_sc1(partial + (size_t)blockIdx.x * NP + tid, from29(canon29(res[tid])));
@@ -1048,7 +1090,7 @@ QG_DEV void tail_eval(const R29* F, uint32_t ss, const SopLds<NP>& sp, const Sop
           R29 a = lo;
           if (t & 1u) a = add29(a, d);
           if (t & 2u) a = add29(a, add29(d, d));
-          v = norm29(a);
+          v = q == 0 ? norm29(a) : a;  // later factors stay lazy (see at_point_lazy)
         } else {
           v = norm29(add29(lo, mul29(sub29(hi, lo), sp.t29[t])));
         }
@@ -1119,11 +1161,11 @@ __global__ void __launch_bounds__(TAIL_BLOCK)
         R29 v;
         if (prev) {  // LDS-resident source: entries 2e, 2e+1 of the previous table
           const R29 x0 = prev[s * ss_prev + 2 * e], x1 = prev[s * ss_prev + 2 * e + 1];
-          v = red6p(add29(x0, mul29(sub29(x1, x0), r)));
+          v = red2p29<FrP>(add29(x0, mul29(sub29(x1, x0), r)));
         } else if (fold) {
           const Fr* src = cur.src[s] + 2 * idx;
           const R29 x0 = to29(ld_sc1(src)), x1 = to29(ld_sc1(src + 1));
-          v = red6p(add29(x0, mul29(sub29(x1, x0), r)));
+          v = red2p29<FrP>(add29(x0, mul29(sub29(x1, x0), r)));
           if (!single) st_sc1(cur.dst[s] + idx, from29(v));
         } else {
           v = to29(ld_sc1(cur.src[s] + idx));
@@ -2302,6 +2344,10 @@ extern "C" {
 int qg_debug_sc_trace(uint64_t* out, size_t n) {
   if (n > 2048 + 4 * 1536) n = 2048 + 4 * 1536;
   return hipMemcpyFromSymbol(out, HIP_SYMBOL(g_sc_trace), n * 8) == hipSuccess ? QG_OK : QG_ERR_DEVICE;
+}
+int qg_debug_sc_wtrace(uint64_t* out, size_t n) {
+  if (n > 4 * 512 * 8 * 2) n = 4 * 512 * 8 * 2;
+  return hipMemcpyFromSymbol(out, HIP_SYMBOL(g_sc_wtrace), n * 8) == hipSuccess ? QG_OK : QG_ERR_DEVICE;
 }
 #endif
 

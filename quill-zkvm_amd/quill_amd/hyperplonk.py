@@ -72,17 +72,26 @@ class VirtualPolyExpr:
 
 
 def _program_c(expr: VirtualPolyExpr):
-    ops, consts = expr.to_program()
-    prog = (ExprOp * len(ops))(*[ExprOp(o, a) for o, a in ops])
-    carr = fr_array(consts) if consts else np.zeros((1, 4), dtype=np.uint64)
-    return prog, len(ops), carr, len(consts)
+    # expressions are immutable once built: the compiled program (read-only for
+    # the library) is kept on the object, so a prover called in a loop does not
+    # recompile it per call
+    c = expr.__dict__.get("_qg_prog")
+    if c is None:
+        ops, consts = expr.to_program()
+        prog = (ExprOp * len(ops))(*[ExprOp(o, a) for o, a in ops])
+        carr = fr_array(consts) if consts else np.zeros((1, 4), dtype=np.uint64)
+        c = expr._qg_prog = (prog, len(ops), carr, len(consts))
+    return c
 
 
 def expr_degree(expr: VirtualPolyExpr) -> int:
-    prog, n, _, _ = _program_c(expr)
-    d = C.c_uint32()
-    check(lib().qg_expr_degree(prog, n, C.byref(d)))
-    return d.value
+    d = expr.__dict__.get("_qg_deg")
+    if d is None:
+        prog, n, _, _ = _program_c(expr)
+        dd = C.c_uint32()
+        check(lib().qg_expr_degree(prog, n, C.byref(dd)))
+        d = expr._qg_deg = dd.value
+    return d
 
 
 class VirtualPolynomialStore:
