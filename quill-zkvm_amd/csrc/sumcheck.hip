@@ -1254,6 +1254,258 @@ __global__ void __launch_bounds__(TAIL_BLOCK)
 }
 
 // ---------------------------------------------------------------------------
+// Slice tail (replaces k_sc_tail whenever a block's slice fits its LDS): the
+// rounds j0..nvars-1 in ONE launch of G blocks (one per CU), block b OWNING
+// the contiguous entries [b S, (b+1) S) of the round-j0 table (S = 2^(nvars -
+// j0) / G per slot).  The fold pairs adjacent entries, so block b's slice of
+// round j+1 is the fold of its own slice of round j: after the one HBM load
+// of the first round the tables never leave the block's LDS, and nothing but
+// the per-round sums crosses blocks (partial rows + grid barrier, then every
+// block runs the identical transcript step).  When a slice is down to one
+// pair, each block folds it to one entry per slot, writes it to HBM, and
+// after one more barrier block 0 gathers the G entries and finishes the last
+// log2(G) rounds alone (the table again in LDS).  The deferred absorb of the
+// previous challenge runs on the last wave beside the other waves' evaluation.
+// ---------------------------------------------------------------------------
+// Barrier over the G blocks of the slice tail with its arrival counter split
+// in 8 shards (block b adds to shard b % 8, its XCD under round-robin
+// dispatch; each shard on its own 128-B line): a few dozen arrivals per line
+// instead of G on one.  The counters run cumulatively through the launch
+// (`target` = all arrivals so far), zeroed by the host per call.  Every wave
+// drains its stores and atomics first; the poll reads every shard (sc1).
+QG_DEV void grid_barrier8(uint32_t* bar8, uint32_t target, uint32_t* err) {
+  drain_stores();
+  __syncthreads();
+  if (threadIdx.x == 0) {
+    __hip_atomic_fetch_add((gu32*)(bar8 + 32 * (blockIdx.x & 7)), 1u, __ATOMIC_RELAXED,
+                           __HIP_MEMORY_SCOPE_AGENT);
+    uint32_t spins = 0;
+    for (;;) {
+      uint32_t v[8], sum = 0;
+#pragma unroll
+      for (int x = 0; x < 8; x++) v[x] = ld_sc1_u32(bar8 + 32 * x);
+#pragma unroll
+      for (int x = 0; x < 8; x++) sum += v[x];
+      if (sum >= target) break;
+      __builtin_amdgcn_s_sleep(1);
+      if (++spins > (1u << 26)) {
+        st_sc1_u32(err, 1u);
+        break;
+      }
+    }
+    __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");  // no instruction: keeps loads below
+  }
+  __syncthreads();
+}
+
+// u64 sums of normalized 29-bit limbs (each sum < 2^40) -> the value mod p,
+// < 2p normalized.  T = L + c 2^261 with L < 2^261 and c < 4 when T is a sum
+// of fewer than 680 values < 2p; 2^261 = ONE (mod p), so T = L + c ONE < 173p.
+QG_DEV R29 limbsum29(const uint64_t* a) {
+  R29 x;
+  uint64_t c = 0;
+#pragma unroll
+  for (int i = 0; i < 9; i++) {
+    const uint64_t v = a[i] + c;
+    x.l[i] = (uint32_t)v & M29;
+    c = v >> 29;
+  }
+  x = normfull29<FrP>(add29(x, R29::from_l9(l9_mul_small(F29P<FrP>::ONE, (uint32_t)c))));
+  x = condsub29<FrP>(x, l9_mul_small(F29P<FrP>::P, 128));
+  return red128p(x);
+}
+
+static constexpr int SL_BLOCK = 256;
+// entries per slot of a block's slice in the first tail round (LDS: K slots x
+// 1.5 x SL_SMAX entries of 36 B: the slice and its half-size fold)
+QG_HD constexpr uint32_t sl_smax(int K) { return K <= 4 ? 256u : 128u; }
+
+template <int K, int NP>
+__global__ void __launch_bounds__(SL_BLOCK)
+    k_sc_slice(TablePtrs tp0, TablePtrs gat, const SopDev* __restrict__ spg, SopHdr h,
+               uint32_t nvars, uint32_t j0, int fold0, int pending0, RoundOut ro,
+               Fr* __restrict__ partial, uint32_t* __restrict__ bar8, uint64_t* __restrict__ acc64,
+               Fr* __restrict__ final_vals, Fr* __restrict__ evaluation) {
+  constexpr uint32_t SMAX = sl_smax(K);
+  __shared__ SopLds<NP> sp;
+  __shared__ R29 Fbuf[K * SMAX * 3 / 2];
+  __shared__ R29 red[(SL_BLOCK / 64) * NP];
+  __shared__ R29 res[NP];
+  __shared__ FinSmem fs;
+  __shared__ uint32_t st[8];
+  __shared__ uint32_t pend[32];
+  __shared__ uint64_t lsum[NP * 9];
+  const uint32_t tid = threadIdx.x, blk = blockIdx.x;
+  const uint32_t nslots = h.nslots, np = h.np;
+  const uint32_t t = tid % NP;
+  const bool last_wave = tid >= SL_BLOCK - 64;
+  // per-round limb accumulators of rounds > j0: [round - j0 - 1][shard 8][NP][9],
+  // zeroed here by block 0 before it meets the others at round j0's barrier
+  constexpr uint32_t ACC_R = 8 * NP * 9;
+  if (blk == 0)
+    for (uint32_t i = tid; i < (nvars - j0 - 1) * ACC_R; i += SL_BLOCK)
+      __hip_atomic_store((gu64*)(acc64 + i), (uint64_t)0, __ATOMIC_RELAXED,
+                         __HIP_MEMORY_SCOPE_AGENT);
+  uint32_t arrived = 0;                          // cumulative barrier arrivals
+  uint32_t G = gridDim.x;                        // blocks holding a slice this round
+  uint32_t S = (1u << (nvars - j0)) / G;         // entries per slot of this block's slice
+  sop_load<NP>(sp, spg, h, true);
+  if (tid < 8) st[tid] = ro.st->state[tid];
+  if (tid < 32) pend[tid] = (pending0 && tid < 20) ? ro.st->pend[tid] : 0u;
+  R29 r = R29::zero();
+  if (fold0) {
+#pragma unroll
+    for (int i = 0; i < 9; i++) r.l[i] = ro.st->r29[i];
+  }
+  R29* cur = Fbuf;                // slot stride S
+  R29* nxt = Fbuf + K * SMAX;     // slot stride S / 2
+  // the block's slice of the round-j0 table (folded from the source by r_{j0-1})
+  for (uint32_t it = tid; it < nslots * S; it += SL_BLOCK) {
+    const uint32_t s = it / S, e = it % S;
+    const size_t idx = (size_t)blk * S + e;
+    R29 v;
+    if (fold0) {
+      const Fr* src = tp0.src[s] + 2 * idx;
+      const R29 x0 = to29(src[0]), x1 = to29(src[1]);
+      v = red2p29<FrP>(add29(x0, mul29(sub29(x1, x0), r)));
+    } else {
+      v = to29(tp0.src[s][idx]);
+    }
+    cur[s * S + e] = v;
+  }
+  int pending = pending0;
+  __syncthreads();
+  for (uint32_t j = j0; j < nvars; j++) {
+    if (blk == 0) SC_TR(16 * j + 0);
+    // ---- evaluate round j on the slice: thread (pair, point) items; the last
+    // wave absorbs the previous challenge instead when one is pending
+    // a round that regroups (below) publishes its slice before the barrier
+    const bool regroup = G > 1 && S <= SMAX / 8;
+    if (regroup)
+      for (uint32_t it = tid; it < nslots * S; it += SL_BLOCK) {
+        const uint32_t s = it / S, e = it % S;
+        st_sc1(gat.dst[s] + (size_t)blk * S + e, from29(cur[s * S + e]));
+      }
+    const uint32_t ne = pending ? SL_BLOCK - 64 : SL_BLOCK;
+    if (pending && last_wave) b3_hash_quad(pend, 80, st, 8);
+    R29 acc = R29::zero();
+    const uint32_t items = (S / 2) * NP;
+    if (tid < ne)
+      for (uint32_t it = tid; it < items; it += ne)
+        if (t < np) tail_eval<NP>(cur, S, sp, h, it / NP, t, acc);
+    if (blk == 0) SC_TR(16 * j + 1);
+    tail_reduce<NP>(acc, std::min(items, ne), np, red, res);
+    if (blk == 0) SC_TR(16 * j + 7);
+    if (G > 1 && j > j0) {
+      // limbs of the block sums added into this round's accumulator shard
+      // (agent-scope u64 atomics at the memory side), one sharded barrier, then
+      // every block fetches the 8 shards with returning atomics and rebuilds
+      // the sums: no partial rows, one memory round trip
+      uint64_t* ar = acc64 + (size_t)(j - j0 - 1) * ACC_R;
+      if (tid < np * 9)
+        __hip_atomic_fetch_add((gu64*)(ar + (blk & 7) * NP * 9 + tid),
+                               (uint64_t)res[tid / 9].l[tid % 9], __ATOMIC_RELAXED,
+                               __HIP_MEMORY_SCOPE_AGENT);
+      arrived += G;
+      grid_barrier8(bar8, arrived, &ro.st->err);
+      if (blk == 0) SC_TR(16 * j + 8);
+      if (tid < np * 9) {
+        uint64_t v[8], a = 0;
+#pragma unroll
+        for (int x = 0; x < 8; x++)
+          v[x] = __hip_atomic_fetch_add((gu64*)(ar + x * NP * 9 + tid), (uint64_t)0,
+                                        __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+#pragma unroll
+        for (int x = 0; x < 8; x++) a += v[x];
+        lsum[tid] = a;
+      }
+      __syncthreads();
+      if (tid < np) res[tid] = limbsum29(lsum + 9 * tid);
+      __syncthreads();
+    } else if (G > 1) {
+      // round j0: partial rows (the accumulators are zeroed behind this barrier)
+      Fr* part = partial;
+      if (tid < np) st_sc1(part + (size_t)blk * NP + tid, from29(canon29(res[tid])));
+      arrived += G;
+      grid_barrier8(bar8, arrived, &ro.st->err);
+      if (blk == 0) SC_TR(16 * j + 8);
+      acc = R29::zero();
+      const uint32_t pl = tid / NP;
+      if (t < np)
+        for (uint32_t b0 = pl; b0 < G; b0 += 4 * (SL_BLOCK / NP)) {
+          Fr v[4];
+#pragma unroll
+          for (int k = 0; k < 4; k++) {
+            const uint32_t b = b0 + k * (SL_BLOCK / NP);
+            v[k] = b < G ? ld_sc1(part + (size_t)b * NP + t) : Fr::zero();
+          }
+#pragma unroll
+          for (int k = 0; k < 4; k++) acc = add29(acc, to29(v[k]));
+          acc = red6p(acc);
+        }
+      tail_reduce<NP>(acc, std::min<uint32_t>(G, SL_BLOCK / NP) * NP, np, red, res);
+    }
+    if (blk == 0) SC_TR(16 * j + 2);
+    finish_core<NP>(sp, np, res, ro, j, fs, st, pend, nullptr, blk == 0 ? 16 * j : 4096, blk == 0,
+                    true);
+    __syncthreads();
+    r = fs.r;
+    pending = 1;
+    if (j + 1 == nvars) break;  // S == 2, G == 1: the final fold below
+    if (regroup) {
+      // f blocks' round-j slices (published before the barrier) become one
+      // block's round-(j+1) slice, folded on the load; the other blocks retire.
+      // Fewer blocks: a cheaper barrier and fewer partial rows per round.
+      const uint32_t f = std::min<uint32_t>(G, 2 * SMAX / S);
+      const uint32_t G2 = G / f;
+      if (blk >= G2) return;
+      const uint32_t S2 = f * S / 2;
+      for (uint32_t it = tid; it < nslots * S2; it += SL_BLOCK) {
+        const uint32_t s = it / S2, e = it % S2;
+        const Fr* src = gat.dst[s] + (size_t)blk * f * S + 2 * e;
+        const R29 x0 = to29(ld_sc1(src)), x1 = to29(ld_sc1(src + 1));
+        Fbuf[s * S2 + e] = red2p29<FrP>(add29(x0, mul29(sub29(x1, x0), r)));
+      }
+      S = S2;
+      G = G2;
+      cur = Fbuf + K * SMAX;  // swapped below: cur = Fbuf (S2 <= SMAX), nxt = the second array
+      nxt = Fbuf;
+    } else {
+      // fold the slice by r_j into the other array
+      const uint32_t h2 = S / 2;
+      for (uint32_t it = tid; it < nslots * h2; it += SL_BLOCK) {
+        const uint32_t s = it / h2, e = it % h2;
+        const R29 x0 = cur[s * S + 2 * e], x1 = cur[s * S + 2 * e + 1];
+        nxt[s * h2 + e] = red2p29<FrP>(add29(x0, mul29(sub29(x1, x0), r)));
+      }
+      S = h2;
+    }
+    R29* tmp = cur;
+    cur = nxt;
+    nxt = tmp;
+    __syncthreads();
+  }
+  // final fold with r_{n-1} on the 32-bit path: one pair per slot left in cur (block 0)
+  if (tid == 0) {
+    const Fr rr = fs.r256;
+    Fr val[K];
+#pragma unroll
+    for (int i = 0; i < K; i++) {
+      if ((uint32_t)i < nslots) {
+        const Fr a = lt_p(from29(cur[i * 2])), b = lt_p(from29(cur[i * 2 + 1]));
+        val[i] = a + rr * (b - a);
+        final_vals[i] = val[i];
+      } else {
+        val[i] = Fr::zero();
+      }
+    }
+    *evaluation = sop_eval_final<K>(spg, h.nmono, val);
+  }
+  // absorb the last challenge bytes
+  if (pending && tid < 64) b3_hash_quad(pend, 80, ro.st->state, 8);
+}
+
+// ---------------------------------------------------------------------------
 // Generic expressions: everything the compiled fast path does not take (more
 // than 8 tables, degree above 15, a monomial expansion beyond 256 / 1024
 // terms, or one that does not expand at all).  The postfix program itself is
@@ -1541,14 +1793,16 @@ static std::shared_ptr<const ScProgram> get_program(const qg_expr_op* prog, size
 // the device holds at once (occupancy API x CUs, one block per CU margin kept
 // for the gfx950 SGPR admission rule of MI355X_MICROARCH.md "Residency").
 // Queried once per context and kernel instantiation.
-template <int K, int NP>
+template <int K, int NP, bool SLICE = false>
 static unsigned persist_grid_cap(qg_ctx* ctx, size_t cus) {
-  const std::string key = "persist_occ_" + std::to_string(K) + "_" + std::to_string(NP);
+  const std::string key = std::string(SLICE ? "slice_occ_" : "persist_occ_") + std::to_string(K) +
+                          "_" + std::to_string(NP);
   auto it = ctx->memo.find(key);
   int occ = 0;
   if (it == ctx->memo.end()) {
-    QG_HIP(hipOccupancyMaxActiveBlocksPerMultiprocessor(
-        &occ, reinterpret_cast<const void*>(&k_sc_tail<K, NP>), TAIL_BLOCK, 0));
+    const void* fn = SLICE ? reinterpret_cast<const void*>(&k_sc_slice<K, NP>)
+                           : reinterpret_cast<const void*>(&k_sc_tail<K, NP>);
+    QG_HIP(hipOccupancyMaxActiveBlocksPerMultiprocessor(&occ, fn, SLICE ? SL_BLOCK : TAIL_BLOCK, 0));
     ctx->memo[key] = std::to_string(occ);
   } else {
     occ = std::stoi(it->second);
@@ -1564,6 +1818,68 @@ static unsigned persist_grid_cap(qg_ctx* ctx, size_t cus) {
   }();
   const int bpc = std::max(1, std::min(bpc_env, occ - 1));
   return (unsigned)std::max<size_t>(1, cus * (size_t)bpc);
+}
+
+// io header: ScState | per-round barrier counters (nvars + 2) | 8 barrier
+// shards of the slice tail, one 128-B line each | challenges ...
+static size_t sumcheck_o_bar8(uint32_t nvars) {
+  return (sizeof(ScState) + sizeof(uint32_t) * (nvars + 2) + 127) & ~(size_t)127;
+}
+static uint32_t* sumcheck_bar8(uint32_t* bar, uint32_t nvars) {
+  uint8_t* io = reinterpret_cast<uint8_t*>(bar) - sizeof(ScState);
+  return reinterpret_cast<uint32_t*>(io + sumcheck_o_bar8(nvars));
+}
+
+// The slice tail (k_sc_slice): G blocks, a power of two <= min(one per CU,
+// SMAX) so block 0 can gather one entry per block, each owning <= SMAX entries
+// per slot.  QG_SC_OLD_TAIL=1 keeps the streaming k_sc_tail (A/B runs).
+template <int K, int NP>
+static size_t slice_gmax(qg_ctx* ctx, size_t cus) {
+  static const bool off = getenv("QG_SC_OLD_TAIL") != nullptr;
+  if (off) return 0;
+  const size_t gm = std::min<size_t>(persist_grid_cap<K, NP, true>(ctx, cus), sl_smax(K));
+  size_t G = 1;
+  while (G * 2 <= gm) G *= 2;
+  return G;
+}
+
+// largest round table (entries per slot) the slice tail can start from
+template <int K, int NP>
+static uint32_t slice_tail_log(qg_ctx* ctx, size_t cus) {
+  const size_t g = slice_gmax<K, NP>(ctx, cus);
+  if (!g) return 0;
+  uint32_t l = 0;
+  while (((size_t)1 << (l + 1)) <= g * sl_smax(K)) l++;
+  return l;
+}
+
+// launches k_sc_slice for rounds j0.. when a block's slice fits its LDS;
+// false: the caller launches k_sc_tail.
+template <int K, int NP>
+static bool launch_slice_tail(qg_ctx* ctx, size_t cus, TablePtrs t0, const SopDev* d_sp, SopHdr h,
+                              uint32_t nvars, uint32_t j0, int fold0,
+                              int pending0, RoundOut ro, uint32_t* bar, Fr* d_final, Fr* d_eval) {
+  const size_t gm = slice_gmax<K, NP>(ctx, cus);
+  if (!gm) return false;
+  const size_t n0 = (size_t)1 << (nvars - j0);
+  size_t G = 1;
+  while (G * 2 <= gm && G * 2 <= n0 / 2) G *= 2;
+  if (n0 / G > sl_smax(K)) return false;
+  Fr* ppart = ctx->scratch_as<Fr>("sc_spartial", (size_t)G * NP);
+  uint64_t* acc64 = ctx->scratch_as<uint64_t>("sc_sacc", (size_t)std::max<uint32_t>(1, nvars - j0) * 8 * NP * 9);
+  // the 8 barrier shards follow the per-round counters (zeroed by the per-call
+  // header copy): sumcheck_bar8
+  uint32_t* bar8 = sumcheck_bar8(bar, nvars);
+  // regroup area: the round table published by the blocks (<= n0 entries per slot)
+  const uint32_t ns = std::max<uint32_t>(h.nslots, 1u);
+  Fr* sg = ctx->scratch_as<Fr>("sc_sgat", (size_t)ns * n0);
+  TablePtrs gat{};
+  for (uint32_t i = 0; i < 8; i++) gat.dst[i] = i < h.nslots ? sg + (size_t)i * n0 : nullptr;
+  hipLaunchKernelGGL((k_sc_slice<K, NP>), dim3((unsigned)G), dim3(SL_BLOCK), 0, ctx->stream, t0,
+                     gat, d_sp, h, nvars, j0, fold0, pending0, ro, ppart, bar8, acc64, d_final,
+                     d_eval);
+  QG_LAUNCH_CHECK();
+  return true;
 }
 
 // thread-per-pair round kernel (k_sc_big) for product expressions and for
@@ -1650,9 +1966,12 @@ static uint32_t run_rounds(qg_ctx* ctx, uint32_t nvars, const std::vector<const 
   }();
   {
     QgTimed tm(ctx, "sumcheck_round");
+    // the slice tail starts once a round's table fits the blocks' LDS slices
+    const uint32_t sl = slice_tail_log<K, NP>(ctx, ctx->num_cus());
+    const int plog = sl ? std::min<int>(pers_log, (int)sl) : pers_log;
     for (; j < nvars; j++) {
       const size_t table = N >> j;  // entries per table evaluated in round j
-      if (table <= ((size_t)1 << pers_log)) break;
+      if (table <= ((size_t)1 << plog)) break;
       const size_t npairs = table / 2;
       TablePtrs tp = cur;
       if (fold) {
@@ -1690,17 +2009,20 @@ static uint32_t run_rounds(qg_ctx* ctx, uint32_t nvars, const std::vector<const 
       bufA = b;
       bufB = a;
     }
-    // persistent launch: one block per CU at most (co-residency for the grid
-    // barrier), fewer when the first persistent round has fewer pair groups
-    const size_t PB = tail_pb(h.nslots, NP);
-    const size_t pairs0 = (N >> j) / 2;
-    const unsigned grid = (unsigned)std::max<size_t>(
-        1, std::min<size_t>(persist_grid_cap<K, NP>(ctx, ctx->num_cus()), (pairs0 + PB - 1) / PB));
-    Fr* ppart = ctx->scratch_as<Fr>("sc_ppartial", (size_t)2 * grid * NP);
-    hipLaunchKernelGGL((k_sc_tail<K, NP>), dim3(grid), dim3(TAIL_BLOCK), 0, ctx->stream, t0,
-                       bufA, bufB, d_sp, h, nvars, j, fold, pending, ro, ppart, bar, d_final,
-                       d_eval);
-    QG_LAUNCH_CHECK();
+    if (!launch_slice_tail<K, NP>(ctx, ctx->num_cus(), t0, d_sp, h, nvars, j, fold, pending, ro,
+                                  bar, d_final, d_eval)) {
+      // persistent launch: one block per CU at most (co-residency for the grid
+      // barrier), fewer when the first persistent round has fewer pair groups
+      const size_t PB = tail_pb(h.nslots, NP);
+      const size_t pairs0 = (N >> j) / 2;
+      const unsigned grid = (unsigned)std::max<size_t>(
+          1, std::min<size_t>(persist_grid_cap<K, NP>(ctx, ctx->num_cus()), (pairs0 + PB - 1) / PB));
+      Fr* ppart = ctx->scratch_as<Fr>("sc_ppartial", (size_t)2 * grid * NP);
+      hipLaunchKernelGGL((k_sc_tail<K, NP>), dim3(grid), dim3(TAIL_BLOCK), 0, ctx->stream, t0,
+                         bufA, bufB, d_sp, h, nvars, j, fold, pending, ro, ppart, bar, d_final,
+                         d_eval);
+      QG_LAUNCH_CHECK();
+    }
   }
   return j;
 }
@@ -1828,13 +2150,16 @@ static uint32_t run_rounds_dist(qg_ctx* ctx, uint32_t nvars, const std::vector<c
     // shares one device, so each persistent grid takes a 1/world share of the CUs
     const size_t cus = comm_is_loopback(ctx) ? std::max<size_t>(1, ctx->num_cus() / world)
                                              : (size_t)ctx->num_cus();
-    const unsigned grid = (unsigned)std::max<size_t>(
-        1, std::min<size_t>(persist_grid_cap<K, NP>(ctx, cus), (pairs0 + PB - 1) / PB));
-    Fr* ppart = ctx->scratch_as<Fr>("sc_ppartial", (size_t)2 * grid * NP);
-    hipLaunchKernelGGL((k_sc_tail<K, NP>), dim3(grid), dim3(TAIL_BLOCK), 0, ctx->stream, t0,
-                       bufA, bufB, d_sp, h, nvars, js, js >= 1 ? 1 : 0, 0, ro, ppart, bar,
-                       d_final, d_eval);
-    QG_LAUNCH_CHECK();
+    if (!launch_slice_tail<K, NP>(ctx, cus, t0, d_sp, h, nvars, js, js >= 1 ? 1 : 0, 0, ro, bar,
+                                  d_final, d_eval)) {
+      const unsigned grid = (unsigned)std::max<size_t>(
+          1, std::min<size_t>(persist_grid_cap<K, NP>(ctx, cus), (pairs0 + PB - 1) / PB));
+      Fr* ppart = ctx->scratch_as<Fr>("sc_ppartial", (size_t)2 * grid * NP);
+      hipLaunchKernelGGL((k_sc_tail<K, NP>), dim3(grid), dim3(TAIL_BLOCK), 0, ctx->stream, t0,
+                         bufA, bufB, d_sp, h, nvars, js, js >= 1 ? 1 : 0, 0, ro, ppart, bar,
+                         d_final, d_eval);
+      QG_LAUNCH_CHECK();
+    }
   }
   return js;
 }
@@ -2213,7 +2538,7 @@ static void sumcheck_run(qg_ctx* ctx, uint32_t nvars, uint32_t ntables,
   // one device region: ScState | barrier counters | chal | coeffs | final (8 slots +
   // evaluation) | lens.  ScState and the counters are (re)initialised per call.
   const size_t o_bar = sizeof(ScState);
-  const size_t o_chal = o_bar + sizeof(uint32_t) * ((nvars + 2 + 7) & ~7u);
+  const size_t o_chal = sumcheck_o_bar8(nvars) + 8 * 128;  // after the barrier shards
   const size_t o_coeffs = o_chal + sizeof(Fr) * nvars;
   const size_t o_final = o_coeffs + sizeof(Fr) * (size_t)nvars * width;
   const size_t o_lens = o_final + sizeof(Fr) * 9;
