@@ -685,6 +685,54 @@ __global__ void __launch_bounds__(SC_BLOCK)
 // LDS-staged k_sc_round.
 // ---------------------------------------------------------------------------
 
+// Barrier over the G blocks of the slice tail with its arrival counter split
+// in 8 shards (block b adds to shard b % 8, its XCD under round-robin
+// dispatch; each shard on its own 128-B line): a few dozen arrivals per line
+// instead of G on one.  The counters run cumulatively through the launch
+// (`target` = all arrivals so far), zeroed by the host per call.  Every wave
+// drains its stores and atomics first; the poll reads every shard (sc1).
+QG_DEV void grid_barrier8(uint32_t* bar8, uint32_t target, uint32_t* err) {
+  drain_stores();
+  __syncthreads();
+  if (threadIdx.x == 0) {
+    __hip_atomic_fetch_add((gu32*)(bar8 + 32 * (blockIdx.x & 7)), 1u, __ATOMIC_RELAXED,
+                           __HIP_MEMORY_SCOPE_AGENT);
+    uint32_t spins = 0;
+    for (;;) {
+      uint32_t v[8], sum = 0;
+#pragma unroll
+      for (int x = 0; x < 8; x++) v[x] = ld_sc1_u32(bar8 + 32 * x);
+#pragma unroll
+      for (int x = 0; x < 8; x++) sum += v[x];
+      if (sum >= target) break;
+      __builtin_amdgcn_s_sleep(1);
+      if (++spins > (1u << 26)) {
+        st_sc1_u32(err, 1u);
+        break;
+      }
+    }
+    __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");  // no instruction: keeps loads below
+  }
+  __syncthreads();
+}
+
+// u64 sums of normalized 29-bit limbs (each sum < 2^40) -> the value mod p,
+// < 2p normalized.  T = L + c 2^261 with L < 2^261 and c < 32 when T is a sum
+// of fewer than 2720 values < 2p; 2^261 = ONE (mod p), so T = L + c ONE < 202p.
+QG_DEV R29 limbsum29(const uint64_t* a) {
+  R29 x;
+  uint64_t c = 0;
+#pragma unroll
+  for (int i = 0; i < 9; i++) {
+    const uint64_t v = a[i] + c;
+    x.l[i] = (uint32_t)v & M29;
+    c = v >> 29;
+  }
+  x = normfull29<FrP>(add29(x, R29::from_l9(l9_mul_small(F29P<FrP>::ONE, (uint32_t)c))));
+  x = condsub29<FrP>(x, l9_mul_small(F29P<FrP>::P, 128));
+  return red128p(x);
+}
+
 // ---------------------------------------------------------------------------
 // Large rounds, thread per pair (k_sc_big).
 //  * Sweep: one thread per pair, grid-stride.  Slot by slot the thread folds
@@ -889,12 +937,14 @@ QG_DEV void sweep_pairs(const AllBufs& tb, uint32_t j, bool fold, const R29& r, 
 template <int K, int NP, bool PURE, bool PF, int WPE = 1>
 __global__ void __launch_bounds__(SC_BLOCK) __attribute__((amdgpu_waves_per_eu(WPE)))
     k_sc_big(AllBufs tb, uint32_t j, const SopDev* __restrict__ spg, SopHdr h, size_t npairs,
-             RoundOut ro, int pending, Fr* __restrict__ partial, Fr* __restrict__ loc, int skip0) {
+             RoundOut ro, int pending, Fr* __restrict__ loc, int skip0, uint64_t* __restrict__ acc_j,
+             uint64_t* __restrict__ acc_next, uint32_t* __restrict__ bar8) {
   __shared__ SopLds<NP> sp;
   __shared__ R29 red[(SC_BLOCK / 64) * NP];
   __shared__ R29 res[NP];
   __shared__ FinSmem fs;
   __shared__ uint32_t last;
+  __shared__ uint64_t lsum[NP * 9];
   const uint32_t tid = threadIdx.x;
   const uint32_t tr = 1024 + 16 * j;
   const bool fold = j > 0;
@@ -940,14 +990,28 @@ __global__ void __launch_bounds__(SC_BLOCK) __attribute__((amdgpu_waves_per_eu(W
   SC_TB(j, 1);
   SC_TW(j);
   block_sums29<NP>(acc, np, red, res);
-  // publish: sc1 row stores, every storing wave drains, then one ticket add
-  if (tid < np) st_sc1(partial + (size_t)blockIdx.x * NP + tid, from29(canon29(res[tid])));
+  // publish: the limbs of the block sums added into this round's accumulator
+  // shard (agent-scope u64 atomics, executed at the memory side), every wave
+  // drains, then a two-level ticket: the block completing its shard (blocks b
+  // with b % 8 = x, one 128-B counter line per shard) adds to the round's
+  // ticket, and the one completing that is the last block
+  if (tid < np * 9)
+    __hip_atomic_fetch_add((gu64*)(acc_j + (blockIdx.x & 7) * (16 * 9) + tid),
+                           (uint64_t)res[tid / 9].l[tid % 9], __ATOMIC_RELAXED,
+                           __HIP_MEMORY_SCOPE_AGENT);
   drain_stores();
   __syncthreads();
   if (tid == 0) {
-    const uint32_t old = __hip_atomic_fetch_add((gu32*)&ro.st->ticket, 1u, __ATOMIC_RELAXED,
-                                                __HIP_MEMORY_SCOPE_AGENT);
-    last = old + 1 == gridDim.x;
+    const uint32_t x = blockIdx.x & 7, nx = (gridDim.x + 7 - x) / 8;
+    bool done = false;
+    const uint32_t o1 = __hip_atomic_fetch_add((gu32*)(bar8 + 32 * x), 1u, __ATOMIC_RELAXED,
+                                               __HIP_MEMORY_SCOPE_AGENT);
+    if (o1 + 1 == nx) {
+      const uint32_t o2 = __hip_atomic_fetch_add((gu32*)&ro.st->ticket, 1u, __ATOMIC_RELAXED,
+                                                 __HIP_MEMORY_SCOPE_AGENT);
+      done = o2 + 1 == (gridDim.x < 8 ? gridDim.x : 8u);
+    }
+    last = done;
     __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");  // no instruction: loads stay below
   }
   __syncthreads();
@@ -955,7 +1019,25 @@ __global__ void __launch_bounds__(SC_BLOCK) __attribute__((amdgpu_waves_per_eu(W
   SC_TR(tr + 2);
   __shared__ uint32_t st_in[8];
   if (tid < 8) st_in[tid] = ld_sc1_u32(&ro.st->state[tid]);
-  sum_rows29<NP>(partial, gridDim.x, np, red, res);
+  if (tid < np * 9) {
+    uint64_t v[8], a = 0;
+#pragma unroll
+    for (int x = 0; x < 8; x++)
+      v[x] = __hip_atomic_fetch_add((gu64*)(acc_j + x * (16 * 9) + tid), (uint64_t)0,
+                                    __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+#pragma unroll
+    for (int x = 0; x < 8; x++) a += v[x];
+    lsum[tid] = a;
+  }
+  __syncthreads();
+  if (tid < np) res[tid] = limbsum29(lsum + 9 * tid);
+  // counters back to zero and the next round's accumulator cleared (the next
+  // kernel on the stream sees both)
+  if (tid < 8) st_sc1_u32(bar8 + 32 * tid, 0u);
+  for (uint32_t i = tid; i < 8 * 16 * 9; i += SC_BLOCK)
+    __hip_atomic_store((gu64*)(acc_next + i), (uint64_t)0, __ATOMIC_RELAXED,
+                       __HIP_MEMORY_SCOPE_AGENT);
+  __syncthreads();
   SC_TR(tr + 8);
   if (tid == 0) ro.st->ticket = 0;
   if (loc) {  // sharded: k_sc_finish applies the claim to the global sums
@@ -1267,54 +1349,6 @@ __global__ void __launch_bounds__(TAIL_BLOCK)
 // log2(G) rounds alone (the table again in LDS).  The deferred absorb of the
 // previous challenge runs on the last wave beside the other waves' evaluation.
 // ---------------------------------------------------------------------------
-// Barrier over the G blocks of the slice tail with its arrival counter split
-// in 8 shards (block b adds to shard b % 8, its XCD under round-robin
-// dispatch; each shard on its own 128-B line): a few dozen arrivals per line
-// instead of G on one.  The counters run cumulatively through the launch
-// (`target` = all arrivals so far), zeroed by the host per call.  Every wave
-// drains its stores and atomics first; the poll reads every shard (sc1).
-QG_DEV void grid_barrier8(uint32_t* bar8, uint32_t target, uint32_t* err) {
-  drain_stores();
-  __syncthreads();
-  if (threadIdx.x == 0) {
-    __hip_atomic_fetch_add((gu32*)(bar8 + 32 * (blockIdx.x & 7)), 1u, __ATOMIC_RELAXED,
-                           __HIP_MEMORY_SCOPE_AGENT);
-    uint32_t spins = 0;
-    for (;;) {
-      uint32_t v[8], sum = 0;
-#pragma unroll
-      for (int x = 0; x < 8; x++) v[x] = ld_sc1_u32(bar8 + 32 * x);
-#pragma unroll
-      for (int x = 0; x < 8; x++) sum += v[x];
-      if (sum >= target) break;
-      __builtin_amdgcn_s_sleep(1);
-      if (++spins > (1u << 26)) {
-        st_sc1_u32(err, 1u);
-        break;
-      }
-    }
-    __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");  // no instruction: keeps loads below
-  }
-  __syncthreads();
-}
-
-// u64 sums of normalized 29-bit limbs (each sum < 2^40) -> the value mod p,
-// < 2p normalized.  T = L + c 2^261 with L < 2^261 and c < 4 when T is a sum
-// of fewer than 680 values < 2p; 2^261 = ONE (mod p), so T = L + c ONE < 173p.
-QG_DEV R29 limbsum29(const uint64_t* a) {
-  R29 x;
-  uint64_t c = 0;
-#pragma unroll
-  for (int i = 0; i < 9; i++) {
-    const uint64_t v = a[i] + c;
-    x.l[i] = (uint32_t)v & M29;
-    c = v >> 29;
-  }
-  x = normfull29<FrP>(add29(x, R29::from_l9(l9_mul_small(F29P<FrP>::ONE, (uint32_t)c))));
-  x = condsub29<FrP>(x, l9_mul_small(F29P<FrP>::P, 128));
-  return red128p(x);
-}
-
 static constexpr int SL_BLOCK = 256;
 // entries per slot of a block's slice in the first tail round (LDS: K slots x
 // 1.5 x SL_SMAX entries of 36 B: the slice and its half-size fold)
@@ -1829,6 +1863,15 @@ static uint32_t* sumcheck_bar8(uint32_t* bar, uint32_t nvars) {
   uint8_t* io = reinterpret_cast<uint8_t*>(bar) - sizeof(ScState);
   return reinterpret_cast<uint32_t*>(io + sumcheck_o_bar8(nvars));
 }
+// big-round limb accumulators (k_sc_big): [shard 8][16 points][9 limbs] u64;
+// round 0's in the io header after the barrier shards (zeroed per call),
+// round 1's in scratch; each round's last block clears the next round's
+static constexpr size_t SC_BACC_BYTES = 8 * 16 * 9 * sizeof(uint64_t);
+static size_t sumcheck_o_bacc0(uint32_t nvars) { return sumcheck_o_bar8(nvars) + 8 * 128; }
+static uint64_t* sumcheck_bacc0(uint32_t* bar, uint32_t nvars) {
+  uint8_t* io = reinterpret_cast<uint8_t*>(bar) - sizeof(ScState);
+  return reinterpret_cast<uint64_t*>(io + sumcheck_o_bacc0(nvars));
+}
 
 // The slice tail (k_sc_slice): G blocks, a power of two <= min(one per CU,
 // SMAX) so block 0 can gather one entry per block, each owning <= SMAX entries
@@ -1898,7 +1941,7 @@ static unsigned sc_big_blocks(qg_ctx* ctx, size_t npairs) {
 template <int K, int NP>
 static int launch_big(qg_ctx* ctx, const std::vector<const Fr*>& src, Fr* X, Fr* Y, size_t N,
                        uint32_t j, const SopDev* d_sp, SopHdr h, size_t npairs, RoundOut ro,
-                       int pending, Fr* partial, Fr* loc) {
+                       int pending, Fr* loc, uint64_t* a0, uint64_t* a1, uint32_t* bar8) {
   // rounds j >= 1: h(0) = h_{j-1}(r_{j-1}) - h(1), exact by construction (the
   // folded table's pair sums ARE the previous message at r); round 0 evaluates
   // every point, so a wrong caller claim still yields the reference's bytes.
@@ -1921,16 +1964,20 @@ static int launch_big(qg_ctx* ctx, const std::vector<const Fr*>& src, Fr* X, Fr*
   static const bool wpe4 = getenv("QG_SC_WPE") != nullptr;
   if (pure && wpe4)
     hipLaunchKernelGGL((k_sc_big<K, 4, true, false, 4>), dim3(blocks), dim3(SC_BLOCK), 0,
-                       ctx->stream, tb, j, d_sp, h, npairs, ro, pending, partial, loc, skip0);
+                       ctx->stream, tb, j, d_sp, h, npairs, ro, pending, loc, skip0, (j & 1) ? a1 : a0,
+                       (j & 1) ? a0 : a1, bar8);
   else if (pure && pf)
     hipLaunchKernelGGL((k_sc_big<K, 4, true, true>), dim3(blocks), dim3(SC_BLOCK), 0, ctx->stream,
-                       tb, j, d_sp, h, npairs, ro, pending, partial, loc, skip0);
+                       tb, j, d_sp, h, npairs, ro, pending, loc, skip0, (j & 1) ? a1 : a0,
+                       (j & 1) ? a0 : a1, bar8);
   else if (pure)
     hipLaunchKernelGGL((k_sc_big<K, 4, true, false>), dim3(blocks), dim3(SC_BLOCK), 0, ctx->stream,
-                       tb, j, d_sp, h, npairs, ro, pending, partial, loc, skip0);
+                       tb, j, d_sp, h, npairs, ro, pending, loc, skip0, (j & 1) ? a1 : a0,
+                       (j & 1) ? a0 : a1, bar8);
   else
     hipLaunchKernelGGL((k_sc_big<4, 4, false, false>), dim3(blocks), dim3(SC_BLOCK), 0, ctx->stream,
-                       tb, j, d_sp, h, npairs, ro, pending, partial, loc, skip0);
+                       tb, j, d_sp, h, npairs, ro, pending, loc, skip0, (j & 1) ? a1 : a0,
+                       (j & 1) ? a0 : a1, bar8);
   QG_LAUNCH_CHECK();
   return skip0;
 }
@@ -1948,6 +1995,9 @@ static uint32_t run_rounds(qg_ctx* ctx, uint32_t nvars, const std::vector<const 
   Fr* X = ctx->scratch_as<Fr>("sc_x", std::max<size_t>(1, (N / 2) * nslots));
   Fr* Y = ctx->scratch_as<Fr>("sc_y", std::max<size_t>(1, (N / 4) * nslots));
   Fr* partial = ctx->scratch_as<Fr>("sc_partial", (size_t)SC_MAX_BLOCKS * NP);
+  uint64_t* a0 = sumcheck_bacc0(bar, nvars);
+  uint64_t* a1 = reinterpret_cast<uint64_t*>(ctx->scratch_as<uint8_t>("sc_bacc1", SC_BACC_BYTES));
+  uint32_t* bar8 = sumcheck_bar8(bar, nvars);
   TablePtrs cur{};
   for (uint32_t i = 0; i < 8; i++) cur.src[i] = i < src.size() ? src[i] : nullptr;
   auto bufs = [&](Fr* base, size_t per) {
@@ -1978,7 +2028,8 @@ static uint32_t run_rounds(qg_ctx* ctx, uint32_t nvars, const std::vector<const 
         const TablePtrs& d = parity ? tY : tX;
         for (int i = 0; i < 8; i++) tp.dst[i] = d.dst[i];
       }
-      if (launch_big<K, NP>(ctx, src, X, Y, N, j, d_sp, h, npairs, ro, pending, partial, nullptr) < 0)
+      if (launch_big<K, NP>(ctx, src, X, Y, N, j, d_sp, h, npairs, ro, pending, nullptr, a0, a1,
+                            bar8) < 0)
         hipLaunchKernelGGL((k_sc_round<K, NP>), dim3(sc_round_blocks(ctx, npairs)), dim3(SC_BLOCK),
                            0, ctx->stream, tp, d_sp, h, npairs, fold, ro, j, pending, partial,
                            (Fr*)nullptr);
@@ -2068,6 +2119,9 @@ static uint32_t run_rounds_dist(qg_ctx* ctx, uint32_t nvars, const std::vector<c
   Fr* X = ctx->scratch_as<Fr>("sc_x", std::max<size_t>(1, (NL / 2) * std::max(nslots, 1u)));
   Fr* Y = ctx->scratch_as<Fr>("sc_y", std::max<size_t>(1, (NL / 4) * std::max(nslots, 1u)));
   Fr* partial = ctx->scratch_as<Fr>("sc_partial", (size_t)SC_MAX_BLOCKS * NP);
+  uint64_t* a0 = sumcheck_bacc0(bar, nvars);
+  uint64_t* a1 = reinterpret_cast<uint64_t*>(ctx->scratch_as<uint8_t>("sc_bacc1", SC_BACC_BYTES));
+  uint32_t* bar8 = sumcheck_bar8(bar, nvars);
   Fr* loc = ctx->scratch_as<Fr>("sc_loc", NP);
   Fr* all = ctx->scratch_as<Fr>("sc_all", (size_t)world * NP);
   TablePtrs cur{};
@@ -2088,7 +2142,7 @@ static uint32_t run_rounds_dist(qg_ctx* ctx, uint32_t nvars, const std::vector<c
         const TablePtrs& d = parity ? tY : tX;
         for (int i = 0; i < 8; i++) tp.dst[i] = d.dst[i];
       }
-      int skip0 = launch_big<K, NP>(ctx, src, X, Y, NL, j, d_sp, h, npairs, ro, 0, partial, loc);
+      int skip0 = launch_big<K, NP>(ctx, src, X, Y, NL, j, d_sp, h, npairs, ro, 0, loc, a0, a1, bar8);
       if (skip0 < 0) {
         skip0 = 0;
         hipLaunchKernelGGL((k_sc_round<K, NP>), dim3(sc_round_blocks(ctx, npairs)), dim3(SC_BLOCK),
@@ -2538,7 +2592,7 @@ static void sumcheck_run(qg_ctx* ctx, uint32_t nvars, uint32_t ntables,
   // one device region: ScState | barrier counters | chal | coeffs | final (8 slots +
   // evaluation) | lens.  ScState and the counters are (re)initialised per call.
   const size_t o_bar = sizeof(ScState);
-  const size_t o_chal = sumcheck_o_bar8(nvars) + 8 * 128;  // after the barrier shards
+  const size_t o_chal = sumcheck_o_bacc0(nvars) + SC_BACC_BYTES;  // after the accumulator
   const size_t o_coeffs = o_chal + sizeof(Fr) * nvars;
   const size_t o_final = o_coeffs + sizeof(Fr) * (size_t)nvars * width;
   const size_t o_lens = o_final + sizeof(Fr) * 9;
