@@ -1358,8 +1358,9 @@ template <int K, int NP>
 __global__ void __launch_bounds__(SL_BLOCK)
     k_sc_slice(TablePtrs tp0, TablePtrs gat, const SopDev* __restrict__ spg, SopHdr h,
                uint32_t nvars, uint32_t j0, int fold0, int pending0, RoundOut ro,
-               Fr* __restrict__ partial, uint32_t* __restrict__ bar8, uint64_t* __restrict__ acc64,
-               Fr* __restrict__ final_vals, Fr* __restrict__ evaluation) {
+               uint64_t* __restrict__ acc_j0, uint32_t* __restrict__ bar8,
+               uint64_t* __restrict__ acc64, Fr* __restrict__ final_vals,
+               Fr* __restrict__ evaluation) {
   constexpr uint32_t SMAX = sl_smax(K);
   __shared__ SopLds<NP> sp;
   __shared__ R29 Fbuf[K * SMAX * 3 / 2];
@@ -1375,6 +1376,7 @@ __global__ void __launch_bounds__(SL_BLOCK)
   const bool last_wave = tid >= SL_BLOCK - 64;
   // per-round limb accumulators of rounds > j0: [round - j0 - 1][shard 8][NP][9],
   // zeroed here by block 0 before it meets the others at round j0's barrier
+  // (round j0 adds into acc_j0, already clear)
   constexpr uint32_t ACC_R = 8 * NP * 9;
   if (blk == 0)
     for (uint32_t i = tid; i < (nvars - j0 - 1) * ACC_R; i += SL_BLOCK)
@@ -1430,14 +1432,16 @@ __global__ void __launch_bounds__(SL_BLOCK)
     if (blk == 0) SC_TR(16 * j + 1);
     tail_reduce<NP>(acc, std::min(items, ne), np, red, res);
     if (blk == 0) SC_TR(16 * j + 7);
-    if (G > 1 && j > j0) {
+    if (G > 1) {
       // limbs of the block sums added into this round's accumulator shard
       // (agent-scope u64 atomics at the memory side), one sharded barrier, then
       // every block fetches the 8 shards with returning atomics and rebuilds
-      // the sums: no partial rows, one memory round trip
-      uint64_t* ar = acc64 + (size_t)(j - j0 - 1) * ACC_R;
+      // the sums: no partial rows, one memory round trip.  Round j0 uses the
+      // big rounds' cleared slot (shard stride 16 x 9), later rounds acc64.
+      uint64_t* ar = j == j0 ? acc_j0 : acc64 + (size_t)(j - j0 - 1) * ACC_R;
+      const uint32_t ss = j == j0 ? 16 * 9 : NP * 9;
       if (tid < np * 9)
-        __hip_atomic_fetch_add((gu64*)(ar + (blk & 7) * NP * 9 + tid),
+        __hip_atomic_fetch_add((gu64*)(ar + (blk & 7) * ss + tid),
                                (uint64_t)res[tid / 9].l[tid % 9], __ATOMIC_RELAXED,
                                __HIP_MEMORY_SCOPE_AGENT);
       arrived += G;
@@ -1447,7 +1451,7 @@ __global__ void __launch_bounds__(SL_BLOCK)
         uint64_t v[8], a = 0;
 #pragma unroll
         for (int x = 0; x < 8; x++)
-          v[x] = __hip_atomic_fetch_add((gu64*)(ar + x * NP * 9 + tid), (uint64_t)0,
+          v[x] = __hip_atomic_fetch_add((gu64*)(ar + x * ss + tid), (uint64_t)0,
                                         __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
 #pragma unroll
         for (int x = 0; x < 8; x++) a += v[x];
@@ -1456,28 +1460,6 @@ __global__ void __launch_bounds__(SL_BLOCK)
       __syncthreads();
       if (tid < np) res[tid] = limbsum29(lsum + 9 * tid);
       __syncthreads();
-    } else if (G > 1) {
-      // round j0: partial rows (the accumulators are zeroed behind this barrier)
-      Fr* part = partial;
-      if (tid < np) st_sc1(part + (size_t)blk * NP + tid, from29(canon29(res[tid])));
-      arrived += G;
-      grid_barrier8(bar8, arrived, &ro.st->err);
-      if (blk == 0) SC_TR(16 * j + 8);
-      acc = R29::zero();
-      const uint32_t pl = tid / NP;
-      if (t < np)
-        for (uint32_t b0 = pl; b0 < G; b0 += 4 * (SL_BLOCK / NP)) {
-          Fr v[4];
-#pragma unroll
-          for (int k = 0; k < 4; k++) {
-            const uint32_t b = b0 + k * (SL_BLOCK / NP);
-            v[k] = b < G ? ld_sc1(part + (size_t)b * NP + t) : Fr::zero();
-          }
-#pragma unroll
-          for (int k = 0; k < 4; k++) acc = add29(acc, to29(v[k]));
-          acc = red6p(acc);
-        }
-      tail_reduce<NP>(acc, std::min<uint32_t>(G, SL_BLOCK / NP) * NP, np, red, res);
     }
     if (blk == 0) SC_TR(16 * j + 2);
     finish_core<NP>(sp, np, res, ro, j, fs, st, pend, nullptr, blk == 0 ? 16 * j : 4096, blk == 0,
@@ -1900,15 +1882,14 @@ static uint32_t slice_tail_log(qg_ctx* ctx, size_t cus) {
 // false: the caller launches k_sc_tail.
 template <int K, int NP>
 static bool launch_slice_tail(qg_ctx* ctx, size_t cus, TablePtrs t0, const SopDev* d_sp, SopHdr h,
-                              uint32_t nvars, uint32_t j0, int fold0,
-                              int pending0, RoundOut ro, uint32_t* bar, Fr* d_final, Fr* d_eval) {
+                              uint32_t nvars, uint32_t j0, int fold0, int pending0, RoundOut ro,
+                              uint32_t* bar, uint64_t* acc_j0, Fr* d_final, Fr* d_eval) {
   const size_t gm = slice_gmax<K, NP>(ctx, cus);
   if (!gm) return false;
   const size_t n0 = (size_t)1 << (nvars - j0);
   size_t G = 1;
   while (G * 2 <= gm && G * 2 <= n0 / 2) G *= 2;
   if (n0 / G > sl_smax(K)) return false;
-  Fr* ppart = ctx->scratch_as<Fr>("sc_spartial", (size_t)G * NP);
   uint64_t* acc64 = ctx->scratch_as<uint64_t>("sc_sacc", (size_t)std::max<uint32_t>(1, nvars - j0) * 8 * NP * 9);
   // the 8 barrier shards follow the per-round counters (zeroed by the per-call
   // header copy): sumcheck_bar8
@@ -1919,7 +1900,7 @@ static bool launch_slice_tail(qg_ctx* ctx, size_t cus, TablePtrs t0, const SopDe
   TablePtrs gat{};
   for (uint32_t i = 0; i < 8; i++) gat.dst[i] = i < h.nslots ? sg + (size_t)i * n0 : nullptr;
   hipLaunchKernelGGL((k_sc_slice<K, NP>), dim3((unsigned)G), dim3(SL_BLOCK), 0, ctx->stream, t0,
-                     gat, d_sp, h, nvars, j0, fold0, pending0, ro, ppart, bar8, acc64, d_final,
+                     gat, d_sp, h, nvars, j0, fold0, pending0, ro, acc_j0, bar8, acc64, d_final,
                      d_eval);
   QG_LAUNCH_CHECK();
   return true;
@@ -1998,6 +1979,12 @@ static uint32_t run_rounds(qg_ctx* ctx, uint32_t nvars, const std::vector<const 
   uint64_t* a0 = sumcheck_bacc0(bar, nvars);
   uint64_t* a1 = reinterpret_cast<uint64_t*>(ctx->scratch_as<uint8_t>("sc_bacc1", SC_BACC_BYTES));
   uint32_t* bar8 = sumcheck_bar8(bar, nvars);
+  // the staged round kernel does not clear the next accumulator slot: the
+  // tail's first slot is then cleared here when it is the scratch one
+  bool staged = false;
+  auto clear_tail_slot = [&](uint32_t j0) {
+    if (staged && (j0 & 1)) QG_HIP(hipMemsetAsync(a1, 0, SC_BACC_BYTES, ctx->stream));
+  };
   TablePtrs cur{};
   for (uint32_t i = 0; i < 8; i++) cur.src[i] = i < src.size() ? src[i] : nullptr;
   auto bufs = [&](Fr* base, size_t per) {
@@ -2029,10 +2016,12 @@ static uint32_t run_rounds(qg_ctx* ctx, uint32_t nvars, const std::vector<const 
         for (int i = 0; i < 8; i++) tp.dst[i] = d.dst[i];
       }
       if (launch_big<K, NP>(ctx, src, X, Y, N, j, d_sp, h, npairs, ro, pending, nullptr, a0, a1,
-                            bar8) < 0)
+                            bar8) < 0) {
         hipLaunchKernelGGL((k_sc_round<K, NP>), dim3(sc_round_blocks(ctx, npairs)), dim3(SC_BLOCK),
                            0, ctx->stream, tp, d_sp, h, npairs, fold, ro, j, pending, partial,
                            (Fr*)nullptr);
+        staged = true;
+      }
       QG_LAUNCH_CHECK();
       if (fold) {
         for (int i = 0; i < 8; i++) cur.src[i] = tp.dst[i];
@@ -2060,8 +2049,11 @@ static uint32_t run_rounds(qg_ctx* ctx, uint32_t nvars, const std::vector<const 
       bufA = b;
       bufB = a;
     }
+    // round j's accumulator slot was cleared by the last big round (or the
+    // per-call header when there is none)
+    clear_tail_slot(j);
     if (!launch_slice_tail<K, NP>(ctx, ctx->num_cus(), t0, d_sp, h, nvars, j, fold, pending, ro,
-                                  bar, d_final, d_eval)) {
+                                  bar, (j & 1) ? a1 : a0, d_final, d_eval)) {
       // persistent launch: one block per CU at most (co-residency for the grid
       // barrier), fewer when the first persistent round has fewer pair groups
       const size_t PB = tail_pb(h.nslots, NP);
@@ -2122,6 +2114,12 @@ static uint32_t run_rounds_dist(qg_ctx* ctx, uint32_t nvars, const std::vector<c
   uint64_t* a0 = sumcheck_bacc0(bar, nvars);
   uint64_t* a1 = reinterpret_cast<uint64_t*>(ctx->scratch_as<uint8_t>("sc_bacc1", SC_BACC_BYTES));
   uint32_t* bar8 = sumcheck_bar8(bar, nvars);
+  // the staged round kernel does not clear the next accumulator slot: the
+  // tail's first slot is then cleared here when it is the scratch one
+  bool staged = false;
+  auto clear_tail_slot = [&](uint32_t j0) {
+    if (staged && (j0 & 1)) QG_HIP(hipMemsetAsync(a1, 0, SC_BACC_BYTES, ctx->stream));
+  };
   Fr* loc = ctx->scratch_as<Fr>("sc_loc", NP);
   Fr* all = ctx->scratch_as<Fr>("sc_all", (size_t)world * NP);
   TablePtrs cur{};
@@ -2145,6 +2143,7 @@ static uint32_t run_rounds_dist(qg_ctx* ctx, uint32_t nvars, const std::vector<c
       int skip0 = launch_big<K, NP>(ctx, src, X, Y, NL, j, d_sp, h, npairs, ro, 0, loc, a0, a1, bar8);
       if (skip0 < 0) {
         skip0 = 0;
+        staged = true;
         hipLaunchKernelGGL((k_sc_round<K, NP>), dim3(sc_round_blocks(ctx, npairs)), dim3(SC_BLOCK),
                            0, ctx->stream, tp, d_sp, h, npairs, fold, ro, j, 0, partial, loc);
       }
@@ -2204,8 +2203,9 @@ static uint32_t run_rounds_dist(qg_ctx* ctx, uint32_t nvars, const std::vector<c
     // shares one device, so each persistent grid takes a 1/world share of the CUs
     const size_t cus = comm_is_loopback(ctx) ? std::max<size_t>(1, ctx->num_cus() / world)
                                              : (size_t)ctx->num_cus();
+    clear_tail_slot(js);
     if (!launch_slice_tail<K, NP>(ctx, cus, t0, d_sp, h, nvars, js, js >= 1 ? 1 : 0, 0, ro, bar,
-                                  d_final, d_eval)) {
+                                  (js & 1) ? a1 : a0, d_final, d_eval)) {
       const unsigned grid = (unsigned)std::max<size_t>(
           1, std::min<size_t>(persist_grid_cap<K, NP>(ctx, cus), (pairs0 + PB - 1) / PB));
       Fr* ppart = ctx->scratch_as<Fr>("sc_ppartial", (size_t)2 * grid * NP);
