@@ -131,7 +131,7 @@ struct SopDev {
   L9 cr29[4];                // 2^522, 2^778 (-> r * 2^261); 2^517, 2^773 (-> r * 2^256)
   Fr coeff[SOP_MAXM];        // Montgomery coefficients (final claim on the 32-bit path)
   uint8_t is_one[SOP_MAXM];  // (final claim)
-  L9 cs29;                   // 2^(261 - e): Montgomery value -> scale S (the round claim)
+  L9 cs29;                   // 2^(517 - e): canonical value -> scale S (the round claim)
 };
 static_assert(offsetof(SopDev, c29) == SOP_HDR_WORDS * 4, "SopDev layout");
 
@@ -670,7 +670,7 @@ __global__ void __launch_bounds__(SC_BLOCK)
     if (tid < NP) loc[tid] = tid < h.np ? from29(canon29(res[tid])) : Fr::zero();
     return;
   }
-  finish_core<NP>(sp, h.np, res, ro, j, fs, st_in, ro.st->pend, nullptr, tr);
+  finish_core<NP>(sp, h.np, res, ro, j, fs, st_in, ro.st->pend, nullptr, tr, true, true);
   if (tid < 9) ro.st->r29[tid] = fs.r.l[tid];
   SC_TR(tr + 7);
 }
@@ -969,7 +969,7 @@ __global__ void __launch_bounds__(SC_BLOCK) __attribute__((amdgpu_waves_per_eu(W
   }
   if (skip0 && blockIdx.x == 0 && tid == 128) {
     // this round's claim h_{j-1}(r_{j-1}) at scale S, for the finisher's
-    // h(0) = claim - h(1): Horner over round j-1's Montgomery coefficients
+    // h(0) = claim - h(1): Horner over round j-1's canonical coefficients
     // (wave 2 of block 0, beside the sweep; handed over write-through)
     const Fr* c = ro.coeffs + (size_t)(j - 1) * ro.width;
     R29 a = to29(c[h.np - 1]);
@@ -1047,7 +1047,7 @@ __global__ void __launch_bounds__(SC_BLOCK) __attribute__((amdgpu_waves_per_eu(W
   if (skip0 && tid == 0)
     res[0] = red6p(sub29(to29(ld_sc1(reinterpret_cast<const Fr*>(ro.st->claim))), res[1]));
   __syncthreads();
-  finish_core<NP>(sp, np, res, ro, j, fs, st_in, ro.st->pend, nullptr, tr);
+  finish_core<NP>(sp, np, res, ro, j, fs, st_in, ro.st->pend, nullptr, tr, true, true);
   if (tid < 9) ro.st->r29[tid] = fs.r.l[tid];
   SC_TR(tr + 7);
 }
@@ -1077,7 +1077,7 @@ __global__ void __launch_bounds__(SC_BLOCK)
   if (skip0 && tid == 0)  // h(0) = claim - h(1) on the global sums
     res[0] = red6p(sub29(to29(*reinterpret_cast<const Fr*>(ro.st->claim)), res[1]));
   __syncthreads();
-  finish_core<NP>(sp, h.np, res, ro, j, fs, st, nullptr, ro.st->state);
+  finish_core<NP>(sp, h.np, res, ro, j, fs, st, nullptr, ro.st->state, 4096, true, true);
   if (tid < 9) ro.st->r29[tid] = fs.r.l[tid];
 }
 
@@ -1791,7 +1791,7 @@ static std::shared_ptr<const ScProgram> get_program(const qg_expr_op* prog, size
   d.cr29[1] = l9_of(pow2_mod_plain<FrP>(778));
   d.cr29[2] = l9_of(pow2_mod_plain<FrP>(517));
   d.cr29[3] = l9_of(pow2_mod_plain<FrP>(773));
-  d.cs29 = l9_of(pow2_mod_plain<FrP>((uint32_t)(261 - e)));
+  d.cs29 = l9_of(pow2_mod_plain<FrP>((uint32_t)(517 - e)));
   bool pure = d.nmono == 1 && sp.is_one[0] && sp.mono_len[0] == d.nslots && d.nslots >= 2 &&
               d.nslots == sp.degree;
   for (uint32_t f = 0; pure && f < d.nfac; f++) pure = sp.fac[f] == f;
@@ -2639,9 +2639,10 @@ static void sumcheck_run(qg_ctx* ctx, uint32_t nvars, uint32_t ntables,
   memcpy(state, h.data(), 32);
   memcpy(round_lens, h.data() + o_lens, sizeof(uint32_t) * nvars);
   const Fr* hc = reinterpret_cast<const Fr*>(h.data() + o_coeffs);
-  // rows of the persistent tail hold canonical words (finish_core canon_out)
-  for (size_t i = 0; i < (size_t)nvars * width; i++)
-    fr_export(i / width >= tail0 ? to_mont(hc[i]) : hc[i], round_coeffs + 4 * i);
+  // every round kernel writes canonical words (finish_core canon_out): the
+  // Montgomery pass after the challenge stays off the device's critical path
+  (void)tail0;
+  for (size_t i = 0; i < (size_t)nvars * width; i++) fr_export(to_mont(hc[i]), round_coeffs + 4 * i);
   const Fr* hp = reinterpret_cast<const Fr*>(h.data() + o_chal);
   for (uint32_t i = 0; i < nvars; i++) fr_export(hp[i], point + 4 * i);
   fr_export(reinterpret_cast<const Fr*>(h.data() + o_final)[8], evaluation);
