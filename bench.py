@@ -45,6 +45,9 @@ def parse():
     ap.add_argument("--steps", type=int, default=5)
     ap.add_argument("--warmup", type=int, default=2)
     ap.add_argument("--log-msm", type=int, default=24)
+    ap.add_argument("--log-msm-small", type=int, default=20,
+                    help="config 2: a resident 2^k MSM with its own SRS (window size chosen "
+                         "for 2^k), commitment checked (0: skip)")
     ap.add_argument("--log-sumcheck", type=int, default=20)
     ap.add_argument("--no-sumcheck", action="store_true")
     ap.add_argument("--log-mle", type=int, default=22,
@@ -74,7 +77,13 @@ def parse():
     return ap.parse_args()
 
 
-SC_KERNELS = ("k_sc_big", "k_sc_round", "k_sc_persist", "k_sc_finish")
+SC_KERNELS = ("k_sc_big", "k_sc_round", "k_sc_persist", "k_sc_finish", "k_sc_slice", "k_sc_tail")
+# qg_trace_marker tags: an empty kernel of `tag` work-groups at the start of each
+# leg lets profiles/kstats.py --legs and pmc_traffic.py attribute every dispatch
+# to its leg (kernels of one grid shape recur across legs)
+LEG_TAGS = {"msm_2p24": 1, "sumcheck": 2, "msm_host": 3, "scaling": 4, "mle_open": 5, "logup": 6,
+            "hyperplonk": 7, "msm_2p20": 8, "cpu_baseline": 9, "probe_msm": 10,
+            "probe_sumcheck": 11, "probe_logup": 12, "probe_mle": 13, "probe_cal": 14}
 
 
 def traffic_probe(args):
@@ -85,16 +94,19 @@ def traffic_probe(args):
     n = 1 << args.log_msm
     srs = q.Srs.generate(dev, TAU, n)
     scalars = q.DeviceVec(dev, n).fill_random(0x5155494C4C + 2)
+    dev.trace_marker(LEG_TAGS["probe_msm"])
     srs.msm_dev(scalars)
     srs.close()
     scalars.close()
     # FETCH_SIZE calibration launches: known counts of random 128-B row gathers
     # (the accumulate's pattern) and of 16-B-per-lane streaming bytes
     import pmc_traffic
+    dev.trace_marker(LEG_TAGS["probe_cal"])
     dev.microbench_fetch(pmc_traffic.CAL_ROWS, pmc_traffic.CAL_GATHERS)
     if not args.no_sumcheck:
         N = 1 << args.log_sumcheck
         tabs = [q.DeviceVec(dev, N).fill_random(0x5155494C4C + 3 + 7 * i) for i in range(3)]
+        dev.trace_marker(LEG_TAGS["probe_sumcheck"])
         sumcheck_prove_device(dev, args.log_sumcheck, tabs, E.Input(0) * E.Input(1) * E.Input(2),
                               0, q.Transcript(b"sumcheck_bench"))
         for t in tabs:
@@ -104,6 +116,7 @@ def traffic_probe(args):
         n = 1 << args.log_logup
         tabs = [q.DeviceVec(dev, n).fill_random(0x5155494C4C + 5 + 11 * i) for i in range(3)]
         out = q.DeviceVec(dev, n)
+        dev.trace_marker(LEG_TAGS["probe_logup"])
         logup_column_device(dev, args.log_logup, tabs, E.Input(0) + E.Const(LOGUP_A) * E.Input(1),
                             LOGUP_BETA, out, E.Input(2))
         for t in tabs + [out]:
@@ -114,6 +127,7 @@ def traffic_probe(args):
         n = 1 << args.log_mle
         kzg = KZG(dev, q.Srs.generate(dev, TAU, n), n - 1)
         poly = q.DeviceVec(dev, n).fill_random(0x5155494C4C + 4)
+        dev.trace_marker(LEG_TAGS["probe_mle"])
         C = kzg.srs.msm_dev(poly)
         t = Transcript(b"MLPCS bench")
         t.append_g1(C)
@@ -181,6 +195,27 @@ def _free_port():
     return p
 
 
+def setup_rank(q, rank, world, local_rank):
+    """One rank's device and communicators, in this order: the torch process
+    group over RCCL on cuda:local_rank (barriers, max-over-ranks, the id
+    broadcast), then the library context on the SAME device, then rank 0's
+    ncclUniqueId broadcast through torch and the library's own RCCL
+    communicator attached with it (qg_ctx_attach_comm).  Returns (dev, dist):
+    dist is torch.distributed, or None at world 1."""
+    dist = None
+    if world > 1:
+        import torch
+        import torch.distributed as dist
+        torch.cuda.set_device(local_rank)
+        dist.init_process_group("nccl", device_id=torch.device("cuda", local_rank))
+    dev = q.Device(local_rank)
+    if world > 1:
+        obj = [q.Device.comm_unique_id() if rank == 0 else None]
+        dist.broadcast_object_list(obj, src=0)
+        dev.attach_comm(rank, world, obj[0])
+    return dev, dist
+
+
 def main():
     args = parse()
     if args.traffic_probe:
@@ -202,14 +237,11 @@ def main():
     traffic = None
     if world == 1 and not args.no_traffic:
         traffic = measure_traffic(args)  # child processes, before this one touches the GPU
-    dist = None
-    if world > 1:
-        import torch
-        import torch.distributed as dist
-        torch.cuda.set_device(local_rank)
-        dist.init_process_group("nccl", device_id=torch.device("cuda", local_rank))
-
     import quill_amd as q
+    dev, dist = setup_rank(q, rank, world, local_rank)
+    if dev.world != args.gpus:
+        print(f"bench.py: communicator world {dev.world} != --gpus {args.gpus}", file=sys.stderr)
+        return 2
 
     def barrier_sync():
         if dist is not None:
@@ -225,15 +257,6 @@ def main():
         dist.all_reduce(t, op=dist.ReduceOp.MAX)
         return float(t.item())
 
-    dev = q.Device(local_rank)
-    if world > 1:
-        import torch.distributed as tdist
-        obj = [q.Device.comm_unique_id() if rank == 0 else None]
-        tdist.broadcast_object_list(obj, src=0)
-        dev.attach_comm(rank, world, obj[0])
-    if dev.world != args.gpus:
-        print(f"bench.py: communicator world {dev.world} != --gpus {args.gpus}", file=sys.stderr)
-        return 2
 
     n = 1 << args.log_msm
     _progress(rank, f"SRS generation 2^{args.log_msm}")
@@ -243,6 +266,7 @@ def main():
     setup_s = time.perf_counter() - t0
 
     _progress(rank, "MSM headline")
+    dev.trace_marker(LEG_TAGS["msm_2p24"])
     for _ in range(args.warmup):
         srs.msm_dev(scalars)
     dev.enable_timing(True)
@@ -324,17 +348,24 @@ def main():
         out["pmc"] = traffic
     if not args.no_sumcheck:
         _progress(rank, "sumcheck")
+        dev.trace_marker(LEG_TAGS["sumcheck"])
         out["sumcheck"] = bench_sumcheck(q, dev, args, barrier_sync, max_over_ranks, rank)
         if traffic is not None and "error" not in traffic:
             tot = sum((traffic[k]["read_bytes_per_launch"] + traffic[k]["write_bytes_per_launch"])
                       * traffic[k]["launches"] for k in SC_KERNELS if k in traffic)
             out["sumcheck"]["roofline"]["traffic"] = tot
+    if args.log_msm_small > 0:
+        _progress(rank, f"MSM 2^{args.log_msm_small} (config 2)")
+        dev.trace_marker(LEG_TAGS["msm_2p20"])
+        out["msm_2p20"] = bench_msm_small(q, dev, args, barrier_sync, max_over_ranks, rank, world)
     if args.host_input:
         _progress(rank, "MSM from host memory")
+        dev.trace_marker(LEG_TAGS["msm_host"])
         out["msm_host_input"] = bench_msm_host(q, dev, args, barrier_sync, max_over_ranks, srs,
                                                scalars, ms_per_step, res)
     if not args.no_scaling_modes:
         _progress(rank, "scaling modes")
+        dev.trace_marker(LEG_TAGS["scaling"])
         out["msm_strong_scaling"] = bench_msm_strong(q, dev, args, barrier_sync, max_over_ranks,
                                                      rank, world, srs if world == 1 else None,
                                                      scalars if world == 1 else None)
@@ -343,17 +374,21 @@ def main():
                                                           max_over_ranks, rank, weak=True)
     if args.log_mle > 0:
         _progress(rank, "ML-PCS open")
+        dev.trace_marker(LEG_TAGS["mle_open"])
         out["mle_open"] = bench_mle(q, dev, args, barrier_sync, max_over_ranks, rank, world)
     if args.log_logup > 0:
         _progress(rank, "Logup")
+        dev.trace_marker(LEG_TAGS["logup"])
         out["logup"] = bench_logup(q, dev, args, barrier_sync, max_over_ranks, rank, world,
                                    traffic)
     if args.log_hp_rows > 0:
         _progress(rank, "HyperPlonk")
+        dev.trace_marker(LEG_TAGS["hyperplonk"])
         out["hyperplonk"] = bench_hyperplonk(q, dev, args, barrier_sync, max_over_ranks, rank,
                                              world)
     if rank == 0 and not args.no_cpu_baseline:
         _progress(rank, "CPU baselines")
+        dev.trace_marker(LEG_TAGS["cpu_baseline"])
         out["cpu_baseline"] = cpu_baseline(args, srs, scalars)
         if not args.no_sumcheck:
             out["sumcheck"]["cpu_baseline"] = cpu_baseline_sumcheck(args)
@@ -378,8 +413,8 @@ LINE_MAX_BYTES = 6000
 _DROP_KEYS = {"note", "traffic_note", "frac_note", "issue_bound_note", "identity", "pmc",
               "commitment_check", "final_transcript_state", "cpu_model", "metric_note"}
 # sections dropped (in this order) if the line is still over budget
-_SHED_ORDER = ("hbm_by_kernel", "kernels_ms", "sumcheck_weak_scaling", "logup", "mle_open",
-               "hyperplonk", "msm_host_input", "msm_strong_scaling")
+_SHED_ORDER = ("kernels_ms", "sumcheck_weak_scaling", "msm_strong_scaling", "msm_host_input",
+               "logup", "mle_open", "hyperplonk", "hbm_by_kernel")
 
 
 def _sig(x, digits=4):
@@ -403,13 +438,15 @@ def _shrink(v, depth=0):
     return _sig(v)
 
 
-def hbm_by_kernel(pmc, top=12):
-    """{kernel: [GB/s, fraction of 8 TB/s, avg us]} for the `top` kernels of the
-    PMC probe by total time (whole-kernel keys, not per-shape)"""
+def hbm_by_kernel(pmc, top=8):
+    """{kernel#leg: [GB/s, fraction of 8 TB/s, avg us]} for the `top` kernels of
+    the PMC probe by total time (per probe leg: probe_msm is the headline MSM)"""
     if not isinstance(pmc, dict) or "error" in pmc:
         return None
+    sel = "#" if any("#" in k for k in pmc) else None  # older probes: whole-kernel keys
     rows = [(k, d) for k, d in pmc.items()
-            if not k.startswith("_") and "@" not in k and isinstance(d, dict) and "hbm_gbps" in d]
+            if not k.startswith("_") and isinstance(d, dict) and "hbm_gbps" in d
+            and (("#" in k) if sel else ("@" not in k))]
     rows.sort(key=lambda kd: -kd[1]["avg_us"] * kd[1].get("launches", 1))
     return {k: [_sig(d["hbm_gbps"], 3), _sig(d["frac_hbm_peak"], 3), _sig(d["avg_us"], 4)]
             for k, d in rows[:top]}
@@ -468,6 +505,41 @@ def bench_msm_host(q, dev, args, barrier_sync, max_over_ranks, srs, scalars, res
             if ms > resident_ms else None,
             "matches_resident_commitment": got == res,
             "note": "pageable host scalars -> qg_kzg_commit; value is never the headline"}
+
+
+def bench_msm_small(q, dev, args, barrier_sync, max_over_ranks, rank, world):
+    """BASELINE config 2: Pippenger G1 MSM at 2^k BN254 scalars per GPU
+    (kzg.rs:61-73), with an SRS generated for 2^k bases (so the window size is
+    the one msm_window_bits picks for 2^k, not the headline's), inputs resident;
+    the commitment is checked against the trapdoor identity after the clock."""
+    n = 1 << args.log_msm_small
+    srs = q.Srs.generate(dev, TAU, n, offset=rank * n)
+    scalars = q.DeviceVec(dev, n).fill_random(0x5155494C4C + 20 + rank)
+    steps = max(args.steps, 5)
+    for _ in range(max(args.warmup, 2)):
+        srs.msm_dev(scalars)
+    barrier_sync()
+    t0 = time.perf_counter()
+    for _ in range(steps):
+        res = srs.msm_dev(scalars)
+    barrier_sync()
+    dt = max_over_ranks(time.perf_counter() - t0)
+    dev.enable_timing(True)
+    for _ in range(steps):
+        srs.msm_dev(scalars)
+    parts = {nm: dev.kernel_time(nm)[0] / steps
+             for nm in ("msm_bucketing", "msm_accumulate", "msm_reduce")}
+    dev.enable_timing(False)
+    c_bits, n_win = srs.window_info()
+    ver = verify_commitment(scalars, res, n, rank, world)
+    srs.close()
+    scalars.close()
+    ms = dt / steps * 1e3
+    return {"metric": f"G1 MSM scalars/s at 2^{args.log_msm_small} BN254 scalars per GPU "
+                      "(BASELINE config 2)",
+            "value": world * n / (ms * 1e-3), "unit": "scalars/s", "ms": ms, "steps": steps,
+            "window_bits": c_bits, "windows": n_win, "parts_ms": parts,
+            "commitment_verified": ver["ok"], "scaling": "weak"}
 
 
 def bench_msm_strong(q, dev, args, barrier_sync, max_over_ranks, rank, world, srs=None,
@@ -557,7 +629,7 @@ def bench_mle(q, dev, args, barrier_sync, max_over_ranks, rank=0, world=1):
     evaluations, point drawn from the transcript after absorbing the commitment
     (the mlpcs.rs:258-267 pattern).  With N ranks the 2^k evaluations and the SRS
     are sharded (rank r holds [r 2^k/N, (r+1) 2^k/N)): eq/dot/quotients and all
-    six MSMs sharded, S polynomial replicated (strong scaling)."""
+    six MSMs sharded, the S polynomial split by frequency residue (strong scaling)."""
     from quill_amd import KZG, Transcript
     k = args.log_mle
     n = 1 << k
@@ -592,7 +664,7 @@ def bench_mle(q, dev, args, barrier_sync, max_over_ranks, rank=0, world=1):
             "ms": dt / steps * 1e3, "higher_is_better": False, "msms_per_step": 6,
             "parts_ms_rank0": parts, "steps": steps,
             "sharding": f"2^{k} evaluations over {world} rank(s) (strong scaling); "
-                        "S polynomial replicated",
+                        "S polynomial split by frequency residue (one all-to-all)",
             "note": "6 MSMs (commit, S commitment, 4 KZG quotients) dominate"}
 
 
@@ -793,6 +865,9 @@ def _headline_traffic(traffic):
     k_msm_accumulate launch shape (the 2^log-msm MSM runs first)"""
     if not traffic or "error" in traffic:
         return None
+    leg = traffic.get("k_msm_accumulate#probe_msm")
+    if leg and "read_bytes_per_launch" in leg:  # the probe's headline MSM, by its marker
+        return (leg["read_bytes_per_launch"] + leg["write_bytes_per_launch"]) * leg["launches"]
     shapes = [k for k in traffic if k.startswith("k_msm_accumulate@")]
     if not shapes:
         return _kernel_traffic(traffic, "k_msm_accumulate")
@@ -808,10 +883,12 @@ def _headline_traffic_row_calibrated(traffic):
     cal = (traffic or {}).get("_fetch_calibration")
     if not cal or "error" in traffic:
         return None
-    shapes = [k for k in traffic if k.startswith("k_msm_accumulate@")]
-    if not shapes:
-        return None
-    d = traffic[max(shapes, key=lambda k: int(k.split("@")[1]))]
+    d = traffic.get("k_msm_accumulate#probe_msm")
+    if not d or "read_bytes_per_launch" not in d:
+        shapes = [k for k in traffic if k.startswith("k_msm_accumulate@")]
+        if not shapes:
+            return None
+        d = traffic[max(shapes, key=lambda k: int(k.split("@")[1]))]
     return ((d["read_bytes_per_launch"] * cal["gather_read_factor"] + d["write_bytes_per_launch"])
             * max(d.get("launches", 1), 1))
 

@@ -61,7 +61,14 @@ const char* qg_version(void);
  * qg_sumcheck_prove treats its tables as the rank's block of the hypercube
  * (high index bits = rank). */
 int qg_comm_unique_id(uint8_t out_id[128]);
+/* world == 1 detaches (plain single-GPU paths) unless QG_FORCE_RCCL=1 is set:
+ * then a real one-rank RCCL communicator is attached (unique_id may be NULL)
+ * and the sharded code paths run through it — a test switch so a 1-GPU box
+ * executes the RCCL transport. */
 int qg_ctx_attach_comm(qg_ctx* ctx, int rank, int world, const uint8_t unique_id[128]);
+/* What the context exchanges through: 0 none (single GPU), 1 the in-process
+ * loopback, 2 an RCCL communicator.  `sharded` = 1 when the sharded paths run. */
+int qg_ctx_comm_info(const qg_ctx* ctx, int* kind, int* rank, int* world, int* sharded);
 /* In-process loopback group: `world` contexts, each driven by its own host
  * thread (possibly on one device), exchange through device-to-device copies
  * instead of RCCL.  Exercises every sharded path on a single GPU. */
@@ -73,6 +80,10 @@ int qg_ctx_attach_loopback(qg_ctx* ctx, qg_loopback* lb, int rank);
  * order) over the attached communicator: the host-side agreement steps of the
  * sharded prover (constraint-check verdicts, boundary rows). */
 int qg_comm_allgather_host(qg_ctx* ctx, const void* send, size_t bytes, void* recv);
+/* Personalised exchange of host bytes: send holds world chunks of `bytes` (chunk d
+ * goes to rank d), recv receives world chunks (chunk s came from rank s); the
+ * collective the sharded S polynomial uses (grouped RCCL send/recv). */
+int qg_comm_alltoall_host(qg_ctx* ctx, const void* send, size_t bytes, void* recv);
 /* The full witness of a trace, concat(columns) (hyperplonk/src/proof/proof.rs:270),
  * as this rank's block: every rank passes its row block (rows / world entries)
  * of each of the `ncols` columns and receives entries
@@ -378,6 +389,11 @@ int qg_microbench_fq_mul(qg_ctx* ctx, double* mul_per_s);
 int qg_microbench_fetch(qg_ctx* ctx, size_t rows, size_t gathers, double* gather_ms,
                         double* stream_ms);
 int qg_ctx_kernel_time(const qg_ctx* ctx, const char* name, double* total_ms, uint32_t* launches);
+/* Profiling marker: launches an empty kernel (k_trace_marker) of `tag` work-groups
+ * on the context stream, so a rocprofv3 kernel trace can be cut into the
+ * caller's phases (profiles/kstats.py --legs groups dispatches by the last
+ * marker).  No other effect. */
+int qg_trace_marker(qg_ctx* ctx, uint32_t tag);
 /* Self-test of the binary-GCD field inversion the Logup column uses per block
  * (csrc/bingcd.h): out[i] = in[i]^-1 (plain canonical integers, 4 x u64 LE;
  * 0 -> 0) in Fr (field = 0) or Fq (field = 1), on the host (ctx may be NULL)

@@ -44,6 +44,26 @@ def _short(name):
     return n.split("::")[-1].split("<")[0]
 
 
+# leg markers of the probe (bench.py traffic_probe: qg_trace_marker(tag), an
+# empty kernel of `tag` 64-lane work-groups); profiles/kstats.py has the same map
+MARKER = "k_trace_marker"
+LEGS = {10: "probe_msm", 11: "probe_sumcheck", 12: "probe_logup", 13: "probe_mle",
+        14: "probe_cal"}
+
+
+def _leg_keys(rows):
+    """[(row, leg)] for (dispatch, kernel, ..., grid work-items) rows in dispatch
+    order, markers dropped: a dispatch belongs to the last marker's leg"""
+    leg, out = "pre", []
+    for r in sorted(rows, key=lambda r: r[0]):
+        if r[1] == MARKER:
+            tag = r[-1] // 64
+            leg = LEGS.get(tag, f"tag{tag}")
+            continue
+        out.append((r, leg))
+    return out
+
+
 def kernel_durations(probe_args, timeout=300):
     """{kernel: (launches, average duration in us)} from a kernel-trace-only pass
     of the same probe (no counters: clean per-launch durations)"""
@@ -58,16 +78,18 @@ def kernel_durations(probe_args, timeout=300):
         if p.returncode != 0:
             raise RuntimeError(f"rocprofv3 --kernel-trace exited {p.returncode}: "
                                + p.stdout.decode(errors="replace")[-800:])
-        acc = {}
+        acc, rows = {}, []
         for f in glob.glob(os.path.join(outdir, "**", "*kernel_trace.csv"), recursive=True):
             with open(f) as fh:
                 for r in csv.DictReader(fh):
-                    k = _short(r["Kernel_Name"])
                     d = (int(r["End_Timestamp"]) - int(r["Start_Timestamp"])) / 1e3
-                    for key in (k, f"{k}@{r['Grid_Size_X']}"):
-                        a = acc.setdefault(key, [0, 0.0])
-                        a[0] += 1
-                        a[1] += d
+                    rows.append((int(r.get("Dispatch_Id") or r["Start_Timestamp"]),
+                                 _short(r["Kernel_Name"]), d, int(r["Grid_Size_X"])))
+        for (_, k, d, g), leg in _leg_keys(rows):
+            for key in (k, f"{k}@{g}", f"{k}#{leg}"):
+                a = acc.setdefault(key, [0, 0.0])
+                a[0] += 1
+                a[1] += d
         return {k: (n, t / n) for k, (n, t) in acc.items()}
     finally:
         shutil.rmtree(outdir, ignore_errors=True)
@@ -127,14 +149,18 @@ def collect(probe_args, timeout=300):
     fetch = run_pass("FETCH_SIZE", probe_args, timeout)
     write = run_pass("WRITE_SIZE", probe_args, timeout)
     out = {}
-    # per kernel, and per kernel@grid (one launch shape = one problem size)
-    for rows, key, fac in ((fetch, "read_bytes", FETCH_FACTOR), (write, "write_bytes", WRITE_FACTOR)):
-        for _, k, v, g in rows:
-            for kk in (k, f"{k}@{g}"):
+    # per kernel, per kernel@grid (one launch shape = one problem size) and per
+    # kernel#leg (the probe phase, from its markers)
+    fetch_l, write_l = _leg_keys(fetch), _leg_keys(write)
+    for rows, key, fac in ((fetch_l, "read_bytes", FETCH_FACTOR),
+                           (write_l, "write_bytes", WRITE_FACTOR)):
+        for (_, k, v, g), leg in rows:
+            for kk in (k, f"{k}@{g}", f"{k}#{leg}"):
                 d = out.setdefault(kk, {"launches": 0, "read_bytes": 0.0, "write_bytes": 0.0})
                 d[key] += v * fac
-    for k, d in out.items():
-        d["launches"] = sum(1 for _, kk, _, g in fetch if kk == k or f"{kk}@{g}" == k)
+    for (_, k, _, g), leg in fetch_l:
+        for kk in (k, f"{k}@{g}", f"{k}#{leg}"):
+            out[kk]["launches"] += 1
     for d in out.values():
         if "read_bytes" not in d:
             continue

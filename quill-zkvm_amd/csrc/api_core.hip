@@ -154,6 +154,10 @@ __global__ void k_first_mismatch(const Fr* a, const Fr* b, size_t n, unsigned lo
   if (!eq) atomicMin(first, (unsigned long long)i);
 }
 
+// profiling marker (qg_trace_marker): no work, only a dispatch whose grid
+// size carries the caller's tag into the kernel trace
+__global__ void k_trace_marker() {}
+
 }  // namespace qg
 
 extern "C" {
@@ -214,6 +218,15 @@ int qg_ctx_kernel_time(const qg_ctx* ctx, const char* name, double* total_ms, ui
   if (total_ms) *total_ms = it == ctx->ktime.end() ? 0.0 : it->second.first;
   if (launches) *launches = it == ctx->ktime.end() ? 0 : it->second.second;
   return QG_OK;
+}
+
+int qg_trace_marker(qg_ctx* ctx, uint32_t tag) {
+  if (!ctx || tag == 0) return QG_ERR_INVALID;
+  return qg_guard(ctx, [&] {
+    QG_HIP(hipSetDevice(ctx->device));
+    hipLaunchKernelGGL(k_trace_marker, dim3(tag), dim3(64), 0, ctx->stream);
+    QG_LAUNCH_CHECK();
+  });
 }
 
 // ---- transcript -----------------------------------------------------------

@@ -8,6 +8,7 @@
 //    bits; one allgather of the (d+1) round sums per round.
 //  * ML-PCS opening: the S polynomial's transform is split by frequency
 //    residue; one all-to-all delivers every rank its slice of S.
+#include <stdlib.h>
 #include <string.h>
 
 #include <condition_variable>
@@ -60,7 +61,7 @@ namespace qg {
   } while (0)
 
 void comm_allgather_bytes(qg_ctx* ctx, const void* d_send, void* d_recv, size_t bytes) {
-  if (ctx->world <= 1) {
+  if (!ctx->sharded) {
     QG_HIP(hipMemcpyAsync(d_recv, d_send, bytes, hipMemcpyDeviceToDevice, ctx->stream));
     return;
   }
@@ -86,7 +87,7 @@ void comm_allgather_bytes(qg_ctx* ctx, const void* d_send, void* d_recv, size_t 
 // grouped point-to-point send/recv over xGMI (no reduction: the payload is
 // field elements, which RCCL cannot add); loopback: device copies.
 void comm_alltoall_bytes(qg_ctx* ctx, const void* d_send, void* d_recv, size_t bytes) {
-  if (ctx->world <= 1) {
+  if (!ctx->sharded) {
     QG_HIP(hipMemcpyAsync(d_recv, d_send, bytes, hipMemcpyDeviceToDevice, ctx->stream));
     return;
   }
@@ -147,7 +148,7 @@ static std::vector<TraceChunk> trace_chunks(uint32_t ncols, size_t rows, int wor
 void trace_full_witness(qg_ctx* ctx, const std::vector<const Fr*>& cols, size_t rows, Fr* full) {
   const uint32_t ncols = (uint32_t)cols.size();
   const int world = ctx->world, rank = ctx->rank;
-  if (world <= 1) {
+  if (!ctx->sharded) {
     for (uint32_t c = 0; c < ncols; c++)
       QG_HIP(hipMemcpyAsync(full + (size_t)c * rows, cols[c], rows * sizeof(Fr),
                             hipMemcpyDeviceToDevice, ctx->stream));
@@ -183,7 +184,10 @@ void comm_release(qg_ctx* ctx) {
   if (ctx->comm->comm) (void)ncclCommDestroy(ctx->comm->comm);
   delete ctx->comm;  // a loopback group is owned by its creator
   ctx->comm = nullptr;
+  ctx->sharded = false;
 }
+
+bool comm_is_rccl(const qg_ctx* ctx) { return ctx->comm && ctx->comm->comm; }
 
 }  // namespace qg
 
@@ -212,13 +216,23 @@ int qg_ctx_attach_comm(qg_ctx* ctx, int rank, int world, const uint8_t unique_id
     }
     ctx->rank = 0;
     ctx->world = 1;
-    ctx->rank = rank;
-    ctx->world = world;
-    if (world == 1) return;
+    ctx->sharded = false;
+    // QG_FORCE_RCCL=1 (test switch): a world-1 context still attaches a real
+    // one-rank RCCL communicator and takes the sharded paths, so a 1-GPU box
+    // executes ncclCommInitRank / ncclAllGather / grouped ncclSend+ncclRecv
+    const char* force = getenv("QG_FORCE_RCCL");
+    const bool forced = world == 1 && force && force[0] && strcmp(force, "0") != 0;
+    if (world == 1 && !forced) return;
     ncclUniqueId id;
-    memcpy(&id, unique_id, 128);
+    if (unique_id)
+      memcpy(&id, unique_id, 128);
+    else
+      QG_NCCL(ncclGetUniqueId(&id));
     ctx->comm = new qg_comm_state();
     QG_NCCL(ncclCommInitRank(&ctx->comm->comm, world, id, rank));
+    ctx->rank = rank;
+    ctx->world = world;
+    ctx->sharded = true;
   });
 }
 
@@ -234,6 +248,29 @@ int qg_comm_allgather_host(qg_ctx* ctx, const void* send, size_t bytes, void* re
                           ctx->stream));
     ctx->sync();
   });
+}
+
+int qg_comm_alltoall_host(qg_ctx* ctx, const void* send, size_t bytes, void* recv) {
+  if (!ctx || (!send && bytes) || (!recv && bytes)) return QG_ERR_INVALID;
+  return qg_guard(ctx, [&] {
+    if (bytes == 0) return;
+    QG_HIP(hipSetDevice(ctx->device));
+    const size_t all = bytes * (size_t)ctx->world;
+    uint8_t* d = ctx->scratch_as<uint8_t>("a2a_host", 2 * all);
+    QG_HIP(hipMemcpyAsync(d, send, all, hipMemcpyHostToDevice, ctx->stream));
+    comm_alltoall_bytes(ctx, d, d + all, bytes);
+    QG_HIP(hipMemcpyAsync(recv, d + all, all, hipMemcpyDeviceToHost, ctx->stream));
+    ctx->sync();
+  });
+}
+
+int qg_ctx_comm_info(const qg_ctx* ctx, int* kind, int* rank, int* world, int* sharded) {
+  if (!ctx) return QG_ERR_INVALID;
+  if (kind) *kind = !ctx->comm ? 0 : ctx->comm->lb ? 1 : ctx->comm->comm ? 2 : 0;
+  if (rank) *rank = ctx->rank;
+  if (world) *world = ctx->world;
+  if (sharded) *sharded = ctx->sharded ? 1 : 0;
+  return QG_OK;
 }
 
 int qg_trace_full_witness(qg_ctx* ctx, const qg_buf* const* col_blocks, uint32_t ncols,
@@ -283,6 +320,7 @@ int qg_ctx_attach_loopback(qg_ctx* ctx, qg_loopback* lb, int rank) {
     ctx->comm->lb = lb;
     ctx->rank = rank;
     ctx->world = lb->world;
+    ctx->sharded = true;  // a one-rank group too: the sharded paths at world 1
   });
 }
 

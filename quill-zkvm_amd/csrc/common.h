@@ -64,6 +64,10 @@ struct qg_ctx {
   // RCCL
   qg_comm_state* comm = nullptr;
   int rank = 0, world = 1;
+  // the sharded code paths run (and exchange through the communicator): world > 1,
+  // or a one-rank group (a world-1 loopback, or the one-rank RCCL communicator
+  // QG_FORCE_RCCL=1 attaches so a 1-GPU box executes the RCCL transport)
+  bool sharded = false;
 
   int cus = 0;  // compute units of `device` (cached)
   int num_cus() {

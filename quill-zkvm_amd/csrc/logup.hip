@@ -618,7 +618,7 @@ static Fr logup_total(qg_ctx* ctx, const Fr* d_res, const uint32_t* d_err) {
   } mine{h.res, h.err, {}};
   Fr total = Fr::zero();
   uint32_t any_err = 0;
-  if (ctx->world > 1) {
+  if (ctx->sharded) {
     uint8_t* d_g = ctx->scratch_as<uint8_t>("lg_gather", sizeof(mine) * (ctx->world + 1));
     QG_HIP(hipMemcpyAsync(d_g, &mine, sizeof(mine), hipMemcpyHostToDevice, ctx->stream));
     comm_allgather_bytes(ctx, d_g, d_g + sizeof(mine), sizeof(mine));
@@ -730,7 +730,11 @@ static Fr logup_run(qg_ctx* ctx, uint32_t nvars, uint32_t ntables, const std::ve
   Fr tinv = Fr::zero();
   if (!ht.err) {
     const Fr tot_plain = ht.tot;  // nonzero: no denominator was zero
-    const Fr inv_plain = inv_bingcd<FrP>(tot_plain);
+    Fr inv_plain = inv_bingcd<FrP>(tot_plain);
+    // one multiply checks the binary GCD (its iteration bound has little
+    // slack); Fermat inversion if it ever did not converge
+    if (!(lg_plain_mul(tot_plain, inv_plain) == from_mont(Fr::one())))
+      inv_plain = from_mont(finv(to_mont(tot_plain)));
     tinv = lg_plain_mul(inv_plain, pow2_mod_plain<FrP>(517));
   }
   if (!ht.err) {

@@ -800,13 +800,17 @@ static constexpr int SP_MAXW = 64;
 struct SpConsts {
   L9 v[SP_MAXW];
 };
-__global__ void k_s_presum(const Fr* __restrict__ f, size_t B, uint32_t h, SpConsts cw,
+// (f has M entries: W/2 whole blocks for W >= 2; at W = 1 it fills half the one
+// block, the rest is the zero padding)
+__global__ void k_s_presum(const Fr* __restrict__ f, size_t M, size_t B, uint32_t h, SpConsts cw,
                            const Fr* __restrict__ pw, Fr* __restrict__ u) {
   const size_t i2 = (size_t)blockIdx.x * blockDim.x + threadIdx.x;
   if (i2 >= B) return;
   R29 acc = R29::zero();
-  for (uint32_t i1 = 0; i1 < h; i1++)
-    acc = red2p29(add29(acc, mul29(to29(f[(size_t)i1 * B + i2]), R29::from_l9(cw.v[i1]))));
+  for (uint32_t i1 = 0; i1 < h; i1++) {
+    const size_t g = (size_t)i1 * B + i2;
+    if (g < M) acc = red2p29(add29(acc, mul29(to29(f[g]), R29::from_l9(cw.v[i1]))));
+  }
   u[i2] = from29(canon29(mul29(acc, to29(pw[i2]))));
 }
 
@@ -860,13 +864,15 @@ __global__ void k_s_combine_res(const Fr* __restrict__ Fc, const Fr* __restrict_
   H[p] = from29(canon29(mul29(mul29(v, red6p29(wi)), R29::from_l9(cst))));
 }
 
-// send[d L + m] = K[d] P[i2] Z[i2], i2 = (d mod 2) L + m   (K: x 2^261, P: x 2^261)
+// send[d L + m] = K[d] P[i2] Z[i2], i2 = ((M + d L) mod B) + m: (d mod 2) L + m
+// for W >= 2 (M = W/2 blocks), L + m at W = 1 (M = L = B/2; `sh` = 1)
+// (K: x 2^261, P: x 2^261)
 __global__ void k_s_outgoing(const Fr* __restrict__ Z, const Fr* __restrict__ P, SpConsts K,
-                             size_t L, uint32_t W, Fr* __restrict__ send) {
+                             size_t L, uint32_t W, uint32_t sh, Fr* __restrict__ send) {
   const size_t i = (size_t)blockIdx.x * blockDim.x + threadIdx.x;
   if (i >= (size_t)W * L) return;
   const uint32_t d = (uint32_t)(i / L);
-  const size_t i2 = (size_t)(d & 1) * L + i % L;
+  const size_t i2 = (size_t)((d + sh) & 1) * L + i % L;
   send[i] = from29(canon29(mul29(mul29(to29(Z[i2]), to29(P[i2])), R29::from_l9(K.v[d]))));
 }
 
@@ -926,17 +932,18 @@ static void s_poly_sharded(qg_ctx* ctx, const Fr* f, size_t M, const uint64_t* p
     SpConsts cw{};
     Fr wk = Fr::one();
     const Fr wWc = fpow_small(wW, cc);
-    for (uint32_t i1 = 0; i1 < W / 2; i1++) {
+    const uint32_t hb = std::max<uint32_t>(1, W / 2);  // input blocks (partial at W = 1)
+    for (uint32_t i1 = 0; i1 < hb; i1++) {
       cw.v[i1] = l9_x261(wk);
       wk = wk * wWc;
     }
-    hipLaunchKernelGGL(k_s_presum, dim3(div_up(B, ML_BLOCK)), dim3(ML_BLOCK), 0, ctx->stream, f, B,
-                       W / 2, cw, pw, tmp);
+    hipLaunchKernelGGL(k_s_presum, dim3(div_up(B, ML_BLOCK)), dim3(ML_BLOCK), 0, ctx->stream, f, M,
+                       B, hb, cw, pw, tmp);
     QG_LAUNCH_CHECK();
     ntt_run(ctx, true, tmp, B, Fq, twB, lb, 0, 0, nullptr);
     // G at residue cc: levels above the block collapse into a host constant,
     // then one launch per level t = lb - 1 .. 0 (ping-pong tmp / Gq; nz >= lb
-    // whenever W >= 2)
+    // whenever W >= 2; at W = 1, nz = lb - 1 and the top level starts from q0 = 1)
     const size_t nz = nvars;
     Fr q0 = Fr::one();
     for (size_t t = nz; t-- > (size_t)lb;) {  // levels with a single entry (t >= lb)
@@ -978,13 +985,13 @@ static void s_poly_sharded(qg_ctx* ctx, const Fr* f, size_t M, const uint64_t* p
   SpConsts Kd{};
   const Fr wWi = finv(wW);
   for (uint32_t d = 0; d < W; d++) {
-    const uint64_t i1 = W / 2 + d / 2;
+    const uint64_t i1 = (M + (size_t)d * L) / B;  // W/2 + d/2 for W >= 2, 0 at W = 1
     Kd.v[d] = l9_x261(fpow_small(wWi, (i1 * c) % W));
   }
   Fr* sendb = ctx->scratch_as<Fr>("sp_send", (size_t)W * L);
   Fr* recvb = ctx->scratch_as<Fr>("sp_recv", (size_t)W * L);
   hipLaunchKernelGGL(k_s_outgoing, dim3(div_up((size_t)W * L, ML_BLOCK)), dim3(ML_BLOCK), 0,
-                     ctx->stream, H, P, Kd, L, W, sendb);
+                     ctx->stream, H, P, Kd, L, W, W == 1 ? 1u : 0u, sendb);
   QG_LAUNCH_CHECK();
   comm_alltoall_bytes(ctx, sendb, recvb, L * sizeof(Fr));
   hipLaunchKernelGGL(k_s_sum_parts, dim3(div_up(L, ML_BLOCK)), dim3(ML_BLOCK), 0, ctx->stream,
@@ -1019,7 +1026,8 @@ static void mle_open_sharded(qg_ctx* ctx, const qg_srs* srs, const Fr* dpoly, si
   // S: this rank's slice from the residue-split transform (s_poly_sharded) or,
   // with QG_S_REPLICATED=1 (A/B runs), the whole S on every rank
   comm_allgather_bytes(ctx, dpoly, dfull, L * sizeof(Fr));
-  static const bool replicated = getenv("QG_S_REPLICATED") != nullptr;
+  const char* rep = getenv("QG_S_REPLICATED");  // read per call: tests toggle it in-process
+  const bool replicated = rep && atoi(rep) != 0;
   Fr* Sl = ctx->scratch_as<Fr>("mle_S_local", L);
   size_t Slen = 0;
   if (N > 1) {
@@ -1064,7 +1072,7 @@ static void mle_open_sharded(qg_ctx* ctx, const qg_srs* srs, const Fr* dpoly, si
 static void mle_open_device(qg_ctx* ctx, const qg_srs* srs, const Fr* dpoly, size_t n,
                             const uint64_t* point, size_t nvars, uint8_t state[32],
                             qg_mle_proof* out, bool unchanged = false) {
-  if (ctx->world > 1) return mle_open_sharded(ctx, srs, dpoly, n, point, nvars, state, out);
+  if (ctx->sharded) return mle_open_sharded(ctx, srs, dpoly, n, point, nvars, state, out);
   const size_t N = (size_t)1 << nvars;
   Fr* dz = ctx->scratch_as<Fr>("mle_z", nvars ? nvars : 1);
   Fr* dpr = ctx->scratch_as<Fr>("mle_pr", N);

@@ -1393,7 +1393,7 @@ static void msm_reduce_phase(qg_ctx* ctx, const qg_srs* srs, const std::vector<M
 // per-rank XYZZ partial -> the MSM over all ranks, affine (allgather + host EC
 // adds: RCCL cannot add curve points)
 static G1Affine msm_finish_ranks(qg_ctx* ctx, G1Xyzz acc) {
-  if (ctx->world > 1) {
+  if (ctx->sharded) {
     G1Xyzz* d_send = ctx->scratch_as<G1Xyzz>("msm_comm_send", 1);
     G1Xyzz* d_recv = ctx->scratch_as<G1Xyzz>("msm_comm_recv", ctx->world);
     QG_HIP(hipMemcpyAsync(d_send, &acc, sizeof(G1Xyzz), hipMemcpyHostToDevice, ctx->stream));
@@ -1441,6 +1441,13 @@ static G1Affine msm_host(qg_ctx* ctx, const qg_srs* srs, const uint64_t* h, size
     return msm_device(ctx, srs, d, n);
   }
   if (!ctx->copy_stream) QG_HIP(hipStreamCreateWithFlags(&ctx->copy_stream, hipStreamNonBlocking));
+  {  // the uploads start after the work already queued on ctx->stream (stream
+     // order in both directions: the scratch slot may still be read there)
+    hipEvent_t ev = ctx->ev_get();
+    QG_HIP(hipEventRecord(ev, ctx->stream));
+    QG_HIP(hipStreamWaitEvent(ctx->copy_stream, ev, 0));
+    ctx->event_pool.push_back(ev);
+  }
   std::vector<MsmRun> runs;
   const size_t per = div_up(n, (size_t)P);
   for (int k = 0; k < P; k++) {

@@ -1860,8 +1860,8 @@ static uint64_t* sumcheck_bacc0(uint32_t* bar, uint32_t nvars) {
 // per slot.  QG_SC_OLD_TAIL=1 keeps the streaming k_sc_tail (A/B runs).
 template <int K, int NP>
 static size_t slice_gmax(qg_ctx* ctx, size_t cus) {
-  static const bool off = getenv("QG_SC_OLD_TAIL") != nullptr;
-  if (off) return 0;
+  const char* off = getenv("QG_SC_OLD_TAIL");  // read per call: tests toggle it in-process
+  if (off && atoi(off) != 0) return 0;
   const size_t gm = std::min<size_t>(persist_grid_cap<K, NP, true>(ctx, cus), sl_smax(K));
   size_t G = 1;
   while (G * 2 <= gm) G *= 2;
@@ -2222,7 +2222,7 @@ template <int K, int NP>
 static uint32_t run_rounds_any(qg_ctx* ctx, uint32_t nvars, const std::vector<const Fr*>& src,
                                const SopDev* d_sp, SopHdr h, RoundOut ro, uint32_t* bar,
                                Fr* d_final, Fr* d_eval) {
-  if (ctx->world > 1) return run_rounds_dist<K, NP>(ctx, nvars, src, d_sp, h, ro, bar, d_final, d_eval);
+  if (ctx->sharded) return run_rounds_dist<K, NP>(ctx, nvars, src, d_sp, h, ro, bar, d_final, d_eval);
   return run_rounds<K, NP>(ctx, nvars, src, d_sp, h, ro, bar, d_final, d_eval);
 }
 
@@ -2687,7 +2687,7 @@ static void zerocheck_run(qg_ctx* ctx, uint32_t nvars, uint32_t ntables,
   Fr* d_eq = ctx->scratch_as<Fr>("zc_eq", N);
   QG_HIP(hipMemcpyAsync(d_z, z.data(), sizeof(Fr) * nvars, hipMemcpyHostToDevice, ctx->stream));
   eq_table_device(ctx, d_z, m, d_eq);
-  if (ctx->world > 1) {
+  if (ctx->sharded) {
     // this rank's block: the high index bits are the rank (eq_eval.rs bit j <-> z_j)
     Fr f = Fr::one();
     for (uint32_t j = m; j < nvars; j++)

@@ -67,6 +67,9 @@ PROTOTYPES = {
     "qg_loopback_destroy": (C.c_int, [P]),
     "qg_ctx_attach_loopback": (C.c_int, [P, P, C.c_int]),
     "qg_comm_allgather_host": (C.c_int, [P, P, SZ, P]),
+    "qg_comm_alltoall_host": (C.c_int, [P, P, SZ, P]),
+    "qg_ctx_comm_info": (C.c_int, [P, C.POINTER(C.c_int), C.POINTER(C.c_int),
+                                   C.POINTER(C.c_int), C.POINTER(C.c_int)]),
     "qg_trace_full_witness": (C.c_int, [P, C.POINTER(P), C.c_uint32, C.c_uint64, P]),
     "qg_transcript_new": (C.c_int, [C.c_char_p, SZ, U8P]),
     "qg_transcript_append": (C.c_int, [U8P, C.c_char_p, SZ]),
@@ -141,6 +144,7 @@ PROTOTYPES = {
     "qg_microbench_fetch": (C.c_int, [P, C.c_size_t, C.c_size_t, C.POINTER(C.c_double),
                                       C.POINTER(C.c_double)]),
     "qg_ctx_kernel_time": (C.c_int, [P, C.c_char_p, C.POINTER(C.c_double), U32P]),
+    "qg_trace_marker": (C.c_int, [P, C.c_uint32]),
 }
 
 _lib = None

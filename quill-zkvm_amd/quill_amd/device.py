@@ -29,10 +29,36 @@ class Device:
         except Exception:
             pass
 
-    def attach_comm(self, rank: int, world: int, unique_id: bytes):
-        buf = (C.c_uint8 * 128).from_buffer_copy(unique_id)
+    def attach_comm(self, rank: int, world: int, unique_id: bytes = None):
+        """RCCL communicator (qg_ctx_attach_comm); world 1 detaches unless
+        QG_FORCE_RCCL=1 (then a one-rank RCCL communicator, unique_id optional)"""
+        buf = None if unique_id is None else (C.c_uint8 * 128).from_buffer_copy(unique_id)
         check(lib().qg_ctx_attach_comm(self.h, rank, world, buf), self.h)
         self.rank, self.world = rank, world
+
+    def comm_info(self) -> dict:
+        """{"kind": "none" | "loopback" | "rccl", "rank", "world", "sharded"}"""
+        k, r, w, s = C.c_int(), C.c_int(), C.c_int(), C.c_int()
+        check(lib().qg_ctx_comm_info(self.h, C.byref(k), C.byref(r), C.byref(w), C.byref(s)),
+              self.h)
+        return {"kind": ("none", "loopback", "rccl")[k.value], "rank": r.value,
+                "world": w.value, "sharded": bool(s.value)}
+
+    def alltoall_bytes(self, chunks: list) -> list:
+        """personalised exchange (qg_comm_alltoall_host): chunks[d] goes to rank d
+        (equal lengths); returns the chunk received from every rank, in rank order"""
+        assert len(chunks) == self.world and len({len(c) for c in chunks}) == 1
+        n = len(chunks[0])
+        src = C.create_string_buffer(b"".join(chunks), n * self.world)
+        dst = C.create_string_buffer(n * self.world)
+        check(lib().qg_comm_alltoall_host(self.h, src, n, dst), self.h)
+        raw = dst.raw
+        return [raw[i * n:(i + 1) * n] for i in range(self.world)]
+
+    def trace_marker(self, tag: int):
+        """an empty kernel of `tag` work-groups on the context stream: cuts a
+        rocprofv3 kernel trace into phases (profiles/kstats.py --legs)"""
+        check(lib().qg_trace_marker(self.h, tag), self.h)
 
     def attach_loopback(self, group, rank: int, world: int = None):
         check(lib().qg_ctx_attach_loopback(self.h, group, rank), self.h)
@@ -45,8 +71,8 @@ class Device:
     def allgather_bytes(self, data: bytes) -> list:
         """every rank's `data` (equal lengths), in rank order (qg_comm_allgather_host)"""
         n = len(data)
-        if self.world == 1 or n == 0:
-            return [bytes(data)]
+        if n == 0:
+            return [bytes(data)] * self.world
         src = C.create_string_buffer(bytes(data), n)
         dst = C.create_string_buffer(n * self.world)
         check(lib().qg_comm_allgather_host(self.h, src, n, dst), self.h)

@@ -1,0 +1,130 @@
+"""The alternate kernels kept beside the defaults, each checked bit
+for bit against the default path on the same inputs:
+  * k_sc_tail, the streaming sumcheck tail: QG_SC_OLD_TAIL=1 on one context, and
+    the sharded prover whose gathered tail does not fit the slice tail (8 source
+    tables at nvars >= 15 over 8 loopback ranks);
+  * k_logup_fused, the one-pass Logup column (QG_LOGUP_FUSED=1);
+  * the replicated S polynomial in the sharded ML opening (QG_S_REPLICATED=1).
+The switches are read per call, so the tests toggle them in-process."""
+import contextlib
+import os
+import random
+
+import pytest
+
+import quill_oracle as o
+
+pytestmark = pytest.mark.gpu
+R = o.R_MOD
+
+
+@contextlib.contextmanager
+def env(name, value):
+    old = os.environ.get(name)
+    os.environ[name] = value
+    try:
+        yield
+    finally:
+        if old is None:
+            os.environ.pop(name)
+        else:
+            os.environ[name] = old
+
+
+def _prove(dev, nv, tabs, expr, label):
+    import quill_amd as q
+    from quill_amd.hyperplonk import sumcheck_prove_device
+    t = q.Transcript(label)
+    coeffs, lens, point, ev = sumcheck_prove_device(dev, nv, tabs, expr, 777, t)
+    return coeffs.tobytes(), lens.tobytes(), point.tobytes(), bytes(ev), t.state
+
+
+@pytest.mark.parametrize("nv,ntab", [(12, 3), (18, 3), (17, 8)])
+def test_old_tail_matches_slice_tail(dev, nv, ntab):
+    import quill_amd as q
+    from quill_amd.hyperplonk import VirtualPolyExpr as E
+    expr = E.Input(0) * E.Input(1) * E.Input(2)
+    for i in range(3, ntab):
+        expr = expr + E.Input(i) * E.Const(i)
+    tabs = [q.DeviceVec(dev, 1 << nv).fill_random(31 * nv + i) for i in range(ntab)]
+    a = _prove(dev, nv, tabs, expr, b"tail-ab")
+    with env("QG_SC_OLD_TAIL", "1"):
+        b = _prove(dev, nv, tabs, expr, b"tail-ab")
+    for t in tabs:
+        t.close()
+    assert a == b
+
+
+@pytest.mark.parametrize("world,nv", [(8, 17), (4, 16)])
+def test_sharded_k8_tail_matches_single(world, nv):
+    """8 source tables: the gathered 2^15-entry tail exceeds what the slice tail
+    covers with 8 slots (and the loopback's 1/world CU share), so run_rounds_dist
+    falls back to k_sc_tail; its proof equals the single-context proof."""
+    import quill_amd as q
+    from quill_amd.hyperplonk import VirtualPolyExpr as E, sumcheck_prove_tables
+    from test_gpu_multirank import run_ranks
+    lw = world.bit_length() - 1
+    N, NL = 1 << nv, 1 << (nv - lw)
+    dev0 = q.Device(0)
+    tabs = [q.DeviceVec(dev0, N).fill_random(500 + i) for i in range(8)]
+    host = [t.to_list() for t in tabs]
+    for t in tabs:
+        t.close()
+    me = E.Input(0) * E.Input(1) * E.Input(2) + E.Input(3) * E.Input(4) * E.Input(5) \
+        - E.Input(6) * E.Input(7)
+    claimed = random.Random(nv).randrange(R)
+    ref = sumcheck_prove_tables(dev0, nv, host, me, claimed, q.Transcript(b"k8"))
+    dev0.close()
+
+    def fn(d, rank, world):
+        return sumcheck_prove_tables(d, nv, [tb[rank * NL:(rank + 1) * NL] for tb in host], me,
+                                     claimed, q.Transcript(b"k8"))
+    for got in run_ranks(world, fn):
+        assert got == ref
+
+
+@pytest.mark.parametrize("nv", [11, 13, 16])
+def test_logup_fused_matches_default(dev, nv):
+    import quill_amd as q
+    from quill_amd import VirtualPolyExpr as E
+    from quill_amd.logup import logup_column_device
+    tabs = [q.DeviceVec(dev, 1 << nv).fill_random(88 + 5 * i + nv) for i in range(3)]
+    res = []
+    for fused in ("0", "1"):
+        out = q.DeviceVec(dev, 1 << nv)
+        with env("QG_LOGUP_FUSED", fused):
+            s = logup_column_device(dev, nv, tabs, E.Input(0) + E.Const(0xA1FA) * E.Input(1),
+                                    0xBE7A, out, E.Input(2))
+        res.append((s, out.to_numpy().tobytes()))
+        out.close()
+    for t in tabs:
+        t.close()
+    assert res[0] == res[1]
+
+
+@pytest.mark.parametrize("world", [2, 4])
+def test_replicated_s_matches_split(world):
+    import quill_amd as q
+    from quill_amd import KZG, Transcript
+    from test_gpu_multirank import run_ranks
+    rnd = random.Random(900 + world)
+    nv = 10
+    N = 1 << nv
+    L = N // world
+    tau = rnd.randrange(R)
+    poly = [rnd.randrange(R) for _ in range(N)]
+    point = [rnd.randrange(R) for _ in range(nv)]
+
+    def fn(d, rank, world):
+        kzg = KZG(d, q.Srs.generate(d, tau, L, offset=rank * L), N - 1)
+        vec = q.DeviceVec.from_list(d, poly[rank * L:(rank + 1) * L])
+        t = Transcript(b"srep")
+        pr = kzg.open_dev(vec, L, point, t)
+        vec.close()
+        kzg.srs.close()
+        return pr, t.state
+    split = run_ranks(world, fn)
+    with env("QG_S_REPLICATED", "1"):
+        rep = run_ranks(world, fn)
+    assert split == rep
+    assert all(x == split[0] for x in split)

@@ -55,7 +55,7 @@ def test_sharded_msm(world):
     assert all(r == exp for r in run_ranks(world, fn))
 
 
-@pytest.mark.parametrize("world,nv_local", [(2, 9), (4, 6), (2, 1), (8, 5), (8, 1)])
+@pytest.mark.parametrize("world,nv_local", [(2, 9), (4, 6), (2, 1), (8, 5), (8, 1), (1, 9)])
 def test_sharded_sumcheck(world, nv_local):
     import quill_amd as q
     from quill_amd.hyperplonk import VirtualPolyExpr as E, sumcheck_prove_tables
@@ -113,7 +113,7 @@ def test_sharded_zerocheck(world):
 
 
 @pytest.mark.parametrize("world,tail_zeros", [(2, 0), (4, 0), (4, 131), (2, 1), (8, 0), (8, 131),
-                                              (8, 300)])
+                                              (8, 300), (1, 0), (1, 131)])
 def test_sharded_mle_open(world, tail_zeros):
     """MLEvalProof::prove with the evaluations and the SRS sharded over ranks
     equals the single-context proof (and transcript state)."""
