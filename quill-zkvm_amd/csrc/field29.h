@@ -466,6 +466,57 @@ __device__ __forceinline__ void sqr29t2(const F29<C>& a, const F29<C>& c, F29<C>
   r2.l[8] = (uint32_t)y;
 }
 
+// N independent products r[n] = a[n] b[n] 2^-261 with their column chains
+// interleaved mad by mad (mul29t2 generalised): consecutive mads belong to
+// different chains, so no hazard s_nop, and N chains are in flight for the
+// wave.  Same arithmetic and operand conditions as mul29t.  r may alias a.
+template <class C, int N>
+__device__ __forceinline__ void mul29tn(const F29<C> (&a)[N], const F29<C> (&b)[N],
+                                        F29<C> (&r)[N]) {
+  uint32_t m[N][9];
+  uint64_t x[N];
+#pragma unroll
+  for (int n = 0; n < N; n++) x[n] = 0;
+#pragma unroll
+  for (int k = 0; k < 9; k++) {
+#pragma unroll
+    for (int j = 0; j < k; j++) {
+#pragma unroll
+      for (int n = 0; n < N; n++) x[n] = mad_vv(a[n].l[j], b[n].l[k - j], x[n]);
+#pragma unroll
+      for (int n = 0; n < N; n++) x[n] = mad_vs(m[n][j], F29P<C>::P.v[k - j], x[n]);
+    }
+#pragma unroll
+    for (int n = 0; n < N; n++) x[n] = mad_vv(a[n].l[k], b[n].l[0], x[n]);
+#pragma unroll
+    for (int n = 0; n < N; n++) m[n][k] = ((uint32_t)x[n] * F29P<C>::INV) & M29;
+#pragma unroll
+    for (int n = 0; n < N; n++) x[n] = mad_vs(m[n][k], F29P<C>::P.v[0], x[n]) >> 29;
+  }
+  uint32_t out[N][9];
+#pragma unroll
+  for (int k = 9; k < 17; k++) {
+#pragma unroll
+    for (int j = k - 8; j < 9; j++) {
+#pragma unroll
+      for (int n = 0; n < N; n++) x[n] = mad_vv(a[n].l[j], b[n].l[k - j], x[n]);
+#pragma unroll
+      for (int n = 0; n < N; n++) x[n] = mad_vs(m[n][j], F29P<C>::P.v[k - j], x[n]);
+    }
+#pragma unroll
+    for (int n = 0; n < N; n++) {
+      out[n][k - 9] = (uint32_t)x[n] & M29;
+      x[n] >>= 29;
+    }
+  }
+#pragma unroll
+  for (int n = 0; n < N; n++) {
+#pragma unroll
+    for (int i = 0; i < 8; i++) r[n].l[i] = out[n][i];
+    r[n].l[8] = (uint32_t)x[n];
+  }
+}
+
 // mulsub29 with one signed chain per column
 template <class C>
 __device__ __forceinline__ F29<C> mulsub29t(const F29<C>& a, const F29<C>& b, const F29<C>& c,
@@ -501,6 +552,8 @@ __device__ __forceinline__ F29<C> mulsub29t(const F29<C>& a, const F29<C>& b, co
 }
 #elif defined(__HIP__)
 // host pass: declarations only (device code, never called from the host)
+template <class C, int N>
+__device__ void mul29tn(const F29<C> (&a)[N], const F29<C> (&b)[N], F29<C> (&r)[N]);
 template <class C>
 __device__ F29<C> mul29t(const F29<C>& a, const F29<C>& b);
 template <class C>

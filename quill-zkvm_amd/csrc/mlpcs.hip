@@ -840,9 +840,12 @@ __global__ void k_eqdft_res(const Fr* __restrict__ qnext, Fr q0, L9 a261, L9 zc2
 // w_B^{-k2} (F_c G_m' + F_m' G_c): twiB holds w_B^{-e} 2^261, cst the
 // per-residue constant x 2^266 (mul29 of the 2^251-scaled products lands in
 // arkworks form).
+// At W = 1 the (-1)^k of w^{k(M-1)} = (-1)^k w^{-k} is (-1)^k2, not the
+// residue's constant (-1)^c: `alt` negates the odd k2.
 __global__ void k_s_combine_res(const Fr* __restrict__ Fc, const Fr* __restrict__ Gc,
                                 const Fr* __restrict__ Fm, const Fr* __restrict__ Gm, int c,
-                                const Fr* __restrict__ twiB, int lb, L9 cst, Fr* __restrict__ H) {
+                                const Fr* __restrict__ twiB, int lb, L9 cst, int alt,
+                                Fr* __restrict__ H) {
   const size_t B = (size_t)1 << lb;
   const size_t p = (size_t)blockIdx.x * blockDim.x + threadIdx.x;
   if (p >= B) return;
@@ -859,7 +862,7 @@ __global__ void k_s_combine_res(const Fr* __restrict__ Fc, const Fr* __restrict_
   const size_t k2 = (size_t)(__brevll((unsigned long long)p) >> (64 - lb));
   const size_t half = B / 2;
   R29 wi = to29(twiB[k2 & (half - 1)]);
-  if (k2 & half) wi = sub29(R29::zero(), wi);
+  if (((k2 & half) != 0) != (alt && (k2 & 1))) wi = sub29(R29::zero(), wi);
   const R29 v = red2p29(add29(mul29(to29(Fc[p]), to29(Gm[pp])), mul29(to29(Fm[pp]), to29(Gc[p]))));
   H[p] = from29(canon29(mul29(mul29(v, red6p29(wi)), R29::from_l9(cst))));
 }
@@ -972,7 +975,7 @@ static void s_poly_sharded(qg_ctx* ctx, const Fr* f, size_t M, const uint64_t* p
   if (c & 1) cst = fneg(cst);
   const L9 cst9 = l9_of29(ml_plain_mul(from_mont(cst), pow2_mod_plain<FrP>(266)));
   hipLaunchKernelGGL(k_s_combine_res, dim3(div_up(B, ML_BLOCK)), dim3(ML_BLOCK), 0, ctx->stream, Fb,
-                     Gb, Fm, Gm, (int)c, twiB, lb, cst9, H);
+                     Gb, Fm, Gm, (int)c, twiB, lb, cst9, W == 1 ? 1 : 0, H);
   QG_LAUNCH_CHECK();
   ntt_run(ctx, false, H, B, H, twiB, lb, 0, 0, nullptr);
   Fr* P = tmp + B;

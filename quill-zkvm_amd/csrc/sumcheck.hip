@@ -780,8 +780,16 @@ QG_DEV R29 at_point(const R29& lo, const R29& d, int t, const SopLds<NP>& sp) {
 QG_DEV void fold_pair(const Fr (&w)[4], bool fold, const R29& r, Fr* dst, R29& lo, R29& hi) {
   if (fold) {
     const R29 x0 = to29(w[0]), x1 = to29(w[1]), x2 = to29(w[2]), x3 = to29(w[3]);
+#ifndef QG_SC_NO_ILP
+    // the two products interleaved (field29.h mul29tn): no dependent-mad nops
+    R29 a[2] = {sub29(x1, x0), sub29(x3, x2)}, b[2] = {r, r};
+    mul29tn<FrP, 2>(a, b, a);
+    lo = red2p29<FrP>(add29(x0, a[0]));
+    hi = red2p29<FrP>(add29(x2, a[1]));
+#else
     lo = red2p29<FrP>(add29(x0, mul29t(sub29(x1, x0), r)));
     hi = red2p29<FrP>(add29(x2, mul29t(sub29(x3, x2), r)));
+#endif
     dst[0] = from29(lo);
     dst[1] = from29(hi);
   } else {
@@ -847,13 +855,38 @@ QG_DEV void sweep_pairs(const AllBufs& tb, uint32_t j, bool fold, const R29& r, 
         R29 lo, hi;
         fold_pair(w, fold, r, tb.dst(j, s) + 2 * p, lo, hi);
         const R29 d = norm29(sub29(hi, lo));
+#ifndef QG_SC_NO_ILP
+        if constexpr (NP == 4) {
+          // the point products as interleaved chains (field29.h mul29tn): 4
+          // (round 0) or 3 (skip0: t = 1..3) independent multiplies in flight
+          if (s == 0) {
 #pragma unroll
-        for (int t = 0; t < NP; t++) {
-          if (t == 0 && skip0) continue;  // h(0) = claim - h(1), by the finisher
-          if (s == 0)
-            prod[t] = at_point<NP>(lo, d, t, sp);
-          else
-            prod[t] = mul29t(prod[t], at_point_lazy<NP>(lo, d, t, sp));
+            for (int t = 0; t < NP; t++) prod[t] = at_point<NP>(lo, d, t, sp);
+          } else if (skip0) {
+            R29 a[3] = {prod[1], prod[2], prod[3]};
+            R29 b[3] = {at_point_lazy<NP>(lo, d, 1, sp), at_point_lazy<NP>(lo, d, 2, sp),
+                        at_point_lazy<NP>(lo, d, 3, sp)};
+            mul29tn<FrP, 3>(a, b, a);
+            prod[1] = a[0];
+            prod[2] = a[1];
+            prod[3] = a[2];
+          } else {
+            R29 b[4];
+#pragma unroll
+            for (int t = 0; t < NP; t++) b[t] = at_point_lazy<NP>(lo, d, t, sp);
+            mul29tn<FrP, 4>(prod, b, prod);
+          }
+        } else
+#endif
+        {
+#pragma unroll
+          for (int t = 0; t < NP; t++) {
+            if (t == 0 && skip0) continue;  // h(0) = claim - h(1), by the finisher
+            if (s == 0)
+              prod[t] = at_point<NP>(lo, d, t, sp);
+            else
+              prod[t] = mul29t(prod[t], at_point_lazy<NP>(lo, d, t, sp));
+          }
         }
         if constexpr (PF) {
 #pragma unroll

@@ -41,7 +41,9 @@ def rank_slice(f, point, W, c):
     FG = {}
     for cc in sorted({c, cm}):
         # u_cc[i2] = w^{i2 cc} sum_{i1 < W/2} w_W^{i1 cc} f[i1 B + i2]
-        u = [pow(w, i2 * cc, R) * sum(pow(wW, i1 * cc, R) * f[i1 * B + i2] for i1 in range(W // 2))
+        # (W = 1: one block, f fills its first half; the rest is zero padding)
+        u = [pow(w, i2 * cc, R) * sum(pow(wW, i1 * cc, R) * f[i1 * B + i2]
+                                      for i1 in range(max(W // 2, 1)) if i1 * B + i2 < M)
              % R for i2 in range(B)]
         Fnat = dft(u, wB)  # F[k2 W + cc], natural k2
         Fbr = [Fnat[bitrev(p, lb)] for p in range(B)]
@@ -51,7 +53,7 @@ def rank_slice(f, point, W, c):
             zt = point[t]
             q0 = q0 * ((1 - zt) + zt * pow(w, cc << t, R)) % R
         prev = None
-        for t in range(lb - 1, -1, -1):
+        for t in range(min(nvars, lb) - 1, -1, -1):  # W = 1: nvars = lb - 1
             bits = lb - t
             zt = point[t]
             cur = []
@@ -74,20 +76,24 @@ def rank_slice(f, point, W, c):
             pp = p ^ ((1 << (p.bit_length() - 1)) - 1) if p else 0
         k2 = bitrev(p, lb)
         v = (Fc[p] * Gm[pp] + Fm[pp] * Gc[p]) % R
-        H.append(v * pow(wB, -k2 % B, R) % R * cst % R)
+        # w^{k(M-1)} = (-1)^k w^{-k}, k = k2 W + c: (-1)^k = (-1)^c for even W,
+        # (-1)^k2 at W = 1
+        sgn = -1 if (W == 1 and k2 & 1) else 1
+        H.append(sgn * v * pow(wB, -k2 % B, R) % R * cst % R)
     # inverse DIT: bit-reversed in, natural out: Z[i2] = sum_k2 H[bitrev(k2)] wB^{-i2 k2}
     Hnat = [H[bitrev(k2, lb)] for k2 in range(B)]
     Z = dft(Hnat, o.fr_inv(wB))
     out = []
     for d in range(W):
-        i1 = W // 2 + d // 2
+        # S[d L + m] = h[M + d L + m] = h[i1 B + i2]: i1 = W/2 + d/2 and
+        # i2 = (d mod 2) L + m for W >= 2; i1 = 0, i2 = L + m at W = 1
+        i1, o2 = divmod(M + d * L, B)
         K = pow(o.fr_inv(wW), (i1 * c) % W, R)
-        out.append([K * pow(wi, c * ((d & 1) * L + m), R) % R * Z[(d & 1) * L + m] % R
-                    for m in range(L)])
+        out.append([K * pow(wi, c * (o2 + m), R) % R * Z[o2 + m] % R for m in range(L)])
     return out
 
 
-@pytest.mark.parametrize("nvars,W", [(3, 2), (4, 4), (4, 8), (5, 2), (5, 8), (6, 4)])
+@pytest.mark.parametrize("nvars,W", [(3, 2), (4, 4), (4, 8), (5, 2), (5, 8), (6, 4), (3, 1), (5, 1)])
 def test_residue_split_s_polynomial(nvars, W):
     rnd = random.Random(nvars * 10 + W)
     M = 1 << nvars
