@@ -601,7 +601,10 @@ QG_DEV uint4 msm_entries4(const uint32_t* __restrict__ entries, uint32_t e, uint
 }
 
 // at most 128 VGPRs: four waves per SIMD (the paired multiplies need ~131)
-__global__ void __launch_bounds__(MSM_BLOCK) __attribute__((amdgpu_waves_per_eu(4)))
+#ifndef QG_MSM_WPE
+#define QG_MSM_WPE 4
+#endif
+__global__ void __launch_bounds__(MSM_BLOCK) __attribute__((amdgpu_waves_per_eu(QG_MSM_WPE)))
     k_msm_accumulate(const MsmPt* __restrict__ table, const uint32_t* __restrict__ entries,
                      const uint32_t* __restrict__ bstart, uint32_t nb, uint32_t L,
                      X29Raw* __restrict__ partial, uint32_t* __restrict__ owner) {
@@ -624,6 +627,51 @@ __global__ void __launch_bounds__(MSM_BLOCK) __attribute__((amdgpu_waves_per_eu(
   // rows are canonical in the R = 2^261 domain, the signed digit picks y or p - y
   X29 acc;
   bool inf = true;
+#ifdef QG_MSM_PF
+  // software-pipelined variant (A/B): the row of entry e + 1 is gathered
+  // before the addition of entry e
+  uint4 g0 = msm_entries4(entries, e0, e1);
+  uint4 g1 = e0 + 4 < e1 ? msm_entries4(entries, e0 + 4, e1) : g0;
+  Q29 ax, ay;
+  bool pinf = msm_pt_load(table, g0.x & 0x7fffffffu, (g0.x >> 31) != 0u, ax, ay);
+  for (uint32_t e = e0; e < e1; e++) {
+    const uint32_t k = (e - e0) & 3u;
+    Q29 bx = ax, by = ay;
+    bool qinf = true;
+    if (e + 1 < e1) {
+      const uint32_t en = k == 0 ? g0.y : k == 1 ? g0.z : k == 2 ? g0.w : g1.x;
+      qinf = msm_pt_load(table, en & 0x7fffffffu, (en >> 31) != 0u, bx, by);
+    }
+    if (k == 3) {
+      g0 = g1;
+      if (e + 5 < e1) g1 = msm_entries4(entries, e + 5, e1);
+    }
+    if (e == next) {
+      msm_flush(partial, owner, t + b, b, acc, inf);
+      inf = true;
+      do {
+        b++;
+        next = bstart[b + 1];
+      } while (next <= e);
+    }
+    if (!pinf) {
+      if (inf) {
+        acc.X = ax;
+        acc.Y = ay;
+        acc.ZZ = Q29::from_l9(F29P<FqP>::ONE);
+        acc.ZZZ = acc.ZZ;
+        inf = false;
+      } else if (!x29_acc_madd_tp(acc, ax, ay)) {
+        x29_acc_madd_exc(acc, ax, ay, &inf);
+      }
+    }
+    ax = bx;
+    ay = by;
+    pinf = qinf;
+  }
+  msm_flush(partial, owner, t + b, b, acc, inf);
+  return;
+#endif
   // entries arrive four at a time (one 16-B load per group of four, the next
   // group in flight during the current one): a thread revisits its entry line
   // only every few microseconds, long after L2 has evicted it, so single-entry
