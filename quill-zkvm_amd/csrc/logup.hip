@@ -241,12 +241,14 @@ __global__ __launch_bounds__(LG_BLOCK) void k_logup(const LgDev* __restrict__ g,
   pre_r[7] = mul29(pre_r[6], lds_row(vs, 7, tid));
   const R29 T = pre_r[LG_K - 1];
 
-  // 2. exclusive prefix / suffix products of T across the block
+  // 2. exclusive prefix / suffix products of T across the block (the two
+  // scans' products as one interleaved pair, field29.h mul29tn)
   R29 ip = T, is = T;  // inclusive in-wave prefix / suffix
   for (int d = 1; d < 64; d <<= 1) {
-    const R29 a = shfl_up29(ip, d), b = shfl_down29(is, d);
-    if (lane >= d) ip = mul29(a, ip);
-    if (lane + d < 64) is = mul29(is, b);
+    R29 x2[2] = {shfl_up29(ip, d), is}, y2[2] = {ip, shfl_down29(is, d)};
+    mul29tn<FrP, 2>(x2, y2, x2);
+    if (lane >= d) ip = x2[0];
+    if (lane + d < 64) is = x2[1];
   }
   if (lane == 63)
 #pragma unroll
@@ -266,27 +268,38 @@ __global__ __launch_bounds__(LG_BLOCK) void k_logup(const LgDev* __restrict__ g,
   const R29 binv = mul29(mul29(to29(*tinv), to29(pre[blockIdx.x])), to29(suf[blockIdx.x]));
   R29 inv_run = mul29(mul29(binv, ep), es);  // 1 / T
 
-  // 3. back-substitution: 1 / v_k overwrites v_k in LDS (own slots only)
-#define LG_BACK(k)                                        \
-  {                                                       \
-    const R29 x = mul29(inv_run, pre_r[k - 1]);           \
-    inv_run = mul29(inv_run, lds_row(vs, k, tid));        \
-    lds_put(vs, k, tid, x);                               \
+  // 3. back-substitution: 1 / v_k overwrites v_k in LDS (own slots only);
+  // the output product and the next running inverse as one interleaved pair
+#define LG_BACK(k)                                                      \
+  {                                                                     \
+    R29 a2[2] = {inv_run, inv_run}, b2[2] = {pre_r[k - 1], lds_row(vs, k, tid)}; \
+    mul29tn<FrP, 2>(a2, b2, a2);                                        \
+    inv_run = a2[1];                                                    \
+    lds_put(vs, k, tid, a2[0]);                                         \
   }
   LG_BACK(7) LG_BACK(6) LG_BACK(5) LG_BACK(4) LG_BACK(3) LG_BACK(2) LG_BACK(1)
 #undef LG_BACK
   lds_put(vs, 0, tid, inv_run);
 
-  // 4. multiplier, store, block sum
+  // 4. multiplier (four rows' products interleaved), store, block sum
   R29 acc = R29::zero();
-  for (int k = 0; k < LG_K; k++) {
-    const size_t row = base + (size_t)k * LG_BLOCK;
-    if (row >= n) break;
-    const R29 x = lds_row(vs, k, tid);
-    const R29 m = lg_eval(g, 1, row);  // M x 2^256
-    const R29 y = canon29(mul29(x, m));
-    out[row] = from29(y);
-    acc = red2p29(add29(acc, y));
+  for (int k0 = 0; k0 < LG_K; k0 += 4) {
+    R29 xs[4], ms[4];
+#pragma unroll
+    for (int u = 0; u < 4; u++) {
+      const size_t row = base + (size_t)(k0 + u) * LG_BLOCK;
+      xs[u] = lds_row(vs, k0 + u, tid);
+      ms[u] = row < n ? lg_eval(g, 1, row) : R29::zero();  // M x 2^256
+    }
+    mul29tn<FrP, 4>(xs, ms, xs);
+#pragma unroll
+    for (int u = 0; u < 4; u++) {
+      const size_t row = base + (size_t)(k0 + u) * LG_BLOCK;
+      if (row >= n) break;
+      const R29 y = canon29(xs[u]);
+      out[row] = from29(y);
+      acc = red2p29(add29(acc, y));
+    }
   }
   // block sum (values < 2p; a wave tree then 4 wave partials)
   for (int d = 32; d >= 1; d >>= 1) {

@@ -296,15 +296,30 @@ QG_DEV void lds_put29(uint32_t* sh, int e, const R29& v) {
   for (int i = 0; i < 9; i++) sh[i * NTT_T + e] = v.l[i];
 }
 
+// Twiddles by stage ("pyramid"): stage s's butterflies use w^(j 2^(logn-1-s))
+// for j < 2^s, stored contiguously at pyr[2^s - 1 + j] (2^logn - 1 entries,
+// twice the flat table).  Neighbouring butterflies of a stage have
+// neighbouring j, so a wave's twiddle loads are runs of consecutive 32-B
+// entries instead of one cache line per lane (the flat table's stride is
+// 2^(logn-1-s) entries).  Built once per (table, logn) from the flat powers.
+__global__ void k_tw_pyramid(const Fr* __restrict__ flat, int logn, Fr* __restrict__ pyr) {
+  const size_t i = (size_t)blockIdx.x * blockDim.x + threadIdx.x;
+  const size_t n = (size_t)1 << logn;
+  if (i + 1 >= n) return;
+  const int st = 63 - __clzll((unsigned long long)(i + 1));  // stage of entry i
+  const size_t j = i + 1 - ((size_t)1 << st);
+  pyr[i] = flat[j << (logn - 1 - st)];
+}
+
 // DIF (forward) or DIT (inverse) stages [s0, s0+B) on every tile.
 //   in:  n entries (entries >= nin read as zero)
 //   out: n entries, or only indices [win_lo, win_hi) written to out - win_lo
-//   tw:  w^k 2^261 (Fr words), k < n/2
+//   tw:  w^k 2^261 (Fr words) as the stage pyramid (pyr != 0) or flat, k < n/2
 template <bool DIF>
 __global__ void __launch_bounds__(NTT_THREADS)
     k_ntt_pass(const Fr* __restrict__ in, size_t nin, Fr* __restrict__ out,
-               const Fr* __restrict__ tw, int logn, int s0, int B, int lgL, size_t win_lo,
-               size_t win_hi) {
+               const Fr* __restrict__ tw, int pyr, int logn, int s0, int B, int lgL,
+               size_t win_lo, size_t win_hi) {
   __shared__ uint32_t sh[9 * NTT_T];
   const int lgT = B + lgL, T = 1 << lgT;
   const int L = 1 << lgL;
@@ -337,7 +352,7 @@ __global__ void __launch_bounds__(NTT_THREADS)
         e0[h] = (mid0 << lgL) | l;
         e1[h] = e0[h] | (1 << (b + lgL));
         const size_t j = ((size_t)(mid0 & ((1 << b) - 1)) << s0) + lo0 + l;  // i0 mod 2^s
-        w[h] = to29(tw[j << (logn - 1 - s)]);
+        w[h] = to29(tw[pyr ? ((size_t)1 << s) - 1 + j : j << (logn - 1 - s)]);
         u[h] = lds_get29(sh, e0[h]);
         v[h] = lds_get29(sh, e1[h]);
       }
@@ -367,188 +382,31 @@ __global__ void __launch_bounds__(NTT_THREADS)
   }
 }
 
-// Radix-4 form of k_ntt_pass: two stages per LDS round trip.  A group is the
-// four tile elements whose mid indices differ only in the two stage bits; the
-// first stage's two butterflies and then the second stage's two run in
-// registers (each thread holds two groups, so four independent products per
-// stage go through mul29tn), and every element is read and written once per
-// two stages (18 instead of 36 LDS accesses per butterfly, half the
-// barriers).  Twiddles: W_s(j) = tw[j << (logn - 1 - s)]; with j0 the lower
-// element's index mod 2^s, DIF over mid bits (b, b-1) (stage s = s0 + b first)
-// uses W_s(j0), W_s(j0 + 2^(s-1)) and W_{s-1}(j0); DIT over mid bits (b, b+1)
-// (stage s = s0 + b first) uses W_s(j0), W_{s+1}(j0) and W_{s+1}(j0 + 2^s).
-// An odd leftover stage runs as the radix-2 step (DIF: the top bit first,
-// DIT: the top bit last).  Same I/O contract and outputs as k_ntt_pass.
-template <bool DIF>
-__global__ void __launch_bounds__(NTT_THREADS)
-    k_ntt_pass4(const Fr* __restrict__ in, size_t nin, Fr* __restrict__ out,
-                const Fr* __restrict__ tw, int logn, int s0, int B, int lgL, size_t win_lo,
-                size_t win_hi) {
-  __shared__ uint32_t sh[9 * NTT_T];
-  const int lgT = B + lgL, T = 1 << lgT;
-  const int L = 1 << lgL;
-  const size_t tid = threadIdx.x;
-  const size_t ngroups = ((size_t)1 << s0) >> lgL;
-  const size_t hi = blockIdx.x / ngroups, lo0 = (blockIdx.x % ngroups) << lgL;
-  const size_t base = (hi << (s0 + B)) + lo0;
-  for (int e = (int)tid; e < T; e += NTT_THREADS) {
-    const size_t i = base + ((size_t)(e >> lgL) << s0) + (e & (L - 1));
-    R29 v = R29::zero();
-    if (i < nin) v = to29(in[i]);
-    lds_put29(sh, e, v);
+// the stage pyramid of a flat twiddle table (cached per table and size)
+static const Fr* ntt_pyramid(qg_ctx* ctx, const Fr* flat, int logn) {
+  const std::string tag = "ntt_pyr_" + std::to_string((uintptr_t)flat);
+  const size_t n = (size_t)1 << logn;
+  Fr* pyr = ctx->scratch_as<Fr>(tag, std::max<size_t>(1, n - 1));
+  const std::string memo = std::to_string(logn) + "@" + std::to_string((uintptr_t)pyr);
+  if (ctx->memo[tag] != memo) {
+    hipLaunchKernelGGL(k_tw_pyramid, dim3(div_up(n, 256)), dim3(256), 0, ctx->stream, flat, logn,
+                       pyr);
+    QG_LAUNCH_CHECK();
+    ctx->memo[tag] = memo;
   }
-  __syncthreads();
-  // one radix-2 stage on mid bit b (the leftover of an odd B)
-  auto radix2 = [&](int b) {
-    const int s = s0 + b;
-    for (int p0 = (int)tid; p0 < T / 2; p0 += 2 * NTT_THREADS) {
-      const bool two = p0 + NTT_THREADS < T / 2;
-      int e0[2], e1[2];
-      R29 u[2], v[2], w[2];
-#pragma unroll
-      for (int h = 0; h < 2; h++) {
-        const int p = h && two ? p0 + NTT_THREADS : p0;
-        const int l = p & (L - 1), q = p >> lgL;
-        const int mid0 = ((q >> b) << (b + 1)) | (q & ((1 << b) - 1));
-        e0[h] = (mid0 << lgL) | l;
-        e1[h] = e0[h] | (1 << (b + lgL));
-        const size_t j = ((size_t)(mid0 & ((1 << b) - 1)) << s0) + lo0 + l;
-        w[h] = to29(tw[j << (logn - 1 - s)]);
-        u[h] = lds_get29(sh, e0[h]);
-        v[h] = lds_get29(sh, e1[h]);
-      }
-      R29 t[2];
-      if (DIF) mul29t2(sub29(u[0], v[0]), w[0], sub29(u[1], v[1]), w[1], t[0], t[1]);
-      else mul29t2(v[0], w[0], v[1], w[1], t[0], t[1]);
-#pragma unroll
-      for (int h = 0; h < 2; h++) {
-        if (h && !two) break;
-        if (DIF) {
-          lds_put29(sh, e0[h], red2p29(add29(u[h], v[h])));
-          lds_put29(sh, e1[h], t[h]);
-        } else {
-          lds_put29(sh, e0[h], red2p29(add29(u[h], t[h])));
-          lds_put29(sh, e1[h], red6p29(sub29(u[h], t[h])));
-        }
-      }
-    }
-    __syncthreads();
-  };
-  // two stages on mid bits (bh, bl) = (b, b-1) for DIF, (b + 1, b) for DIT
-  auto radix4 = [&](int b) {
-    const int bl = DIF ? b - 1 : b;  // the lower of the two bits
-    const int G4 = T / 4;            // groups per tile (>= 2 NTT_THREADS when T = 2048)
-    for (int g0 = (int)tid; g0 < G4; g0 += 2 * NTT_THREADS) {
-      const bool two = g0 + NTT_THREADS < G4;
-      int e[2][4];
-      R29 x[2][4], wa[2], wb[2], wc[2];
-#pragma unroll
-      for (int hh = 0; hh < 2; hh++) {
-        const int g = hh && two ? g0 + NTT_THREADS : g0;
-        const int l = g & (L - 1), q = g >> lgL;  // q: mid with the two bits removed
-        const int mid0 = ((q >> bl) << (bl + 2)) | (q & ((1 << bl) - 1));
-        const int e00 = (mid0 << lgL) | l;
-        const int dl = 1 << (bl + lgL), dh = 2 << (bl + lgL);
-        e[hh][0] = e00;
-        e[hh][1] = e00 | dl;
-        e[hh][2] = e00 | dh;
-        e[hh][3] = e00 | dl | dh;
-        const size_t j0 = ((size_t)(mid0 & ((1 << bl) - 1)) << s0) + lo0 + l;
-        const int sl = s0 + bl;  // stage of the lower bit
-        if (DIF) {  // stage sl + 1 (pairs 0-2, 1-3), then sl (pairs 0-1, 2-3)
-          wa[hh] = to29(tw[j0 << (logn - 2 - sl)]);
-          wb[hh] = to29(tw[(j0 + ((size_t)1 << sl)) << (logn - 2 - sl)]);
-          wc[hh] = to29(tw[j0 << (logn - 1 - sl)]);
-        } else {  // stage sl (pairs 0-1, 2-3), then sl + 1 (pairs 0-2, 1-3)
-          wc[hh] = to29(tw[j0 << (logn - 1 - sl)]);
-          wa[hh] = to29(tw[j0 << (logn - 2 - sl)]);
-          wb[hh] = to29(tw[(j0 + ((size_t)1 << sl)) << (logn - 2 - sl)]);
-        }
-#pragma unroll
-        for (int k = 0; k < 4; k++) x[hh][k] = lds_get29(sh, e[hh][k]);
-      }
-      if (DIF) {
-        // stage (high bit): (0, 2) by wa, (1, 3) by wb
-        R29 a4[4] = {sub29(x[0][0], x[0][2]), sub29(x[0][1], x[0][3]), sub29(x[1][0], x[1][2]),
-                     sub29(x[1][1], x[1][3])};
-        R29 b4[4] = {wa[0], wb[0], wa[1], wb[1]};
-#pragma unroll
-        for (int hh = 0; hh < 2; hh++) {
-          x[hh][0] = red2p29(add29(x[hh][0], x[hh][2]));
-          x[hh][1] = red2p29(add29(x[hh][1], x[hh][3]));
-        }
-        mul29tn<FrP, 4>(a4, b4, a4);
-        x[0][2] = a4[0];
-        x[0][3] = a4[1];
-        x[1][2] = a4[2];
-        x[1][3] = a4[3];
-        // stage (low bit): (0, 1) and (2, 3), both by wc
-        R29 c4[4] = {sub29(x[0][0], x[0][1]), sub29(x[0][2], x[0][3]), sub29(x[1][0], x[1][1]),
-                     sub29(x[1][2], x[1][3])};
-        R29 d4[4] = {wc[0], wc[0], wc[1], wc[1]};
-#pragma unroll
-        for (int hh = 0; hh < 2; hh++) {
-          x[hh][0] = red2p29(add29(x[hh][0], x[hh][1]));
-          x[hh][2] = red2p29(add29(x[hh][2], x[hh][3]));
-        }
-        mul29tn<FrP, 4>(c4, d4, c4);
-        x[0][1] = c4[0];
-        x[0][3] = c4[1];
-        x[1][1] = c4[2];
-        x[1][3] = c4[3];
-      } else {
-        // stage (low bit): (0, 1) and (2, 3), both by wc
-        R29 c4[4] = {x[0][1], x[0][3], x[1][1], x[1][3]};
-        R29 d4[4] = {wc[0], wc[0], wc[1], wc[1]};
-        mul29tn<FrP, 4>(c4, d4, c4);
-#pragma unroll
-        for (int hh = 0; hh < 2; hh++) {
-          const R29 t1 = c4[2 * hh], t3 = c4[2 * hh + 1];
-          x[hh][1] = red6p29(sub29(x[hh][0], t1));
-          x[hh][0] = red2p29(add29(x[hh][0], t1));
-          x[hh][3] = red6p29(sub29(x[hh][2], t3));
-          x[hh][2] = red2p29(add29(x[hh][2], t3));
-        }
-        // stage (high bit): (0, 2) by wa, (1, 3) by wb
-        R29 a4[4] = {x[0][2], x[0][3], x[1][2], x[1][3]};
-        R29 b4[4] = {wa[0], wb[0], wa[1], wb[1]};
-        mul29tn<FrP, 4>(a4, b4, a4);
-#pragma unroll
-        for (int hh = 0; hh < 2; hh++) {
-          const R29 t2 = a4[2 * hh], t3 = a4[2 * hh + 1];
-          x[hh][2] = red6p29(sub29(x[hh][0], t2));
-          x[hh][0] = red2p29(add29(x[hh][0], t2));
-          x[hh][3] = red6p29(sub29(x[hh][1], t3));
-          x[hh][1] = red2p29(add29(x[hh][1], t3));
-        }
-      }
-#pragma unroll
-      for (int hh = 0; hh < 2; hh++) {
-        if (hh && !two) break;
-#pragma unroll
-        for (int k = 0; k < 4; k++) lds_put29(sh, e[hh][k], x[hh][k]);
-      }
-    }
-    __syncthreads();
-  };
-  if (DIF) {
-    int b = B - 1;
-    if (B & 1) radix2(b--);
-    for (; b >= 1; b -= 2) radix4(b);
-  } else {
-    int b = 0;
-    for (; b + 1 < B; b += 2) radix4(b);
-    if (b < B) radix2(b);
-  }
-  for (int e = (int)tid; e < T; e += NTT_THREADS) {
-    const size_t i = base + ((size_t)(e >> lgL) << s0) + (e & (L - 1));
-    if (i >= win_lo && i < win_hi) out[i - win_lo] = from29(canon29(lds_get29(sh, e)));
-  }
+  return pyr;
 }
 
 // runs every pass in place on `a` (the first pass reads `in`), direction by DIF
 static void ntt_run(qg_ctx* ctx, bool dif, const Fr* in, size_t nin, Fr* a, const Fr* tw, int logn,
                     size_t win_lo, size_t win_hi, Fr* win_out) {
+  // QG_NTT_FLAT=1: twiddles from the flat table (A/B runs)
+  static const bool flat = [] {
+    const char* e = getenv("QG_NTT_FLAT");
+    return e && atoi(e) != 0;
+  }();
+  const Fr* pyr = flat ? tw : ntt_pyramid(ctx, tw, logn);
+  const int pmode = flat ? 0 : 1;
   std::vector<NttPass> plan = ntt_plan(logn);
   if (dif) std::reverse(plan.begin(), plan.end());
   const size_t n = (size_t)1 << logn;
@@ -560,24 +418,12 @@ static void ntt_run(qg_ctx* ctx, bool dif, const Fr* in, size_t nin, Fr* a, cons
     Fr* dst = last && win_out ? win_out : a;
     const size_t lo = last && win_out ? win_lo : 0, hi = last && win_out ? win_hi : n;
     const unsigned blocks = (unsigned)(n >> (P.B + P.lgL));
-    // radix-4 passes on full tiles (QG_NTT_R2=1: the radix-2 kernel, A/B runs)
-    static const bool r2 = [] {
-      const char* e = getenv("QG_NTT_R2");
-      return e && atoi(e) != 0;
-    }();
-    const bool r4 = !r2 && P.B + P.lgL == NTT_LGT && P.B >= 2;
-    if (dif && r4)
-      hipLaunchKernelGGL(k_ntt_pass4<true>, dim3(blocks), dim3(NTT_THREADS), 0, ctx->stream, src, ns,
-                         dst, tw, logn, P.s0, P.B, P.lgL, lo, hi);
-    else if (r4)
-      hipLaunchKernelGGL(k_ntt_pass4<false>, dim3(blocks), dim3(NTT_THREADS), 0, ctx->stream, src,
-                         ns, dst, tw, logn, P.s0, P.B, P.lgL, lo, hi);
-    else if (dif)
+    if (dif)
       hipLaunchKernelGGL(k_ntt_pass<true>, dim3(blocks), dim3(NTT_THREADS), 0, ctx->stream, src, ns,
-                         dst, tw, logn, P.s0, P.B, P.lgL, lo, hi);
+                         dst, pyr, pmode, logn, P.s0, P.B, P.lgL, lo, hi);
     else
       hipLaunchKernelGGL(k_ntt_pass<false>, dim3(blocks), dim3(NTT_THREADS), 0, ctx->stream, src,
-                         ns, dst, tw, logn, P.s0, P.B, P.lgL, lo, hi);
+                         ns, dst, pyr, pmode, logn, P.s0, P.B, P.lgL, lo, hi);
     QG_LAUNCH_CHECK();
   }
 }

@@ -600,11 +600,12 @@ QG_DEV uint4 msm_entries4(const uint32_t* __restrict__ entries, uint32_t e, uint
   return r;
 }
 
-// at most 128 VGPRs: four waves per SIMD (the paired multiplies need ~131)
-#ifndef QG_MSM_WPE
-#define QG_MSM_WPE 4
-#endif
-__global__ void __launch_bounds__(MSM_BLOCK) __attribute__((amdgpu_waves_per_eu(QG_MSM_WPE)))
+// at most 128 VGPRs: four waves per SIMD (the paired multiplies need ~131).
+// PF: the software-pipelined form (the row of entry e + 1 gathered before the
+// addition of entry e), three waves per SIMD: -1.5 % at 2^24 scalars, +3 % at
+// 2^20 (profiles/r04_msm_prefetch_ab.txt), so only the largest MSMs take it.
+template <bool PF>
+__global__ void __launch_bounds__(MSM_BLOCK) __attribute__((amdgpu_waves_per_eu(PF ? 3 : 4)))
     k_msm_accumulate(const MsmPt* __restrict__ table, const uint32_t* __restrict__ entries,
                      const uint32_t* __restrict__ bstart, uint32_t nb, uint32_t L,
                      X29Raw* __restrict__ partial, uint32_t* __restrict__ owner) {
@@ -627,9 +628,7 @@ __global__ void __launch_bounds__(MSM_BLOCK) __attribute__((amdgpu_waves_per_eu(
   // rows are canonical in the R = 2^261 domain, the signed digit picks y or p - y
   X29 acc;
   bool inf = true;
-#ifdef QG_MSM_PF
-  // software-pipelined variant (A/B): the row of entry e + 1 is gathered
-  // before the addition of entry e
+  if constexpr (PF) {
   uint4 g0 = msm_entries4(entries, e0, e1);
   uint4 g1 = e0 + 4 < e1 ? msm_entries4(entries, e0 + 4, e1) : g0;
   Q29 ax, ay;
@@ -671,7 +670,7 @@ __global__ void __launch_bounds__(MSM_BLOCK) __attribute__((amdgpu_waves_per_eu(
   }
   msm_flush(partial, owner, t + b, b, acc, inf);
   return;
-#endif
+  }
   // entries arrive four at a time (one 16-B load per group of four, the next
   // group in flight during the current one): a thread revisits its entry line
   // only every few microseconds, long after L2 has evicted it, so single-entry
@@ -1320,8 +1319,18 @@ static MsmRun msm_accumulate_phase(qg_ctx* ctx, const qg_srs* srs, const Fr* d_s
     QG_HIP(hipMemsetAsync(owner, 0xff, nslots * sizeof(uint32_t), ctx->stream));
     {
       QgTimed tm(ctx, "msm_accumulate");
-      hipLaunchKernelGGL(k_msm_accumulate, dim3(div_up(max_threads, MSM_BLOCK)), dim3(MSM_BLOCK),
-                         0, ctx->stream, srs->d_table, entries, bstart, nb, L, partial, owner);
+      // the prefetching form for the largest MSMs only (2^27+ entries: 2^24
+      // scalars x 13 windows); QG_MSM_PF=0/1 forces it (A/B runs)
+      bool pf = max_entries >= ((size_t)1 << 27);
+      if (const char* ov = getenv("QG_MSM_PF")) pf = atoi(ov) != 0;
+      if (pf)
+        hipLaunchKernelGGL(k_msm_accumulate<true>, dim3(div_up(max_threads, MSM_BLOCK)),
+                           dim3(MSM_BLOCK), 0, ctx->stream, srs->d_table, entries, bstart, nb, L,
+                           partial, owner);
+      else
+        hipLaunchKernelGGL(k_msm_accumulate<false>, dim3(div_up(max_threads, MSM_BLOCK)),
+                           dim3(MSM_BLOCK), 0, ctx->stream, srs->d_table, entries, bstart, nb, L,
+                           partial, owner);
       QG_LAUNCH_CHECK();
     }
     run.empty = n == 0;

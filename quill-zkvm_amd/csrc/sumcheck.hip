@@ -837,8 +837,7 @@ struct AllBufs {
 template <int K, int NP, bool PURE, bool PF>
 QG_DEV void sweep_pairs(const AllBufs& tb, uint32_t j, bool fold, const R29& r, size_t npairs,
                         size_t p0, size_t stride, const SopLds<NP>& sp, const SopHdr& h,
-                        bool skip0, R29 (&acc)[NP], uint32_t* dyn = nullptr,
-                        uint32_t* sh_chunk = nullptr) {
+                        bool skip0, R29 (&acc)[NP]) {
   const uint32_t nslots = h.nslots, np = h.np;
   uint32_t cnt = 0;
   if constexpr (PURE) {
@@ -904,34 +903,7 @@ QG_DEV void sweep_pairs(const AllBufs& tb, uint32_t j, bool fold, const R29& r, 
         cnt = 0;
       }
     };
-    {
-      // SC_BLOCK-pair chunks: chunk blockIdx + i G (the grid-stride sweep) for
-      // all but the last round of chunks, the rest handed out by one atomic
-      // counter per round (dyn): blocks on slower CUs take fewer (the static
-      // sweep's end times spread over ~30 % of the round).  dyn == nullptr:
-      // static throughout.
-      (void)p0;
-      (void)stride;
-      const size_t nch = (npairs + SC_BLOCK - 1) / SC_BLOCK, G = gridDim.x;
-      const size_t q = nch / G > 0 ? nch / G - 1 : 0;
-      const uint32_t tid = threadIdx.x;
-      for (size_t i = 0;; i++) {  // one call site of the pair body (code size)
-        size_t c;
-        if (dyn == nullptr || i < q) {
-          c = blockIdx.x + i * G;
-        } else {  // block-uniform branch
-          if (tid == 0)
-            *sh_chunk = (uint32_t)(q * G) + __hip_atomic_fetch_add((gu32*)dyn, 1u, __ATOMIC_RELAXED,
-                                                                    __HIP_MEMORY_SCOPE_AGENT);
-          __syncthreads();
-          c = *sh_chunk;
-          __syncthreads();
-        }
-        if (c >= nch) break;
-        const size_t p = c * SC_BLOCK + tid;
-        if (p < npairs) body(p);
-      }
-    }
+    for (size_t p = p0; p < npairs; p += stride) body(p);
 
   } else {
   for (size_t p = p0; p < npairs; p += stride) {
@@ -999,9 +971,8 @@ template <int K, int NP, bool PURE, bool PF, int WPE = 1>
 __global__ void __launch_bounds__(SC_BLOCK) __attribute__((amdgpu_waves_per_eu(WPE)))
     k_sc_big(AllBufs tb, uint32_t j, const SopDev* __restrict__ spg, SopHdr h, size_t npairs,
              RoundOut ro, int pending, Fr* __restrict__ loc, int skip0, uint64_t* __restrict__ acc_j,
-             uint64_t* __restrict__ acc_next, uint32_t* __restrict__ bar8, uint32_t* __restrict__ dyn) {
+             uint64_t* __restrict__ acc_next, uint32_t* __restrict__ bar8) {
   __shared__ SopLds<NP> sp;
-  __shared__ uint32_t sh_chunk;
   __shared__ R29 red[(SC_BLOCK / 64) * NP];
   __shared__ R29 res[NP];
   __shared__ FinSmem fs;
@@ -1047,7 +1018,7 @@ __global__ void __launch_bounds__(SC_BLOCK) __attribute__((amdgpu_waves_per_eu(W
 #pragma unroll
   for (int t = 0; t < NP; t++) acc[t] = R29::zero();
   sweep_pairs<K, NP, PURE, PF>(tb, j, fold, r, npairs, (size_t)blockIdx.x * SC_BLOCK + tid,
-                               (size_t)gridDim.x * SC_BLOCK, sp, h, skip0 != 0, acc, dyn, &sh_chunk);
+                               (size_t)gridDim.x * SC_BLOCK, sp, h, skip0 != 0, acc);
   if (blockIdx.x == 0) SC_TR(tr + 1);
   SC_TB(j, 1);
   SC_TW(j);
@@ -1412,24 +1383,9 @@ __global__ void __launch_bounds__(TAIL_BLOCK)
 // previous challenge runs on the last wave beside the other waves' evaluation.
 // ---------------------------------------------------------------------------
 static constexpr int SL_BLOCK = 256;
-// The block's slice lives in dynamic LDS, nslots x smax entries of 36 B, folded
-// in place.  smax (entries per slot) is the largest power of two whose slices
-// fit SL_LDS_BYTES: the more entries a slice holds, the earlier (larger table)
-// the tail takes over from the big-round launches (3 slots: 1024 entries, the
-// tail starts at 2^18-entry tables on 256 CUs).  After the regroups a slice
-// holds at most SL_RG entries per slot.
-static constexpr uint32_t SL_LDS_BYTES = 112 * 1024;
-static constexpr uint32_t SL_RG = 256;
-static constexpr uint32_t SL_SMAX_CAP = 1024;
-QG_HD constexpr uint32_t sl_smax(uint32_t nslots) {
-  uint32_t m = SL_SMAX_CAP;
-  const uint32_t ns = nslots ? nslots : 1;
-  while (m > SL_RG && (size_t)ns * m * 36 > SL_LDS_BYTES) m >>= 1;
-  return m;
-}
-static size_t sl_lds_bytes(uint32_t nslots, uint32_t smax) {
-  return (size_t)(nslots ? nslots : 1) * smax * 36;
-}
+// entries per slot of a block's slice in the first tail round (LDS: K slots x
+// 1.5 x SL_SMAX entries of 36 B: the slice and its half-size fold)
+QG_HD constexpr uint32_t sl_smax(int K) { return K <= 4 ? 256u : 128u; }
 
 template <int K, int NP>
 __global__ void __launch_bounds__(SL_BLOCK)
@@ -1438,8 +1394,9 @@ __global__ void __launch_bounds__(SL_BLOCK)
                uint64_t* __restrict__ acc_j0, uint32_t* __restrict__ bar8,
                uint64_t* __restrict__ acc64, Fr* __restrict__ final_vals,
                Fr* __restrict__ evaluation) {
-  extern __shared__ R29 Fbuf[];  // nslots x (entries per slot), stride S, folded in place
+  constexpr uint32_t SMAX = sl_smax(K);
   __shared__ SopLds<NP> sp;
+  __shared__ R29 Fbuf[K * SMAX * 3 / 2];
   __shared__ R29 red[(SL_BLOCK / 64) * NP];
   __shared__ R29 res[NP];
   __shared__ FinSmem fs;
@@ -1469,7 +1426,8 @@ __global__ void __launch_bounds__(SL_BLOCK)
 #pragma unroll
     for (int i = 0; i < 9; i++) r.l[i] = ro.st->r29[i];
   }
-  R29* const cur = Fbuf;  // slot stride S
+  R29* cur = Fbuf;                // slot stride S
+  R29* nxt = Fbuf + K * SMAX;     // slot stride S / 2
   // the block's slice of the round-j0 table (folded from the source by r_{j0-1})
   for (uint32_t it = tid; it < nslots * S; it += SL_BLOCK) {
     const uint32_t s = it / S, e = it % S;
@@ -1491,7 +1449,7 @@ __global__ void __launch_bounds__(SL_BLOCK)
     // ---- evaluate round j on the slice: thread (pair, point) items; the last
     // wave absorbs the previous challenge instead when one is pending
     // a round that regroups (below) publishes its slice before the barrier
-    const bool regroup = G > 1 && S <= SL_RG / 8;
+    const bool regroup = G > 1 && S <= SMAX / 8;
     if (regroup)
       for (uint32_t it = tid; it < nslots * S; it += SL_BLOCK) {
         const uint32_t s = it / S, e = it % S;
@@ -1547,7 +1505,7 @@ __global__ void __launch_bounds__(SL_BLOCK)
       // f blocks' round-j slices (published before the barrier) become one
       // block's round-(j+1) slice, folded on the load; the other blocks retire.
       // Fewer blocks: a cheaper barrier and fewer partial rows per round.
-      const uint32_t f = std::min<uint32_t>(G, 2 * SL_RG / S);
+      const uint32_t f = std::min<uint32_t>(G, 2 * SMAX / S);
       const uint32_t G2 = G / f;
       if (blk >= G2) return;
       const uint32_t S2 = f * S / 2;
@@ -1555,28 +1513,25 @@ __global__ void __launch_bounds__(SL_BLOCK)
         const uint32_t s = it / S2, e = it % S2;
         const Fr* src = gat.dst[s] + (size_t)blk * f * S + 2 * e;
         const R29 x0 = to29(ld_sc1(src)), x1 = to29(ld_sc1(src + 1));
-        cur[s * S2 + e] = red2p29<FrP>(add29(x0, mul29(sub29(x1, x0), r)));
+        Fbuf[s * S2 + e] = red2p29<FrP>(add29(x0, mul29(sub29(x1, x0), r)));
       }
       S = S2;
       G = G2;
+      cur = Fbuf + K * SMAX;  // swapped below: cur = Fbuf (S2 <= SMAX), nxt = the second array
+      nxt = Fbuf;
     } else {
-      // fold the slice by r_j in place: output it (slot s, entry e, it = s S/2 + e)
-      // reads entries 2 it and 2 it + 1 (slot stride S = 2 (S/2)).  Chunk k of
-      // SL_BLOCK outputs overwrites inputs of chunk k/2, so every thread reads
-      // its pair before any thread of the chunk writes (one barrier per chunk)
-      const uint32_t total = nslots * (S / 2);
-      for (uint32_t it0 = 0; it0 < total; it0 += SL_BLOCK) {
-        const uint32_t it = it0 + tid;
-        R29 x0 = R29::zero(), x1 = R29::zero();
-        if (it < total) {
-          x0 = cur[2 * it];
-          x1 = cur[2 * it + 1];
-        }
-        __syncthreads();
-        if (it < total) cur[it] = red2p29<FrP>(add29(x0, mul29(sub29(x1, x0), r)));
+      // fold the slice by r_j into the other array
+      const uint32_t h2 = S / 2;
+      for (uint32_t it = tid; it < nslots * h2; it += SL_BLOCK) {
+        const uint32_t s = it / h2, e = it % h2;
+        const R29 x0 = cur[s * S + 2 * e], x1 = cur[s * S + 2 * e + 1];
+        nxt[s * h2 + e] = red2p29<FrP>(add29(x0, mul29(sub29(x1, x0), r)));
       }
-      S = S / 2;
+      S = h2;
     }
+    R29* tmp = cur;
+    cur = nxt;
+    nxt = tmp;
     __syncthreads();
   }
   // final fold with r_{n-1} on the 32-bit path: one pair per slot left in cur (block 0)
@@ -1888,26 +1843,20 @@ static std::shared_ptr<const ScProgram> get_program(const qg_expr_op* prog, size
 // for the gfx950 SGPR admission rule of MI355X_MICROARCH.md "Residency").
 // Queried once per context and kernel instantiation.
 template <int K, int NP, bool SLICE = false>
-static unsigned persist_grid_cap(qg_ctx* ctx, size_t cus, size_t dyn_lds = 0) {
+static unsigned persist_grid_cap(qg_ctx* ctx, size_t cus) {
   const std::string key = std::string(SLICE ? "slice_occ_" : "persist_occ_") + std::to_string(K) +
-                          "_" + std::to_string(NP) + "_" + std::to_string(dyn_lds);
+                          "_" + std::to_string(NP);
   auto it = ctx->memo.find(key);
   int occ = 0;
   if (it == ctx->memo.end()) {
     const void* fn = SLICE ? reinterpret_cast<const void*>(&k_sc_slice<K, NP>)
                            : reinterpret_cast<const void*>(&k_sc_tail<K, NP>);
-    if (SLICE && dyn_lds > 64 * 1024)
-      QG_HIP(hipFuncSetAttribute(fn, hipFuncAttributeMaxDynamicSharedMemorySize, (int)dyn_lds));
-    QG_HIP(hipOccupancyMaxActiveBlocksPerMultiprocessor(&occ, fn, SLICE ? SL_BLOCK : TAIL_BLOCK,
-                                                        dyn_lds));
+    QG_HIP(hipOccupancyMaxActiveBlocksPerMultiprocessor(&occ, fn, SLICE ? SL_BLOCK : TAIL_BLOCK, 0));
     ctx->memo[key] = std::to_string(occ);
   } else {
     occ = std::stoi(it->second);
   }
   QG_CHECK(occ >= 1, QG_ERR_DEVICE, "persistent sumcheck kernel cannot be resident");
-  // the slice tail is launched cooperatively (co-residency guaranteed by the
-  // runtime or the launch fails): one block per CU
-  if (SLICE) return (unsigned)std::max<size_t>(1, cus);
   // bpc blocks per CU (QG_SC_TAIL_BPC, default 1), never more than the
   // occupancy answer minus one: a spare block slot per CU keeps the barrier
   // safe next to other kernels' blocks and under the gfx950 SGPR admission
@@ -1942,13 +1891,11 @@ static uint64_t* sumcheck_bacc0(uint32_t* bar, uint32_t nvars) {
 // The slice tail (k_sc_slice): G blocks, a power of two <= min(one per CU,
 // SMAX) so block 0 can gather one entry per block, each owning <= SMAX entries
 // per slot.  QG_SC_OLD_TAIL=1 keeps the streaming k_sc_tail (A/B runs).
-static constexpr size_t SL_GMAX = 256;  // two regroups of 16: 256 -> 16 -> 1 blocks
 template <int K, int NP>
-static size_t slice_gmax(qg_ctx* ctx, size_t cus, uint32_t nslots) {
+static size_t slice_gmax(qg_ctx* ctx, size_t cus) {
   const char* off = getenv("QG_SC_OLD_TAIL");  // read per call: tests toggle it in-process
   if (off && atoi(off) != 0) return 0;
-  const size_t gm = std::min<size_t>(
-      persist_grid_cap<K, NP, true>(ctx, cus, sl_lds_bytes(nslots, sl_smax(nslots))), SL_GMAX);
+  const size_t gm = std::min<size_t>(persist_grid_cap<K, NP, true>(ctx, cus), sl_smax(K));
   size_t G = 1;
   while (G * 2 <= gm) G *= 2;
   return G;
@@ -1956,11 +1903,11 @@ static size_t slice_gmax(qg_ctx* ctx, size_t cus, uint32_t nslots) {
 
 // largest round table (entries per slot) the slice tail can start from
 template <int K, int NP>
-static uint32_t slice_tail_log(qg_ctx* ctx, size_t cus, uint32_t nslots) {
-  const size_t g = slice_gmax<K, NP>(ctx, cus, nslots);
+static uint32_t slice_tail_log(qg_ctx* ctx, size_t cus) {
+  const size_t g = slice_gmax<K, NP>(ctx, cus);
   if (!g) return 0;
   uint32_t l = 0;
-  while (((size_t)1 << (l + 1)) <= g * sl_smax(nslots)) l++;
+  while (((size_t)1 << (l + 1)) <= g * sl_smax(K)) l++;
   return l;
 }
 
@@ -1970,16 +1917,12 @@ template <int K, int NP>
 static bool launch_slice_tail(qg_ctx* ctx, size_t cus, TablePtrs t0, const SopDev* d_sp, SopHdr h,
                               uint32_t nvars, uint32_t j0, int fold0, int pending0, RoundOut ro,
                               uint32_t* bar, uint64_t* acc_j0, Fr* d_final, Fr* d_eval) {
-  const size_t gm = slice_gmax<K, NP>(ctx, cus, h.nslots);
+  const size_t gm = slice_gmax<K, NP>(ctx, cus);
   if (!gm) return false;
   const size_t n0 = (size_t)1 << (nvars - j0);
   size_t G = 1;
   while (G * 2 <= gm && G * 2 <= n0 / 2) G *= 2;
-  const uint32_t smax = sl_smax(h.nslots);
-  if (n0 / G > smax) return false;
-  // per-slot capacity: the first slice, or a regrouped one (<= SL_RG entries)
-  const size_t lds = sl_lds_bytes(h.nslots, (uint32_t)std::max<size_t>(n0 / G, std::min<size_t>(SL_RG, n0)));
-  (void)persist_grid_cap<K, NP, true>(ctx, cus, lds);  // sets the dynamic-LDS attribute
+  if (n0 / G > sl_smax(K)) return false;
   uint64_t* acc64 = ctx->scratch_as<uint64_t>("sc_sacc", (size_t)std::max<uint32_t>(1, nvars - j0) * 8 * NP * 9);
   // the 8 barrier shards follow the per-round counters (zeroed by the per-call
   // header copy): sumcheck_bar8
@@ -1989,13 +1932,10 @@ static bool launch_slice_tail(qg_ctx* ctx, size_t cus, TablePtrs t0, const SopDe
   Fr* sg = ctx->scratch_as<Fr>("sc_sgat", (size_t)ns * n0);
   TablePtrs gat{};
   for (uint32_t i = 0; i < 8; i++) gat.dst[i] = i < h.nslots ? sg + (size_t)i * n0 : nullptr;
-  // cooperative launch: the grid barrier's co-residency is the runtime's
-  // guarantee (the launch fails rather than deadlock beside other work)
-  void* args[] = {&t0, &gat, (void*)&d_sp, &h, &nvars, &j0, &fold0, &pending0, &ro,
-                  &acc_j0, &bar8, &acc64, &d_final, &d_eval};
-  QG_HIP(hipLaunchCooperativeKernel(reinterpret_cast<const void*>(&k_sc_slice<K, NP>),
-                                    dim3((unsigned)G), dim3(SL_BLOCK), args, (unsigned)lds,
-                                    ctx->stream));
+  hipLaunchKernelGGL((k_sc_slice<K, NP>), dim3((unsigned)G), dim3(SL_BLOCK), 0, ctx->stream, t0,
+                     gat, d_sp, h, nvars, j0, fold0, pending0, ro, acc_j0, bar8, acc64, d_final,
+                     d_eval);
+  QG_LAUNCH_CHECK();
   return true;
 }
 
@@ -2015,8 +1955,7 @@ static unsigned sc_big_blocks(qg_ctx* ctx, size_t npairs) {
 template <int K, int NP>
 static int launch_big(qg_ctx* ctx, const std::vector<const Fr*>& src, Fr* X, Fr* Y, size_t N,
                        uint32_t j, const SopDev* d_sp, SopHdr h, size_t npairs, RoundOut ro,
-                       int pending, Fr* loc, uint64_t* a0, uint64_t* a1, uint32_t* bar8,
-                       uint32_t* dyn = nullptr) {
+                       int pending, Fr* loc, uint64_t* a0, uint64_t* a1, uint32_t* bar8) {
   // rounds j >= 1: h(0) = h_{j-1}(r_{j-1}) - h(1), exact by construction (the
   // folded table's pair sums ARE the previous message at r); round 0 evaluates
   // every point, so a wrong caller claim still yields the reference's bytes.
@@ -2040,19 +1979,19 @@ static int launch_big(qg_ctx* ctx, const std::vector<const Fr*>& src, Fr* X, Fr*
   if (pure && wpe4)
     hipLaunchKernelGGL((k_sc_big<K, 4, true, false, 4>), dim3(blocks), dim3(SC_BLOCK), 0,
                        ctx->stream, tb, j, d_sp, h, npairs, ro, pending, loc, skip0, (j & 1) ? a1 : a0,
-                       (j & 1) ? a0 : a1, bar8, dyn);
+                       (j & 1) ? a0 : a1, bar8);
   else if (pure && pf)
     hipLaunchKernelGGL((k_sc_big<K, 4, true, true>), dim3(blocks), dim3(SC_BLOCK), 0, ctx->stream,
                        tb, j, d_sp, h, npairs, ro, pending, loc, skip0, (j & 1) ? a1 : a0,
-                       (j & 1) ? a0 : a1, bar8, dyn);
+                       (j & 1) ? a0 : a1, bar8);
   else if (pure)
     hipLaunchKernelGGL((k_sc_big<K, 4, true, false>), dim3(blocks), dim3(SC_BLOCK), 0, ctx->stream,
                        tb, j, d_sp, h, npairs, ro, pending, loc, skip0, (j & 1) ? a1 : a0,
-                       (j & 1) ? a0 : a1, bar8, dyn);
+                       (j & 1) ? a0 : a1, bar8);
   else
     hipLaunchKernelGGL((k_sc_big<4, 4, false, false>), dim3(blocks), dim3(SC_BLOCK), 0, ctx->stream,
                        tb, j, d_sp, h, npairs, ro, pending, loc, skip0, (j & 1) ? a1 : a0,
-                       (j & 1) ? a0 : a1, bar8, dyn);
+                       (j & 1) ? a0 : a1, bar8);
   QG_LAUNCH_CHECK();
   return skip0;
 }
@@ -2093,13 +2032,13 @@ static uint32_t run_rounds(qg_ctx* ctx, uint32_t nvars, const std::vector<const 
   // QG_SC_PERS_LOG overrides where the persistent tail takes over (tuning)
   static const int pers_log = [] {
     const char* e = getenv("QG_SC_PERS_LOG");
-    return e ? atoi(e) : 64;  // default: the slice tail takes over as early as its LDS allows
+    return e ? atoi(e) : PERS_LOG;
   }();
   {
     QgTimed tm(ctx, "sumcheck_round");
     // the slice tail starts once a round's table fits the blocks' LDS slices
-    const uint32_t sl = slice_tail_log<K, NP>(ctx, ctx->num_cus(), nslots);
-    const int plog = sl ? std::min<int>(pers_log, (int)sl) : PERS_LOG;
+    const uint32_t sl = slice_tail_log<K, NP>(ctx, ctx->num_cus());
+    const int plog = sl ? std::min<int>(pers_log, (int)sl) : pers_log;
     for (; j < nvars; j++) {
       const size_t table = N >> j;  // entries per table evaluated in round j
       if (table <= ((size_t)1 << plog)) break;
@@ -2109,13 +2048,8 @@ static uint32_t run_rounds(qg_ctx* ctx, uint32_t nvars, const std::vector<const 
         const TablePtrs& d = parity ? tY : tX;
         for (int i = 0; i < 8; i++) tp.dst[i] = d.dst[i];
       }
-      // the round's dynamic chunk counter: round j's barrier counter (zeroed
-      // per call; k_sc_tail only uses those of its own rounds).  QG_SC_NODYN=1:
-      // the static grid-stride sweep (A/B runs)
-      const char* nodyn = getenv("QG_SC_NODYN");
-      uint32_t* dyn = (nodyn && atoi(nodyn) != 0) ? nullptr : bar + j;
       if (launch_big<K, NP>(ctx, src, X, Y, N, j, d_sp, h, npairs, ro, pending, nullptr, a0, a1,
-                            bar8, dyn) < 0) {
+                            bar8) < 0) {
         hipLaunchKernelGGL((k_sc_round<K, NP>), dim3(sc_round_blocks(ctx, npairs)), dim3(SC_BLOCK),
                            0, ctx->stream, tp, d_sp, h, npairs, fold, ro, j, pending, partial,
                            (Fr*)nullptr);

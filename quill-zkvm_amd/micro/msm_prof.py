@@ -26,11 +26,16 @@ def main():
     sizes = [int(x) for x in sys.argv[2].split(",")] if len(sys.argv) > 2 else [lmax]
     reps = int(sys.argv[3]) if len(sys.argv) > 3 else 3
     dev = q.Device(0)
-    srs = q.Srs.generate(dev, TAU, 1 << lmax)
+    own = os.environ.get("MSM_PROF_OWN_SRS") == "1"  # an SRS per size (its own window bits)
+    srs = None if own else q.Srs.generate(dev, TAU, 1 << lmax)
     scalars = q.DeviceVec(dev, 1 << lmax).fill_random(0x5155494C4C + 2)
     oc.lib()
     for lg in sizes:
         n = 1 << lg
+        if own:
+            if srs is not None:
+                srs.close()
+            srs = q.Srs.generate(dev, TAU, n)
         srs.msm_dev(scalars, n)  # warm
         dev.enable_timing(True)
         t0 = time.perf_counter()
@@ -42,7 +47,7 @@ def main():
         dev.enable_timing(False)
         v = oc.fr_horner(scalars.to_numpy(n), TAU)
         ok = oc.g1_mul((1, 2), v) == res
-        print(f"2^{lg}: {dt * 1e3:.3f} ms/msm  " +
+        print(f"2^{lg}: {dt * 1e3:.3f} ms/msm  c={srs.window_info()[0]}  " +
               "  ".join(f"{k} {v:.3f}" for k, v in parts.items()) + f"  verified={ok}",
               flush=True)
         assert ok
