@@ -444,9 +444,13 @@ def hbm_by_kernel(pmc, top=8):
     if not isinstance(pmc, dict) or "error" in pmc:
         return None
     sel = "#" if any("#" in k for k in pmc) else None  # older probes: whole-kernel keys
+    # the probe's hot-path legs only: not its setup (SRS generation before the
+    # first marker, "#pre") nor the FETCH_SIZE calibration launches
+    skip_legs = ("#pre", "#probe_cal")
     rows = [(k, d) for k, d in pmc.items()
             if not k.startswith("_") and isinstance(d, dict) and "hbm_gbps" in d
-            and (("#" in k) if sel else ("@" not in k))]
+            and (("#" in k and not k.endswith(skip_legs) and not k.startswith(("k_srs_", "k_fb_")))
+                 if sel else ("@" not in k))]
     rows.sort(key=lambda kd: -kd[1]["avg_us"] * kd[1].get("launches", 1))
     return {k: [_sig(d["hbm_gbps"], 3), _sig(d["frac_hbm_peak"], 3), _sig(d["avg_us"], 4)]
             for k, d in rows[:top]}

@@ -1229,6 +1229,14 @@ static MsmRun msm_accumulate_phase(qg_ctx* ctx, const qg_srs* srs, const Fr* d_s
     } else {
       int elog = max_entries >= ((size_t)1 << 27) ? 7 : 6;
       while (elog > 2 && (max_entries >> elog) < (size_t)ctx->num_cus() * 16 * 64 * 3) elog--;
+      // but at most ~4 chunks per bucket: below that the reduction's slot
+      // merges cost more than the accumulation gains from the extra threads
+      // (own-SRS MSMs, profiles/r04_msm_small_elog.txt: 2^20 / 2^18 / 2^16 at
+      // c = 17 / 16 / 15 take 1.73 / 1.09 / 0.73 ms with the thread rule alone,
+      // 1.69 / 0.87 / 0.69 ms with 64 / 32 / 32 entries per chunk)
+      int emin = 0;
+      while (emin < 7 && ((size_t)1 << emin) * 4 * nb < max_entries) emin++;
+      elog = std::max(elog, emin);
       L = 1u << elog;
     }
     if (const char* ov = getenv("QG_MSM_ELOG")) L = 1u << atoi(ov);  // tuning experiments
