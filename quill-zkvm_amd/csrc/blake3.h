@@ -381,43 +381,6 @@ QG_DEV void b3_compress_quad(uint32_t l, uint32_t cvl, uint32_t cvh, const uint3
 // BLAKE3 of a word message in LDS (<= 1024 bytes; bytes past nbytes up to the
 // next 64-byte boundary must be zero), root output words [0, nout) (nout <= 16)
 // written to out (LDS or global) by lanes 0..3.  Call with the whole wave.
-// The same hash continued from block b0 with this lane's chaining words
-// (cvl, cvh) after blocks [0, b0) (b3_block0_quad gives them for b0 = 1).
-QG_DEV void b3_hash_quad_from(uint32_t cvl, uint32_t cvh, uint32_t b0, const uint32_t* msg,
-                              uint32_t nbytes, uint32_t* out, int nout) {
-  const uint32_t lane = __lane_id(), l = lane & 3;
-  const uint32_t nblocks = nbytes ? (nbytes + 63) / 64 : 1;
-  for (uint32_t bi = b0; bi < nblocks; bi++) {
-    uint32_t m[16];
-#pragma unroll
-    for (int i = 0; i < 16; i++) m[i] = msg[bi * 16 + i];
-    const bool last = bi + 1 == nblocks;
-    const uint32_t blen = last ? nbytes - bi * 64 : 64u;
-    const uint32_t flags = (bi == 0 ? B3_CHUNK_START : 0u) | (last ? (B3_CHUNK_END | B3_ROOT) : 0u);
-    uint32_t o0, o1, o2, o3;
-    b3_compress_quad(l, cvl, cvh, m, 0, blen, flags, o0, o1, o2, o3);
-    if (!last) {
-      cvl = o0;
-      cvh = o1;
-    } else if (lane < 4) {
-      if ((int)l < nout) out[l] = o0;
-      if ((int)(4 + l) < nout) out[4 + l] = o1;
-      if ((int)(8 + l) < nout) out[8 + l] = o2;
-      if ((int)(12 + l) < nout) out[12 + l] = o3;
-    }
-  }
-}
-
-// First block (64 message words m, more blocks follow) of a one-chunk hash:
-// this lane's chaining words after it.
-QG_DEV void b3_block0_quad(const uint32_t (&m)[16], uint32_t& cvl, uint32_t& cvh) {
-  const uint32_t l = __lane_id() & 3;
-  const uint32_t il = b3_pick4(l, 0x6A09E667u, 0xBB67AE85u, 0x3C6EF372u, 0xA54FF53Au);
-  const uint32_t ih = b3_pick4(l, 0x510E527Fu, 0x9B05688Cu, 0x1F83D9ABu, 0x5BE0CD19u);
-  uint32_t o2, o3;
-  b3_compress_quad(l, il, ih, m, 0, 64u, B3_CHUNK_START, cvl, cvh, o2, o3);
-}
-
 QG_DEV void b3_hash_quad(const uint32_t* msg, uint32_t nbytes, uint32_t* out, int nout) {
   const uint32_t lane = __lane_id(), l = lane & 3;
   uint32_t cvl = b3_pick4(l, 0x6A09E667u, 0xBB67AE85u, 0x3C6EF372u, 0xA54FF53Au);

@@ -488,7 +488,6 @@ struct FinSmem {
   uint32_t chin[16];  // state' || "challenge" || zero pad
   uint32_t xof[16];   // B3-XOF(state' || "challenge")[0..64)
   uint32_t ab[32];    // state' || challenge bytes || zero pad (absorb)
-  uint32_t cv1[8];    // chaining value after the absorb's first block (wave 1)
   R29 r;              // the round challenge * 2^261 (fold multiplier)
   Fr r256;            // the round challenge (Montgomery, R = 2^256)
 };
@@ -516,49 +515,15 @@ QG_DEV void finish_core(const SopLds<NP>& sp, uint32_t np, const R29* ev, const 
   // canonical coefficients (transcript bytes) first; the Montgomery ones (proof
   // output) after the challenge.  Lazy sums: <= 4 terms < 2p per lane, U <= 8
   // lanes: < 64p before the one reduction.
-  // Wave 1 repeats coefficient 0's lanes (bit-identical arithmetic) and runs
-  // the absorb's first BLAKE3 block (state || len || c0[0..24)) beside wave
-  // 0's interpolation, betting on an untrimmed message (len = np); wave 0
-  // continues from that chaining value when the bet holds.
-#ifndef QG_SC_NO_EARLY
-  const bool w1 = tid >= 64 && tid < 64 + U;
-#else
-  const bool w1 = false;
-#endif
   R29 cc = R29::zero();
-  if ((w0 && ct < np) || w1) {
-    const uint32_t c = w1 ? 0u : ct, uu = w1 ? tid - 64 : cu;
-    for (uint32_t u = uu; u < np; u += U) cc = add29(cc, mul29(sp.vc[c * NP + u], ev[u]));
+  if (w0 && ct < np) {
+    for (uint32_t u = cu; u < np; u += U) cc = add29(cc, mul29(sp.vc[ct * NP + u], ev[u]));
   }
   cc = norm29(cc);
 #pragma unroll
   for (uint32_t m = 1; m < U; m <<= 1) cc = norm29(add29(cc, shfl_xor29(cc, m)));
   // U <= 8 products < 2p each: < 16p
   const Fr ccw = from29(canon29(red16p29<FrP>(cc)));
-#ifndef QG_SC_NO_EARLY
-  if (tid >= 64 && tid < 128) {
-    const uint32_t c0w0 = __shfl(ccw.v[0], 0, 64), c0w1 = __shfl(ccw.v[1], 0, 64),
-                   c0w2 = __shfl(ccw.v[2], 0, 64), c0w3 = __shfl(ccw.v[3], 0, 64),
-                   c0w4 = __shfl(ccw.v[4], 0, 64), c0w5 = __shfl(ccw.v[5], 0, 64);
-    uint32_t m[16];
-#pragma unroll
-    for (int i = 0; i < 8; i++) m[i] = state_in[i];
-    m[8] = np;
-    m[9] = 0;
-    m[10] = c0w0;
-    m[11] = c0w1;
-    m[12] = c0w2;
-    m[13] = c0w3;
-    m[14] = c0w4;
-    m[15] = c0w5;
-    uint32_t cvl, cvh;
-    b3_block0_quad(m, cvl, cvh);
-    if (tid < 68) {
-      fs.cv1[tid - 64] = cvl;
-      fs.cv1[tid - 60] = cvh;
-    }
-  }
-#endif
   const bool lead = w0 && cu == 0 && ct < np;
   if (writer && canon_out && lead) ro.coeffs[(size_t)j * ro.width + ct] = ccw;
   if (writer) {
@@ -584,19 +549,8 @@ QG_DEV void finish_core(const SopLds<NP>& sp, uint32_t np, const R29* ev, const 
   if (tid >= 11 && tid < 16) fs.chin[tid] = 0;
   SC_TR(tr + 3);
   __syncthreads();
-  // state' = B3(state || len || coefficients): from wave 1's first block when
-  // the message was not trimmed (the first block then matches its bet)
-  if (w0) {
-#ifndef QG_SC_NO_EARLY
-    if (len == np && np >= 1) {
-      const uint32_t l = tid & 3;
-      b3_hash_quad_from(fs.cv1[l], fs.cv1[4 + l], 1, fs.msg, 40 + 32 * len, fs.chin, 8);
-    } else
-#endif
-    {
-      b3_hash_quad(fs.msg, 40 + 32 * len, fs.chin, 8);
-    }
-  }
+  // state' = B3(state || len || coefficients)
+  if (w0) b3_hash_quad(fs.msg, 40 + 32 * len, fs.chin, 8);
   __syncthreads();
   SC_TR(tr + 4);
   // challenge bytes = B3-XOF(state' || "challenge")[0..48)
