@@ -1166,7 +1166,13 @@ struct MsmRun {
   uint32_t* owner = nullptr;
   uint32_t* bstart = nullptr;
   uint32_t* misc = nullptr;  // [0] nchunks, [1] max accumulation threads per bucket
+  // misc[1..3] copied to pinned host memory right after the bucket scan, and
+  // its event: the reduction's launch plan waits for the bucketing only, so
+  // its kernels are queued while the accumulation still runs
+  const uint32_t* h_mx = nullptr;
+  hipEvent_t ev_mx = nullptr;
 };
+static constexpr int MSM_MAX_BATCH = 1024;
 
 // bucketing (two-pass radix sort) + bucket accumulation of MSM `slot` of a
 // batch: sum_i d_scalars[i] * base[srs_off + i]
@@ -1315,6 +1321,16 @@ static MsmRun msm_accumulate_phase(qg_ctx* ctx, const qg_srs* srs, const Fr* d_s
       hipLaunchKernelGGL(k_scan_add, dim3(div_up(nb, 256)), dim3(256), 0, ctx->stream, tile_tot,
                          (size_t)nb, bstart, tstart, cursor, counts, L, T, misc);
       QG_LAUNCH_CHECK();
+      {
+        QG_CHECK(slot >= 0 && slot < MSM_MAX_BATCH, QG_ERR_UNSUPPORTED, "MSM batch too large");
+        uint32_t* hmx =
+            reinterpret_cast<uint32_t*>(ctx->pinned_get("msm_mx", MSM_MAX_BATCH * 4 * sizeof(uint32_t)));
+        QG_HIP(hipMemcpyAsync(hmx + 4 * slot, misc + 1, 3 * sizeof(uint32_t), hipMemcpyDeviceToHost,
+                              ctx->stream));
+        run.ev_mx = ctx->ev_get();
+        QG_HIP(hipEventRecord(run.ev_mx, ctx->stream));
+        run.h_mx = hmx + 4 * slot;
+      }
       hipLaunchKernelGGL(k_sort_chunk_offsets, dim3(div_up(nb, 256)), dim3(256), 0, ctx->stream,
                          cbase, chist, LO, nb, bstart, coff);
       QG_LAUNCH_CHECK();
@@ -1366,19 +1382,25 @@ static void msm_reduce_phase(qg_ctx* ctx, const qg_srs* srs, const std::vector<M
   for (uint32_t i = 0; i < k; i++)
     if (!runs[i].empty) live.push_back(i);
   if (live.empty()) return;
-  QG_CHECK(live.size() <= 1024, QG_ERR_UNSUPPORTED, "MSM batch too large");
+  QG_CHECK(live.size() <= (size_t)MSM_MAX_BATCH, QG_ERR_UNSUPPORTED, "MSM batch too large");
   const uint32_t kl = (uint32_t)live.size();
   const uint32_t nb = 1u << (srs->c - 1);
-  // per MSM (one transfer): max accumulation threads per bucket, and the
-  // partial-slot range of the buckets the tree steps pre-sum
-  uint32_t* d_mx = ctx->scratch_as<uint32_t>("msm_maxtpb", 3 * (size_t)kl);
-  for (uint32_t q = 0; q < kl; q++)
-    QG_HIP(hipMemcpyAsync(d_mx + 3 * q, runs[live[q]].misc + 1, 3 * sizeof(uint32_t),
-                          hipMemcpyDeviceToDevice, ctx->stream));
+  // per MSM: max accumulation threads per bucket, and the partial-slot range of
+  // the buckets the tree steps pre-sum, from the pinned copies queued after
+  // each bucket scan (waiting on those events only: the accumulations keep
+  // running while the reduction's kernels are queued behind them)
   std::vector<uint32_t> mx(3 * (size_t)kl);
-  QG_HIP(hipMemcpyAsync(mx.data(), d_mx, 3 * kl * sizeof(uint32_t), hipMemcpyDeviceToHost,
-                        ctx->stream));
-  QG_HIP(hipStreamSynchronize(ctx->stream));
+  // QG_MSM_SYNC_PLAN=1: wait for the whole stream first (the round-3 timing, A/B runs)
+  if (const char* ov = getenv("QG_MSM_SYNC_PLAN"))
+    if (atoi(ov) != 0) QG_HIP(hipStreamSynchronize(ctx->stream));
+  for (uint32_t q = 0; q < kl; q++) {
+    const MsmRun& r = runs[live[q]];
+    QG_CHECK(r.ev_mx && r.h_mx, QG_ERR_ASSERT, "MSM run without its bucket-scan event");
+    QG_HIP(hipEventSynchronize(r.ev_mx));
+    for (int i = 0; i < 3; i++) mx[3 * q + i] = r.h_mx[i];
+  }
+  for (const MsmRun& r : runs)
+    if (r.ev_mx) ctx->event_pool.push_back(r.ev_mx);
   // level 1: S = 2^slog1 buckets per thread, as many threads as the chip has
   // SIMD lanes (one wave per SIMD) over the whole batch; folds of 2^gl1 lanes
   const size_t lanes = (size_t)ctx->num_cus() * 4 * 64;

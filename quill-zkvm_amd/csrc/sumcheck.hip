@@ -1974,18 +1974,12 @@ static int launch_big(qg_ctx* ctx, const std::vector<const Fr*>& src, Fr* X, Fr*
   const unsigned blocks = sc_big_blocks(ctx, npairs);
   // QG_SC_PF=1: next slot's entries prefetched during the current slot (tuning)
   static const bool pf = getenv("QG_SC_PF") != nullptr;
-  // QG_SC_WPE=3 / 4: the product sweep compiled for 3 / 4 waves per SIMD
-  // (<= 168 / 128 VGPRs; tuning)
-  static const int wpe = [] {
-    const char* e = getenv("QG_SC_WPE");
-    return e ? atoi(e) : 1;
-  }();
-  if (pure && wpe == 4)
+  // QG_SC_WPE=4: the product sweep compiled for 4 waves per SIMD (<= 128 VGPRs,
+  // spills; tuning.  3 waves measured too: 0.214 -> 0.288 ms of big rounds,
+  // profiles/r04_sumcheck_wpe_blocks_ab.txt)
+  static const bool wpe4 = getenv("QG_SC_WPE") != nullptr;
+  if (pure && wpe4)
     hipLaunchKernelGGL((k_sc_big<K, 4, true, false, 4>), dim3(blocks), dim3(SC_BLOCK), 0,
-                       ctx->stream, tb, j, d_sp, h, npairs, ro, pending, loc, skip0, (j & 1) ? a1 : a0,
-                       (j & 1) ? a0 : a1, bar8);
-  else if (pure && wpe == 3)
-    hipLaunchKernelGGL((k_sc_big<K, 4, true, false, 3>), dim3(blocks), dim3(SC_BLOCK), 0,
                        ctx->stream, tb, j, d_sp, h, npairs, ro, pending, loc, skip0, (j & 1) ? a1 : a0,
                        (j & 1) ? a0 : a1, bar8);
   else if (pure && pf)
