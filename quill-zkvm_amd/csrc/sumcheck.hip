@@ -842,13 +842,18 @@ QG_DEV void sweep_pairs(const AllBufs& tb, uint32_t j, bool fold, const R29& r, 
   uint32_t cnt = 0;
   if constexpr (PURE) {
     // one pair: fold the slots, multiply the points, accumulate lazily
+    // PF: the entries of the next slot (and, after the last slot, of the next
+    // pair's slot 0) are in flight during the current slot's arithmetic
+    Fr w[4], wn[4];
+    if constexpr (PF)
+      if (p0 < npairs) load_pair(tb.src(j, 0) + (fold ? 4 : 2) * p0, fold, w);
     auto body = [&](size_t p) {
       R29 prod[NP];
-      Fr w[4], wn[4];
-      if constexpr (PF) load_pair(tb.src(j, 0) + (fold ? 4 : 2) * p, fold, w);
       for (uint32_t s = 0; s < nslots; s++) {
         if constexpr (PF) {
           if (s + 1 < nslots) load_pair(tb.src(j, s + 1) + (fold ? 4 : 2) * p, fold, wn);
+          else if (p + stride < npairs)
+            load_pair(tb.src(j, 0) + (fold ? 4 : 2) * (p + stride), fold, wn);
         } else {
           load_pair(tb.src(j, s) + (fold ? 4 : 2) * p, fold, w);
         }
