@@ -834,7 +834,7 @@ struct AllBufs {
   QG_DEV Fr* dst(uint32_t j, uint32_t s) const { return (j & 1) ? X + capX * s : Y + capY * s; }
 };
 
-template <int K, int NP, bool PURE, bool PF>
+template <int K, int NP, bool PURE>
 QG_DEV void sweep_pairs(const AllBufs& tb, uint32_t j, bool fold, const R29& r, size_t npairs,
                         size_t p0, size_t stride, const SopLds<NP>& sp, const SopHdr& h,
                         bool skip0, R29 (&acc)[NP]) {
@@ -842,21 +842,14 @@ QG_DEV void sweep_pairs(const AllBufs& tb, uint32_t j, bool fold, const R29& r, 
   uint32_t cnt = 0;
   if constexpr (PURE) {
     // one pair: fold the slots, multiply the points, accumulate lazily
-    // PF: the entries of the next slot (and, after the last slot, of the next
-    // pair's slot 0) are in flight during the current slot's arithmetic
-    Fr w[4], wn[4];
-    if constexpr (PF)
-      if (p0 < npairs) load_pair(tb.src(j, 0) + (fold ? 4 : 2) * p0, fold, w);
+    // (prefetching the next slot's and the next pair's entries during the
+    // current slot was measured slower: +14 us over the big rounds at 2^20,
+    // profiles/r04_sumcheck_prefetch_ab.txt)
     auto body = [&](size_t p) {
       R29 prod[NP];
+      Fr w[4];
       for (uint32_t s = 0; s < nslots; s++) {
-        if constexpr (PF) {
-          if (s + 1 < nslots) load_pair(tb.src(j, s + 1) + (fold ? 4 : 2) * p, fold, wn);
-          else if (p + stride < npairs)
-            load_pair(tb.src(j, 0) + (fold ? 4 : 2) * (p + stride), fold, wn);
-        } else {
-          load_pair(tb.src(j, s) + (fold ? 4 : 2) * p, fold, w);
-        }
+        load_pair(tb.src(j, s) + (fold ? 4 : 2) * p, fold, w);
         R29 lo, hi;
         fold_pair(w, fold, r, tb.dst(j, s) + 2 * p, lo, hi);
         const R29 d = norm29(sub29(hi, lo));
@@ -892,10 +885,6 @@ QG_DEV void sweep_pairs(const AllBufs& tb, uint32_t j, bool fold, const R29& r, 
             else
               prod[t] = mul29t(prod[t], at_point_lazy<NP>(lo, d, t, sp));
           }
-        }
-        if constexpr (PF) {
-#pragma unroll
-          for (int i = 0; i < 4; i++) w[i] = wn[i];
         }
       }
       // products of >= 2 factors are < 4p: three lazy additions stay below 16p
@@ -972,7 +961,7 @@ QG_DEV void sweep_pairs(const AllBufs& tb, uint32_t j, bool fold, const R29& r, 
 // (sweep_pairs), per-block partial rows, and the last block to publish
 // (ticket election) sums the rows and runs the transcript step (or, sharded,
 // writes this rank's local sums).
-template <int K, int NP, bool PURE, bool PF, int WPE = 1>
+template <int K, int NP, bool PURE, int WPE = 1>
 __global__ void __launch_bounds__(SC_BLOCK) __attribute__((amdgpu_waves_per_eu(WPE)))
     k_sc_big(AllBufs tb, uint32_t j, const SopDev* __restrict__ spg, SopHdr h, size_t npairs,
              RoundOut ro, int pending, Fr* __restrict__ loc, int skip0, uint64_t* __restrict__ acc_j,
@@ -1022,7 +1011,7 @@ __global__ void __launch_bounds__(SC_BLOCK) __attribute__((amdgpu_waves_per_eu(W
   R29 acc[NP];
 #pragma unroll
   for (int t = 0; t < NP; t++) acc[t] = R29::zero();
-  sweep_pairs<K, NP, PURE, PF>(tb, j, fold, r, npairs, (size_t)blockIdx.x * SC_BLOCK + tid,
+  sweep_pairs<K, NP, PURE>(tb, j, fold, r, npairs, (size_t)blockIdx.x * SC_BLOCK + tid,
                                (size_t)gridDim.x * SC_BLOCK, sp, h, skip0 != 0, acc);
   if (blockIdx.x == 0) SC_TR(tr + 1);
   SC_TB(j, 1);
@@ -1977,26 +1966,20 @@ static int launch_big(qg_ctx* ctx, const std::vector<const Fr*>& src, Fr* X, Fr*
   tb.capX = N / 2;
   tb.capY = std::max<size_t>(1, N / 4);
   const unsigned blocks = sc_big_blocks(ctx, npairs);
-  // QG_SC_PF=1: next slot's entries prefetched during the current slot (tuning)
-  static const bool pf = getenv("QG_SC_PF") != nullptr;
   // QG_SC_WPE=4: the product sweep compiled for 4 waves per SIMD (<= 128 VGPRs,
   // spills; tuning.  3 waves measured too: 0.214 -> 0.288 ms of big rounds,
   // profiles/r04_sumcheck_wpe_blocks_ab.txt)
   static const bool wpe4 = getenv("QG_SC_WPE") != nullptr;
   if (pure && wpe4)
-    hipLaunchKernelGGL((k_sc_big<K, 4, true, false, 4>), dim3(blocks), dim3(SC_BLOCK), 0,
+    hipLaunchKernelGGL((k_sc_big<K, 4, true, 4>), dim3(blocks), dim3(SC_BLOCK), 0,
                        ctx->stream, tb, j, d_sp, h, npairs, ro, pending, loc, skip0, (j & 1) ? a1 : a0,
                        (j & 1) ? a0 : a1, bar8);
-  else if (pure && pf)
-    hipLaunchKernelGGL((k_sc_big<K, 4, true, true>), dim3(blocks), dim3(SC_BLOCK), 0, ctx->stream,
-                       tb, j, d_sp, h, npairs, ro, pending, loc, skip0, (j & 1) ? a1 : a0,
-                       (j & 1) ? a0 : a1, bar8);
   else if (pure)
-    hipLaunchKernelGGL((k_sc_big<K, 4, true, false>), dim3(blocks), dim3(SC_BLOCK), 0, ctx->stream,
+    hipLaunchKernelGGL((k_sc_big<K, 4, true>), dim3(blocks), dim3(SC_BLOCK), 0, ctx->stream,
                        tb, j, d_sp, h, npairs, ro, pending, loc, skip0, (j & 1) ? a1 : a0,
                        (j & 1) ? a0 : a1, bar8);
   else
-    hipLaunchKernelGGL((k_sc_big<4, 4, false, false>), dim3(blocks), dim3(SC_BLOCK), 0, ctx->stream,
+    hipLaunchKernelGGL((k_sc_big<4, 4, false>), dim3(blocks), dim3(SC_BLOCK), 0, ctx->stream,
                        tb, j, d_sp, h, npairs, ro, pending, loc, skip0, (j & 1) ? a1 : a0,
                        (j & 1) ? a0 : a1, bar8);
   QG_LAUNCH_CHECK();
