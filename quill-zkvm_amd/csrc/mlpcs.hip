@@ -641,13 +641,18 @@ static void s_poly_device(qg_ctx* ctx, const Fr* f, size_t nf, const Fr* g, size
   ntt_run(ctx, false, H, n, H, twi, logn, M, 2 * M - 1, S);
 }
 
-// highest nonzero index + 1: per-thread max over a grid-stride range, wave max
-// by shuffles, one atomic per wave (a contended atomic per element cost 0.75 ms
-// at 2^22)
+// highest nonzero index + 1: per-thread max over a grid-stride range of
+// [lo, hi), wave max by shuffles, one atomic per wave (a contended atomic per
+// element cost 0.75 ms at 2^22).  With skip set, a block whose start finds
+// *out already nonzero exits: the tail launch covered the higher indices, so
+// any body index is below the answer (a full body scan at 2^23 is 110 us;
+// most vectors end in a nonzero value).
 __global__ void __launch_bounds__(256)
-    k_last_nonzero(const Fr* __restrict__ a, size_t n, unsigned long long* out) {
+    k_last_nonzero(const Fr* __restrict__ a, size_t lo, size_t hi, int skip,
+                   unsigned long long* out) {
+  if (skip && __hip_atomic_load(out, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT)) return;
   unsigned long long m = 0;
-  for (size_t i = (size_t)blockIdx.x * blockDim.x + threadIdx.x; i < n;
+  for (size_t i = lo + (size_t)blockIdx.x * blockDim.x + threadIdx.x; i < hi;
        i += (size_t)gridDim.x * blockDim.x)
     if (!a[i].is_zero()) m = i + 1;
   for (int k = 32; k > 0; k >>= 1) {
@@ -657,14 +662,23 @@ __global__ void __launch_bounds__(256)
   if ((threadIdx.x & 63) == 0 && m) atomicMax(out, m);
 }
 
-// trimmed length of a device vector
+// trimmed length of a device vector: the last 16K entries first (8 blocks),
+// then the rest, skipped when the tail held a nonzero
 static size_t trimmed_len(qg_ctx* ctx, const Fr* a, size_t n) {
   if (n == 0) return 0;
   unsigned long long* d = ctx->scratch_as<unsigned long long>("trim_len", 1);
   QG_HIP(hipMemsetAsync(d, 0, sizeof(unsigned long long), ctx->stream));
-  const unsigned blocks = (unsigned)std::min<size_t>(2048, div_up(n, 256));
-  hipLaunchKernelGGL(k_last_nonzero, dim3(blocks), dim3(256), 0, ctx->stream, a, n, d);
+  constexpr size_t TAIL = 16384;
+  const size_t body = n > TAIL ? n - TAIL : 0;
+  hipLaunchKernelGGL(k_last_nonzero, dim3((unsigned)std::min<size_t>(8, div_up(n - body, 256))),
+                     dim3(256), 0, ctx->stream, a, body, n, 0, d);
   QG_LAUNCH_CHECK();
+  if (body) {
+    const unsigned blocks = (unsigned)std::min<size_t>(2048, div_up(body, 256));
+    hipLaunchKernelGGL(k_last_nonzero, dim3(blocks), dim3(256), 0, ctx->stream, a, (size_t)0,
+                       body, 1, d);
+    QG_LAUNCH_CHECK();
+  }
   unsigned long long h = 0;
   QG_HIP(hipMemcpyAsync(&h, d, sizeof(h), hipMemcpyDeviceToHost, ctx->stream));
   ctx->sync();
