@@ -250,28 +250,35 @@ static void suffix_horner_batch(qg_ctx* ctx, const std::vector<ShIn>& in, int de
 }
 
 // ---------------------------------------------------------------- NTT
-// Radix-2 NTT passes of up to 11 stages each on LDS tiles of 2048 elements
-// held as 9 x 29-bit limbs (SoA: conflict-free), so a 2^23-point transform is
+// Radix-2 NTT passes of up to 10 stages each on LDS tiles of 1024 elements
+// held as 9 x 29-bit limbs (SoA: conflict-free), so a 2^24-point transform is
 // three HBM round trips instead of one per stage.  A pass over stages
 // [s0, s0 + B) works on tiles of 2^B "mid" indices x L consecutive "lo"
-// indices (L = 2048 / 2^B): element (mid, l) is index
+// indices (L = 1024 / 2^B): element (mid, l) is index
 //   hi 2^(s0+B) + mid 2^s0 + lo0 + l,
-// so every global access is a run of L consecutive Fr (L >= 16 above the first
-// pass).  Forward: DIF (natural in, bit-reversed out); inverse: DIT
+// so every global access is a run of L consecutive Fr (L >= 8 above the first
+// pass).  36 KB tiles let four blocks share a CU (16 waves; the 2048-element
+// 72 KB tiles fit two: S polynomial at 2^23 -5 %, profiles/r04_ntt_tile_ab.txt).  Forward: DIF (natural in, bit-reversed out); inverse: DIT
 // (bit-reversed in, natural out) -- no bit-reversal pass at all.  Data stay in
 // arkworks form (x 2^256): twiddles are stored as w^k 2^261, so mul29 keeps the
 // scale.  Every value is < 2p inside a pass, canonical (< p) when stored.
-static constexpr int NTT_T = 2048;      // elements per tile
-static constexpr int NTT_LGT = 11;
-static constexpr int NTT_THREADS = 256;
+#ifndef QG_NTT_LGT
+#define QG_NTT_LGT 10
+#endif
+static constexpr int NTT_LGT = QG_NTT_LGT;
+static constexpr int NTT_T = 1 << NTT_LGT;  // elements per tile
+#ifndef QG_NTT_THREADS
+#define QG_NTT_THREADS 256
+#endif
+static constexpr int NTT_THREADS = QG_NTT_THREADS;
 using R29 = F29<FrP>;
 
 struct NttPass {
   int s0, B, lgL;
 };
 
-// stage ranges: [0, min(11, logn)) first (contiguous tiles), then chunks of at
-// most 7 stages (runs of >= 16 elements)
+// stage ranges: [0, min(10, logn)) first (contiguous tiles), then chunks of at
+// most 7 stages (runs of >= 8 elements)
 static std::vector<NttPass> ntt_plan(int logn) {
   std::vector<NttPass> v;
   int s = 0;

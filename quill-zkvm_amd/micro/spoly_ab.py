@@ -13,6 +13,9 @@ import threading
 
 HERE = os.path.dirname(os.path.abspath(__file__))
 sys.path.insert(0, os.path.dirname(HERE))
+if os.environ.get("QG_LIB"):  # A/B builds of the library (micro benchmark only)
+    import quill_amd._lib as _L  # noqa: E402
+    _L.LIB_PATH = os.path.abspath(os.environ["QG_LIB"])
 import quill_amd as q  # noqa: E402
 from quill_amd import KZG, Transcript  # noqa: E402
 

@@ -13,7 +13,7 @@ import pytest
 import quill_oracle as o
 
 R = o.R_MOD
-NTT_LGT = 11  # log2 of the 2048-element LDS tile
+NTT_LGT = 10  # log2 of the 1024-element LDS tile
 
 
 def ntt_plan(logn):
@@ -134,7 +134,7 @@ def bitrev(x, b):
     return int(format(x, f"0{b}b")[::-1], 2) if b else 0
 
 
-@pytest.mark.parametrize("logn", [3, 11, 12, 13, 15])
+@pytest.mark.parametrize("logn", [3, 10, 11, 12, 13, 15])
 @pytest.mark.parametrize("radix4,use_pyr", [(False, True), (False, False), (True, True)])
 def test_ntt_passes_roundtrip(logn, radix4, use_pyr):
     n = 1 << logn
@@ -149,5 +149,6 @@ def test_ntt_passes_roundtrip(logn, radix4, use_pyr):
 
 
 def test_plan_tiles():
-    assert ntt_plan(11) == [(0, 11, 0)]
-    assert ntt_plan(24) == [(0, 11, 0), (11, 7, 4), (18, 6, 5)]
+    assert ntt_plan(10) == [(0, 10, 0)]
+    assert ntt_plan(11) == [(0, 10, 0), (10, 1, 9)]
+    assert ntt_plan(24) == [(0, 10, 0), (10, 7, 3), (17, 7, 3)]
