@@ -78,12 +78,44 @@ def fr_list(arr) -> list:
     return [fr_from_mont_limbs(row) for row in a]
 
 
+_U64_ARR = {}
+_U32_ARR = {}
+
+
+def _arr_type(cache, ct, n):
+    t = cache.get(n)
+    if t is None:
+        t = cache[n] = ct * n
+    return t
+
+
 def u64p(arr: np.ndarray):
+    """The array's memory as a u64* argument.  A writable array is wrapped as a
+    ctypes array over the same buffer (~0.5 us; ndarray.ctypes.data_as costs
+    ~4 us, which the per-call wrappers of the small provers paid several times)."""
     assert arr.dtype == np.uint64 and arr.flags["C_CONTIGUOUS"]
+    if arr.flags.writeable and arr.size:
+        return _arr_type(_U64_ARR, C.c_uint64, arr.size).from_buffer(arr)
     return arr.ctypes.data_as(C.POINTER(C.c_uint64))
 
 
+def u32p(arr: np.ndarray):
+    """u32 counterpart of u64p"""
+    assert arr.dtype == np.uint32 and arr.flags["C_CONTIGUOUS"]
+    if arr.flags.writeable and arr.size:
+        return _arr_type(_U32_ARR, C.c_uint32, arr.size).from_buffer(arr)
+    return arr.ctypes.data_as(C.POINTER(C.c_uint32))
+
+
+_FR_C_SMALL = {}
+
+
 def fr_c(x: int):
+    if 0 <= x < 256:  # small constants (claims of 0, ones) recur in every call
+        limbs = _FR_C_SMALL.get(x)
+        if limbs is None:
+            limbs = _FR_C_SMALL[x] = tuple(fr_to_mont_limbs(x))
+        return (C.c_uint64 * 4)(*limbs)
     return (C.c_uint64 * 4)(*fr_to_mont_limbs(x))
 
 

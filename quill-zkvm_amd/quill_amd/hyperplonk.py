@@ -12,7 +12,7 @@ import numpy as np
 
 from ._lib import ExprOp, check, lib
 from .device import Device, DeviceVec
-from .field import R_MOD, eq_eval, fr_array, fr_c, fr_canonical_array, fr_inv, fr_list, u64p
+from .field import R_MOD, eq_eval, fr_array, fr_c, fr_canonical_array, fr_inv, fr_list, u32p, u64p
 from .pcs import EvaluationClaim
 from .transcript import Transcript
 
@@ -344,8 +344,7 @@ def sumcheck_prove_device(dev: Device, num_vars: int, tables, expr: VirtualPolyE
     ev = (C.c_uint64 * 4)()
     check(lib().qg_sumcheck_prove_dev(
         dev.h, num_vars, len(tables), ptrs, prog, plen, u64p(carr), nc, fr_c(claimed_sum),
-        transcript.c_state(), u64p(coeffs), lens.ctypes.data_as(C.POINTER(C.c_uint32)),
-        u64p(point), ev), dev.h)
+        transcript.c_state(), u64p(coeffs), u32p(lens), u64p(point), ev), dev.h)
     return coeffs, lens, point, ev
 
 
