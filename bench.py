@@ -342,6 +342,9 @@ def main():
         "commitment_x_low64": hex(0 if res is None else res[0] & ((1 << 64) - 1)),
         "commitment_verified": verified["ok"],
         "commitment_check": verified,
+        # bucket-scan plan copies re-read synchronously (stale generation tag); 0
+        # while the event ordering holds
+        "msm_plan_refetch": dev.counter("msm_plan_refetch"),
     }
 
     if traffic is not None:
@@ -394,6 +397,7 @@ def main():
             out["sumcheck"]["cpu_baseline"] = cpu_baseline_sumcheck(args)
         if args.log_mle > 0 and isinstance(out.get("mle_open"), dict):
             out["mle_open"]["cpu_baseline"] = cpu_baseline_mle(args)
+    out["msm_plan_refetch"] = dev.counter("msm_plan_refetch")  # over every leg
     if rank == 0:
         write_detail(out, args.detail_out)
         print(json.dumps(compact(out), separators=(",", ":")), flush=True)
@@ -722,12 +726,24 @@ def bench_logup(q, dev, args, barrier_sync, max_over_ranks, rank=0, world=1, tra
                                  "3 table reads + 1 column write of 32 B per row; the kernels "
                                  "also write and re-read the denominators (+64 B/row)")},
            "column_sum_low64": hex(s & ((1 << 64) - 1))}
+    if not fused:
+        # the column is multiply-bound: Montgomery products per row of the
+        # 3-kernel path, counted from csrc/logup.hip (denominator a t1 and the
+        # block product 2 + scans 0.5; prefix 0.875, wave scans 1.5, wave / block
+        # inverses 1.0, back-substitution 1.75, multiplier 1)
+        muls = LOGUP_MULS_PER_ROW * n
+        res["compute"] = {"fr_mul_per_row": LOGUP_MULS_PER_ROW,
+                          "fr_mul_per_s": muls / (kern_ms * 1e-3),
+                          "frac_issue_bound": muls / (kern_ms * 1e-3)
+                          / (VMAD_LANE_OPS_PER_S / MADS_PER_FQ_MUL)}
     if rank == 0 and not args.no_cpu_baseline:
         res["cpu_baseline"] = cpu_baseline_logup(args, tabs, out)
     for t in tabs + [out]:
         t.close()
     return res
 
+
+LOGUP_MULS_PER_ROW = 8.6
 
 HP_PHASES = ("msm_bucketing", "msm_accumulate", "msm_reduce", "sumcheck_round", "sumcheck_tail",
              "logup_column", "eq_table", "inner_product", "s_polynomial", "kzg_division")

@@ -220,6 +220,12 @@ int qg_ctx_kernel_time(const qg_ctx* ctx, const char* name, double* total_ms, ui
   return QG_OK;
 }
 
+int qg_ctx_counter(const qg_ctx* ctx, const char* name, uint64_t* value) {
+  if (!ctx || !name || !value) return QG_ERR_INVALID;
+  *value = std::string(name) == "msm_plan_refetch" ? ctx->msm_plan_refetch : 0;
+  return QG_OK;
+}
+
 int qg_trace_marker(qg_ctx* ctx, uint32_t tag) {
   if (!ctx || tag == 0) return QG_ERR_INVALID;
   return qg_guard(ctx, [&] {

@@ -68,6 +68,11 @@ struct qg_ctx {
   // or a one-rank group (a world-1 loopback, or the one-rank RCCL communicator
   // QG_FORCE_RCCL=1 attaches so a 1-GPU box executes the RCCL transport)
   bool sharded = false;
+  // MSM bucket-scan plan copies: generation tag of the last run, and the number
+  // of copies found stale (re-read synchronously; stays 0 when the event
+  // ordering holds)
+  uint32_t msm_gen = 0;
+  uint64_t msm_plan_refetch = 0;
 
   int cus = 0;  // compute units of `device` (cached)
   int num_cus() {

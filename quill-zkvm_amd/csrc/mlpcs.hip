@@ -441,12 +441,22 @@ __global__ void k_fr_to261(Fr* __restrict__ a, size_t n, L9 c) {
   if (i < n) a[i] = from29(canon29(mul29(to29(a[i]), R29::from_l9(c))));
 }
 
-// bit-reversed domain: H_br[k] = twM[j] (F[j] G[-j] + F[-j] G[j]), j = bitrev(k);
-// bitrev(-j) = k with every bit below k's top set bit flipped.  twM carries
-// w^{j(M-1)} n^-1 2^266, so mul29 of the 2^251-scaled products lands in
-// arkworks form with 1/n folded in.
+// twM in the combine's order: out[k] = in[bitrev(k)] c 2^-261 (the table is
+// built once per (logn, M); read in natural order by k_s_combine_br, its
+// loads are coalesced instead of one line per lane)
+__global__ void k_fr_to261_br(const Fr* __restrict__ in, int logn, L9 c, Fr* __restrict__ out) {
+  const size_t k = (size_t)blockIdx.x * blockDim.x + threadIdx.x;
+  if (k >= ((size_t)1 << logn)) return;
+  const size_t j = (size_t)(__brevll((unsigned long long)k) >> (64 - logn));
+  out[k] = from29(canon29(mul29(to29(in[j]), R29::from_l9(c))));
+}
+
+// bit-reversed domain: H_br[k] = tw_k (F[j] G[-j] + F[-j] G[j]), j = bitrev(k);
+// bitrev(-j) = k with every bit below k's top set bit flipped.  twMb[k] =
+// twM[bitrev(k)] carries w^{j(M-1)} n^-1 2^266, so mul29 of the 2^251-scaled
+// products lands in arkworks form with 1/n folded in.
 __global__ void k_s_combine_br(const Fr* __restrict__ F, const Fr* __restrict__ G,
-                               const Fr* __restrict__ twM, int logn, Fr* __restrict__ H) {
+                               const Fr* __restrict__ twMb, int logn, Fr* __restrict__ H) {
   const size_t k = (size_t)blockIdx.x * blockDim.x + threadIdx.x;
   const size_t n = (size_t)1 << logn;
   if (k >= n) return;
@@ -455,10 +465,9 @@ __global__ void k_s_combine_br(const Fr* __restrict__ F, const Fr* __restrict__ 
     const int hb = 63 - __clzll((unsigned long long)k);
     kn = k ^ (((size_t)1 << hb) - 1);
   }
-  const size_t j = (size_t)(__brevll((unsigned long long)k) >> (64 - logn));
   const R29 a = to29(F[k]), bb = to29(G[kn]), c = to29(F[kn]), d = to29(G[k]);
   const R29 v = red2p29(add29(mul29(a, bb), mul29(c, d)));
-  H[k] = from29(canon29(mul29(v, to29(twM[j]))));
+  H[k] = from29(canon29(mul29(v, to29(twMb[k]))));
 }
 
 __global__ void k_powers_ml(Fr base, size_t n, int K, Fr* out) {
@@ -470,22 +479,6 @@ __global__ void k_powers_ml(Fr base, size_t n, int K, Fr* out) {
     out[i0 + j] = x;
     x = x * base;
   }
-}
-
-// H[j] = w^{j(M-1)} (F[j] G[-j] + F[-j] G[j]), times n^{-1} folded in later
-__global__ void k_s_combine(const Fr* __restrict__ F, const Fr* __restrict__ G,
-                            const Fr* __restrict__ twM, size_t n, Fr* __restrict__ H) {
-  size_t j = (size_t)blockIdx.x * blockDim.x + threadIdx.x;
-  if (j >= n) return;
-  size_t nj = (n - j) & (n - 1);
-  Fr v = F[j] * G[nj] + F[nj] * G[j];
-  H[j] = v * twM[j];
-}
-
-__global__ void k_scale_copy(const Fr* __restrict__ in, Fr s, size_t n, Fr* __restrict__ out) {
-  size_t i = (size_t)blockIdx.x * blockDim.x + threadIdx.x;
-  if (i >= n) return;
-  out[i] = in[i] * s;
 }
 
 // host-side 256-bit exponent power
@@ -548,19 +541,45 @@ static void ntt_twiddles(qg_ctx* ctx, int logn, Fr** tw, Fr** twi,
 // One level per launch, 2^(L-t) entries; ~2 multiplies per entry over all
 // levels (~4 x 2^L in total) instead of L/2 per entry of a forward NTT.
 // Q is kept in arkworks form (x 2^256), the factor in the 2^261 domain.
+// With twb = the flat table in bit-reversed order (twb[i] = tw[bitrev_{L-1}(i)]),
+// level t's twiddle w^(bitrev_{L-t}(k) 2^t) is twb[k >> 1], negated for odd k
+// (the top bit of the exponent is k's low bit, w^(2^(L-1)) = -1): consecutive
+// entries read consecutive table words instead of one cache line per lane.
 __global__ void k_eqdft_level(const Fr* __restrict__ qnext, L9 a261, L9 z261,
-                              const Fr* __restrict__ tw, int logn, int t, Fr* __restrict__ q) {
+                              const Fr* __restrict__ twb, int logn, int t, Fr* __restrict__ q) {
   const size_t len = (size_t)1 << (logn - t);
   const size_t k = (size_t)blockIdx.x * blockDim.x + threadIdx.x;
   if (k >= len) return;
-  // j = bitrev_{L-t}(k); w^(j 2^t): tw[] holds w^m 2^261 for m < 2^(L-1)
   const size_t j = (size_t)(__brevll((unsigned long long)k) >> (64 - (logn - t)));
   const size_t m = j << t, half = (size_t)1 << (logn - 1);
-  R29 w = to29(tw[m & (half - 1)]);
-  if (m & half) w = sub29(R29::zero(), w);  // w^(2^(L-1)) = -1 (lazy 4p - w)
+  R29 w = to29(twb[m & (half - 1)]);
+  if (m & half) w = sub29(R29::zero(), w);
   const R29 f = red6p29(add29(R29::from_l9(a261), mul29(R29::from_l9(z261), w)));
   const R29 qn = qnext ? to29(qnext[k >> 1]) : to29(Fr::one());
   q[k] = from29(canon29(mul29(f, qn)));
+}
+
+// twb[i] = tw[bitrev_{L-1}(i)] for i < 2^(L-1) (one entry for L <= 1)
+__global__ void k_tw_bitrev(const Fr* __restrict__ tw, int logn, size_t h, Fr* __restrict__ twb) {
+  const size_t i = (size_t)blockIdx.x * blockDim.x + threadIdx.x;
+  if (i >= h) return;
+  const size_t j = logn > 1 ? (size_t)(__brevll((unsigned long long)i) >> (65 - logn)) : 0;
+  twb[i] = tw[j];
+}
+
+// the flat twiddle table in bit-reversed order (cached per table and size)
+static const Fr* ntt_tw_bitrev(qg_ctx* ctx, const Fr* tw, int logn) {
+  const std::string tag = "ntt_twb_" + std::to_string((uintptr_t)tw);
+  const size_t h = logn > 1 ? (size_t)1 << (logn - 1) : 1;
+  Fr* twb = ctx->scratch_as<Fr>(tag, h);
+  const std::string memo = std::to_string(logn) + "@" + std::to_string((uintptr_t)twb);
+  if (ctx->memo[tag] != memo) {
+    hipLaunchKernelGGL(k_tw_bitrev, dim3(div_up(h, 256)), dim3(256), 0, ctx->stream, tw, logn, h,
+                       twb);
+    QG_LAUNCH_CHECK();
+    ctx->memo[tag] = memo;
+  }
+  return twb;
 }
 
 static L9 l9_of29(const Fr& x) {
@@ -592,8 +611,9 @@ static void s_poly_device(qg_ctx* ctx, const Fr* f, size_t nf, const Fr* g, size
   Fr* twM = ctx->scratch_as<Fr>("ntt_twM", n);
   Fr *tw, *twi;
   ntt_twiddles(ctx, logn, &tw, &twi);
-  // w^{j(M-1)} n^-1 2^266 for j < n: powers of w^{M-1} (x 2^256), then x n^-1 2^271 via mul29.
-  // Depends on (logn, M) only: cached per context like the twiddles.
+  // w^{j(M-1)} n^-1 2^266 for j < n: powers of w^{M-1} (x 2^256, staged in H),
+  // then x n^-1 2^271 via mul29 into twM in bit-reversed order.  Depends on
+  // (logn, M) only: cached per context like the twiddles.
   const std::string twm_memo = std::to_string(logn) + ":" + std::to_string(M) + "@" +
                                std::to_string((uintptr_t)twM);
   if (ctx->memo["ntt_twM"] != twm_memo) {
@@ -601,7 +621,7 @@ static void s_poly_device(qg_ctx* ctx, const Fr* f, size_t nf, const Fr* g, size
     const Fr wM = fpow_small(w, (uint64_t)(M - 1));
     const int K = 64;
     hipLaunchKernelGGL(k_powers_ml, dim3(div_up(div_up(n, K), 256)), dim3(256), 0, ctx->stream, wM,
-                       n, K, twM);
+                       n, K, H);
     QG_LAUNCH_CHECK();
     const Fr ninv_plain = from_mont(finv(from_u64<FrP>(n)));
     const Fr cM = ml_plain_mul(ninv_plain, pow2_mod_plain<FrP>(271));
@@ -610,7 +630,8 @@ static void s_poly_device(qg_ctx* ctx, const Fr* f, size_t nf, const Fr* g, size
       const R29 t = to29(cM);
       for (int i = 0; i < 9; i++) c9.v[i] = t.l[i];
     }
-    hipLaunchKernelGGL(k_fr_to261, dim3(div_up(n, 256)), dim3(256), 0, ctx->stream, twM, n, c9);
+    hipLaunchKernelGGL(k_fr_to261_br, dim3(div_up(n, 256)), dim3(256), 0, ctx->stream, H, logn, c9,
+                       twM);
     QG_LAUNCH_CHECK();
     ctx->memo["ntt_twM"] = twm_memo;
   }
@@ -625,6 +646,7 @@ static void s_poly_device(qg_ctx* ctx, const Fr* f, size_t nf, const Fr* g, size
   if (eq_z && nz >= 1 && ((size_t)1 << nz) == ng && (int)nz < logn) {
     // levels t = nz-1 .. 0 ping-pong between G and H (H is free until the combine),
     // ending in G (t = 0: 2^logn entries, bit-reversed order)
+    const Fr* twb = tw;
     for (int t = (int)nz - 1; t >= 0; t--) {
       const Fr z = fr_import(eq_z + 4 * t);
       const Fr zp = from_mont(z), ap = from_mont(Fr::one() - z);
@@ -634,7 +656,7 @@ static void s_poly_device(qg_ctx* ctx, const Fr* f, size_t nf, const Fr* g, size
       const Fr* src = t == (int)nz - 1 ? nullptr : ((t & 1) == 0 ? H : G);
       const size_t len = (size_t)1 << (logn - t);
       hipLaunchKernelGGL(k_eqdft_level, dim3(div_up(len, 256)), dim3(256), 0, ctx->stream, src,
-                         a9, z9, tw, logn, t, dst);
+                         a9, z9, twb, logn, t, dst);
       QG_LAUNCH_CHECK();
     }
   } else {
@@ -876,17 +898,17 @@ __global__ void k_s_presum(const Fr* __restrict__ f, size_t M, size_t B, uint32_
 // launch (k_eqdft_level restricted to k = c mod W): level t has 2^(lb - t)
 // entries e (lb = log2 B), k2 = bitrev(e), factor a_t + z_t w^{(k2 W + c) 2^t}
 // = a_t + (z_t w^{c 2^t}) w_B^{k2 2^t}; Q_t[e] = factor Q_{t+1}[e >> 1].
-// twB: w_B^m 2^261 for m < B/2 (w_B^{B/2} = -1).
+// twBb: w_B^m 2^261 for m < B/2 (w_B^{B/2} = -1) in bit-reversed order
+// (ntt_tw_bitrev): w_B^{k2 2^t} is twBb[e >> 1], negated for odd e (as in
+// k_eqdft_level).
 __global__ void k_eqdft_res(const Fr* __restrict__ qnext, Fr q0, L9 a261, L9 zc261,
-                            const Fr* __restrict__ twB, int lb, int t, Fr* __restrict__ q) {
+                            const Fr* __restrict__ twBb, int lb, int t, Fr* __restrict__ q) {
   const int bits = lb - t;
   const size_t len = (size_t)1 << bits;
   const size_t e = (size_t)blockIdx.x * blockDim.x + threadIdx.x;
   if (e >= len) return;
-  const size_t k2 = bits ? (size_t)(__brevll((unsigned long long)e) >> (64 - bits)) : 0;
-  const size_t m = k2 << t, half = (size_t)1 << (lb - 1);
-  R29 w = to29(twB[m & (half - 1)]);
-  if (m & half) w = sub29(R29::zero(), w);
+  R29 w = to29(twBb[e >> 1]);
+  if (e & 1) w = sub29(R29::zero(), w);
   const R29 fct = red6p29(add29(R29::from_l9(a261), mul29(R29::from_l9(zc261), w)));
   const R29 qn = qnext ? to29(qnext[e >> 1]) : to29(q0);
   q[e] = from29(canon29(mul29(fct, qn)));
@@ -895,14 +917,16 @@ __global__ void k_eqdft_res(const Fr* __restrict__ qnext, Fr q0, L9 a261, L9 zc2
 // Hs at residue c in the bit-reversed block order: p -> k2 = bitrev(p); the
 // partner of -k is residue m = -c mod W at position ~p (c != 0) or, for c = 0,
 // the bit-reversed negation (k_s_combine_br's rule).  Hs = (-1)^c w^{-c} / n
-// w_B^{-k2} (F_c G_m' + F_m' G_c): twiB holds w_B^{-e} 2^261, cst the
+// w_B^{-k2} (F_c G_m' + F_m' G_c): twiBb holds w_B^{-e} 2^261 (e < B/2) in
+// bit-reversed order, so w_B^{-k2} = +-twiBb[p >> 1] (the sign from k2's top
+// bit, p's low bit; k2's low bit is p's top bit), cst the
 // per-residue constant x 2^266 (mul29 of the 2^251-scaled products lands in
 // arkworks form).
 // At W = 1 the (-1)^k of w^{k(M-1)} = (-1)^k w^{-k} is (-1)^k2, not the
 // residue's constant (-1)^c: `alt` negates the odd k2.
 __global__ void k_s_combine_res(const Fr* __restrict__ Fc, const Fr* __restrict__ Gc,
                                 const Fr* __restrict__ Fm, const Fr* __restrict__ Gm, int c,
-                                const Fr* __restrict__ twiB, int lb, L9 cst, int alt,
+                                const Fr* __restrict__ twiBb, int lb, L9 cst, int alt,
                                 Fr* __restrict__ H) {
   const size_t B = (size_t)1 << lb;
   const size_t p = (size_t)blockIdx.x * blockDim.x + threadIdx.x;
@@ -917,10 +941,9 @@ __global__ void k_s_combine_res(const Fr* __restrict__ Fc, const Fr* __restrict_
       pp = p ^ (((size_t)1 << hb) - 1);
     }
   }
-  const size_t k2 = (size_t)(__brevll((unsigned long long)p) >> (64 - lb));
-  const size_t half = B / 2;
-  R29 wi = to29(twiB[k2 & (half - 1)]);
-  if (((k2 & half) != 0) != (alt && (k2 & 1))) wi = sub29(R29::zero(), wi);
+  const bool k2top = lb > 0 && (p & 1), k2low = lb > 0 && ((p >> (lb - 1)) & 1);
+  R29 wi = to29(twiBb[p >> 1]);
+  if (k2top != (alt && k2low)) wi = sub29(R29::zero(), wi);
   const R29 v = red2p29(add29(mul29(to29(Fc[p]), to29(Gm[pp])), mul29(to29(Fm[pp]), to29(Gc[p]))));
   H[p] = from29(canon29(mul29(mul29(v, red6p29(wi)), R29::from_l9(cst))));
 }
@@ -1012,6 +1035,7 @@ static void s_poly_sharded(qg_ctx* ctx, const Fr* f, size_t M, const uint64_t* p
       q0 = q0 * ((Fr::one() - zt) + zt * fpow_small(w, (uint64_t)cc << t));
     }
     const int top = (int)std::min<size_t>(nz, (size_t)lb);
+    const Fr* twBb = ntt_tw_bitrev(ctx, twB, lb);
     const Fr* qn = nullptr;
     for (int t = top - 1; t >= 0; t--) {
       const Fr zt = fr_import(point + 4 * t);
@@ -1020,7 +1044,7 @@ static void s_poly_sharded(qg_ctx* ctx, const Fr* f, size_t M, const uint64_t* p
       Fr* dst = (t & 1) == 0 ? Gq : tmp;
       const size_t len = (size_t)1 << (lb - t);
       hipLaunchKernelGGL(k_eqdft_res, dim3(div_up(len, ML_BLOCK)), dim3(ML_BLOCK), 0, ctx->stream,
-                         qn, q0, a9, z9, twB, lb, t, dst);
+                         qn, q0, a9, z9, twBb, lb, t, dst);
       QG_LAUNCH_CHECK();
       qn = dst;
     }
@@ -1033,7 +1057,8 @@ static void s_poly_sharded(qg_ctx* ctx, const Fr* f, size_t M, const uint64_t* p
   if (c & 1) cst = fneg(cst);
   const L9 cst9 = l9_of29(ml_plain_mul(from_mont(cst), pow2_mod_plain<FrP>(266)));
   hipLaunchKernelGGL(k_s_combine_res, dim3(div_up(B, ML_BLOCK)), dim3(ML_BLOCK), 0, ctx->stream, Fb,
-                     Gb, Fm, Gm, (int)c, twiB, lb, cst9, W == 1 ? 1 : 0, H);
+                     Gb, Fm, Gm, (int)c, ntt_tw_bitrev(ctx, twiB, lb), lb, cst9, W == 1 ? 1 : 0,
+                     H);
   QG_LAUNCH_CHECK();
   ntt_run(ctx, false, H, B, H, twiB, lb, 0, 0, nullptr);
   Fr* P = tmp + B;

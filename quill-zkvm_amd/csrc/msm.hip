@@ -553,9 +553,10 @@ __global__ void k_scan_top(uint2* __restrict__ tile_tot, int ntiles, uint32_t* _
 __global__ void k_scan_add(const uint2* __restrict__ tile_off, size_t nb, uint32_t* __restrict__ bstart,
                            uint32_t* __restrict__ tstart, uint32_t* __restrict__ cursor,
                            const uint32_t* __restrict__ counts, uint32_t L, uint32_t T,
-                           uint32_t* __restrict__ misc) {
+                           uint32_t* __restrict__ misc, uint32_t gen) {
   size_t i = (size_t)blockIdx.x * blockDim.x + threadIdx.x;
   if (i >= nb) return;
+  if (i == 0) misc[4] = gen;  // tag of this run's plan words (checked by the reader)
   uint2 off = tile_off[i / SCAN_TILE];
   uint32_t b = bstart[i] + off.x;
   bstart[i] = b;
@@ -1165,12 +1166,14 @@ struct MsmRun {
   X29Raw* partial = nullptr;
   uint32_t* owner = nullptr;
   uint32_t* bstart = nullptr;
-  uint32_t* misc = nullptr;  // [0] nchunks, [1] max accumulation threads per bucket
+  uint32_t* misc = nullptr;  // [0] nchunks, [1] max accumulation threads per bucket,
+                             // [2..3] skewed slot range, [4] generation tag
   // misc[1..3] copied to pinned host memory right after the bucket scan, and
   // its event: the reduction's launch plan waits for the bucketing only, so
   // its kernels are queued while the accumulation still runs
   const uint32_t* h_mx = nullptr;
   hipEvent_t ev_mx = nullptr;
+  uint32_t gen = 0;  // misc[4] of this run: h_mx[3] must equal it
 };
 static constexpr int MSM_MAX_BATCH = 1024;
 
@@ -1205,7 +1208,7 @@ static MsmRun msm_accumulate_phase(qg_ctx* ctx, const qg_srs* srs, const Fr* d_s
     uint32_t* gstart = ctx->scratch_as<uint32_t>("msm_gstart", H + 1);
     uint32_t* cbase = ctx->scratch_as<uint32_t>("msm_cbase", H + 1);
     uint32_t* cgroup = ctx->scratch_as<uint32_t>("msm_cgroup", max_chunks);
-    uint32_t* misc = ctx->scratch_as<uint32_t>("msm_misc" + sfx, 4);  // [0] nchunks, [1] max tpb
+    uint32_t* misc = ctx->scratch_as<uint32_t>("msm_misc" + sfx, 5);  // [0] nchunks, [1] max tpb
     uint32_t* chist = ctx->scratch_as<uint32_t>("msm_chist", max_chunks * NL);
     uint32_t* coff = ctx->scratch_as<uint32_t>("msm_coff", max_chunks * NL);
     uint32_t* tmp_e = ctx->scratch_as<uint32_t>("msm_tmp_e", max_entries + 1);
@@ -1318,14 +1321,15 @@ static MsmRun msm_accumulate_phase(qg_ctx* ctx, const qg_srs* srs, const Fr* d_s
       hipLaunchKernelGGL(k_scan_top, dim3(1), dim3(1024), 0, ctx->stream, tile_tot, ntiles,
                          bstart, tstart, (size_t)nb);
       QG_LAUNCH_CHECK();
+      run.gen = ++ctx->msm_gen;
       hipLaunchKernelGGL(k_scan_add, dim3(div_up(nb, 256)), dim3(256), 0, ctx->stream, tile_tot,
-                         (size_t)nb, bstart, tstart, cursor, counts, L, T, misc);
+                         (size_t)nb, bstart, tstart, cursor, counts, L, T, misc, run.gen);
       QG_LAUNCH_CHECK();
       {
         QG_CHECK(slot >= 0 && slot < MSM_MAX_BATCH, QG_ERR_UNSUPPORTED, "MSM batch too large");
         uint32_t* hmx =
             reinterpret_cast<uint32_t*>(ctx->pinned_get("msm_mx", MSM_MAX_BATCH * 4 * sizeof(uint32_t)));
-        QG_HIP(hipMemcpyAsync(hmx + 4 * slot, misc + 1, 3 * sizeof(uint32_t), hipMemcpyDeviceToHost,
+        QG_HIP(hipMemcpyAsync(hmx + 4 * slot, misc + 1, 4 * sizeof(uint32_t), hipMemcpyDeviceToHost,
                               ctx->stream));
         run.ev_mx = ctx->ev_get();
         QG_HIP(hipEventRecord(run.ev_mx, ctx->stream));
@@ -1397,7 +1401,16 @@ static void msm_reduce_phase(qg_ctx* ctx, const qg_srs* srs, const std::vector<M
     const MsmRun& r = runs[live[q]];
     QG_CHECK(r.ev_mx && r.h_mx, QG_ERR_ASSERT, "MSM run without its bucket-scan event");
     QG_HIP(hipEventSynchronize(r.ev_mx));
-    for (int i = 0; i < 3; i++) mx[3 * q + i] = r.h_mx[i];
+    if (r.h_mx[3] == r.gen) {
+      for (int i = 0; i < 3; i++) mx[3 * q + i] = r.h_mx[i];
+    } else {  // the pinned copy is not this run's: read the words in stream order
+      QG_HIP(hipStreamSynchronize(ctx->stream));
+      uint32_t w[4];
+      QG_HIP(hipMemcpy(w, r.misc + 1, sizeof(w), hipMemcpyDeviceToHost));
+      QG_CHECK(w[3] == r.gen, QG_ERR_ASSERT, "MSM bucket-scan plan words of another run");
+      for (int i = 0; i < 3; i++) mx[3 * q + i] = w[i];
+      ctx->msm_plan_refetch++;
+    }
   }
   for (const MsmRun& r : runs)
     if (r.ev_mx) ctx->event_pool.push_back(r.ev_mx);

@@ -145,6 +145,7 @@ PROTOTYPES = {
                                       C.POINTER(C.c_double)]),
     "qg_ctx_kernel_time": (C.c_int, [P, C.c_char_p, C.POINTER(C.c_double), U32P]),
     "qg_trace_marker": (C.c_int, [P, C.c_uint32]),
+    "qg_ctx_counter": (C.c_int, [P, C.c_char_p, C.POINTER(C.c_uint64)]),
 }
 
 _lib = None

@@ -60,6 +60,12 @@ class Device:
         rocprofv3 kernel trace into phases (profiles/kstats.py --legs)"""
         check(lib().qg_trace_marker(self.h, tag), self.h)
 
+    def counter(self, name: str) -> int:
+        """diagnostic counter of the context (qg_ctx_counter)"""
+        v = C.c_uint64()
+        check(lib().qg_ctx_counter(self.h, name.encode(), C.byref(v)), self.h)
+        return v.value
+
     def attach_loopback(self, group, rank: int, world: int = None):
         check(lib().qg_ctx_attach_loopback(self.h, group, rank), self.h)
         self.rank = rank

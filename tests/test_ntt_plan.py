@@ -152,3 +152,31 @@ def test_plan_tiles():
     assert ntt_plan(10) == [(0, 10, 0)]
     assert ntt_plan(11) == [(0, 10, 0), (10, 1, 9)]
     assert ntt_plan(24) == [(0, 10, 0), (10, 7, 3), (17, 7, 3)]
+
+
+@pytest.mark.parametrize("logn", [1, 2, 5, 9])
+def test_eqdft_bitrev_twiddle_index(logn):
+    """k_eqdft_level reads twb[k >> 1] (twb = flat table in bit-reversed order),
+    negated for odd k, where the product formula needs w^(bitrev_{L-t}(k) 2^t)
+    (csrc/mlpcs.hip): the same exponent for every level t and entry k."""
+    half = 1 << (logn - 1)
+    twb = [bitrev(i, logn - 1) for i in range(half)]  # exponents held by twb
+    for t in range(logn):
+        for k in range(1 << (logn - t)):
+            m = bitrev(k, logn - t) << t
+            assert twb[k >> 1] == m & (half - 1)
+            assert ((m & half) != 0) == bool(k & 1)
+
+
+@pytest.mark.parametrize("lb", [1, 2, 6, 9])
+def test_combine_res_bitrev_twiddle_index(lb):
+    """k_s_combine_res reads twiBb[p >> 1] (bit-reversed w_B^{-e} table) with
+    the sign from p's low bit and the `alt` flip from p's top bit, where the
+    combine needs w_B^{-k2}, k2 = bitrev_lb(p), reduced by w_B^{B/2} = -1."""
+    half = 1 << (lb - 1)
+    twb = [bitrev(i, lb - 1) for i in range(half)]
+    for p in range(1 << lb):
+        k2 = bitrev(p, lb)
+        assert twb[p >> 1] == k2 & (half - 1)
+        assert ((k2 & half) != 0) == bool(p & 1)
+        assert bool(k2 & 1) == bool((p >> (lb - 1)) & 1)
