@@ -550,10 +550,8 @@ __global__ void k_eqdft_level(const Fr* __restrict__ qnext, L9 a261, L9 z261,
   const size_t len = (size_t)1 << (logn - t);
   const size_t k = (size_t)blockIdx.x * blockDim.x + threadIdx.x;
   if (k >= len) return;
-  const size_t j = (size_t)(__brevll((unsigned long long)k) >> (64 - (logn - t)));
-  const size_t m = j << t, half = (size_t)1 << (logn - 1);
-  R29 w = to29(twb[m & (half - 1)]);
-  if (m & half) w = sub29(R29::zero(), w);
+  R29 w = to29(twb[k >> 1]);
+  if (k & 1) w = sub29(R29::zero(), w);  // lazy 4p - w
   const R29 f = red6p29(add29(R29::from_l9(a261), mul29(R29::from_l9(z261), w)));
   const R29 qn = qnext ? to29(qnext[k >> 1]) : to29(Fr::one());
   q[k] = from29(canon29(mul29(f, qn)));
@@ -646,7 +644,7 @@ static void s_poly_device(qg_ctx* ctx, const Fr* f, size_t nf, const Fr* g, size
   if (eq_z && nz >= 1 && ((size_t)1 << nz) == ng && (int)nz < logn) {
     // levels t = nz-1 .. 0 ping-pong between G and H (H is free until the combine),
     // ending in G (t = 0: 2^logn entries, bit-reversed order)
-    const Fr* twb = tw;
+    const Fr* twb = ntt_tw_bitrev(ctx, tw, logn);
     for (int t = (int)nz - 1; t >= 0; t--) {
       const Fr z = fr_import(eq_z + 4 * t);
       const Fr zp = from_mont(z), ap = from_mont(Fr::one() - z);
