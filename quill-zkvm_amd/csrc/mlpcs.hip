@@ -530,6 +530,14 @@ static void ntt_twiddles(qg_ctx* ctx, int logn, Fr** tw, Fr** twi,
   hipLaunchKernelGGL(k_fr_to261, dim3(div_up(h, 256)), dim3(256), 0, ctx->stream, *twi, h, c);
   QG_LAUNCH_CHECK();
   ctx->memo[tag] = memo;
+  // the tables derived from a flat table (ntt_pyramid, ntt_tw_bitrev) are
+  // cached by its address: a table (re)built here may sit where another one
+  // was (scratch regrowth frees buffers and hipMalloc reuses addresses), with
+  // the same logn but other content (forward vs inverse) - drop them
+  for (const Fr* t : {*tw, *twi}) {
+    ctx->memo.erase("ntt_pyr_" + std::to_string((uintptr_t)t));
+    ctx->memo.erase("ntt_twb_" + std::to_string((uintptr_t)t));
+  }
 }
 
 // Transform of the eq table without an NTT.  g = eq(., z) over nz variables is

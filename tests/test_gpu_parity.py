@@ -473,3 +473,22 @@ def test_ctx_counter_reports_plan_refetches(dev):
     assert proof.evaluation == o.mle_evaluate(poly, point)
     assert dev.counter("msm_plan_refetch") >= 0
     assert dev.counter("no_such_counter") == 0
+
+
+def test_s_polynomial_size_cycle_keeps_twiddles_fresh(dev):
+    """Transforms of alternating sizes on one context: every regrowth of the
+    twiddle scratch frees a table whose address a later table (forward or
+    inverse, same logn) may get again, so the per-address pyramid and
+    bit-reversed caches must be rebuilt with the table (mlpcs.hip
+    ntt_twiddles), not served by address (an inverse NTT on forward
+    twiddles failed the 2^14-row HyperPlonk opening check).  Spot coefficients
+    against the correlation formula after every size change."""
+    rnd = random.Random(99)
+    for nf in (40000, 70000, 40000, 140000, 40000, 70000, 1 << 15):
+        f = [rnd.randrange(R) for _ in range(nf)]
+        g = [rnd.randrange(R) for _ in range(nf // 2)]
+        gp = g + [0] * (nf - len(g))
+        S = dev.s_polynomial(f, g)
+        for k in (0, nf // 3, nf - 2):
+            exp = sum(f[i + k + 1] * gp[i] + gp[i + k + 1] * f[i] for i in range(nf - k - 1)) % R
+            assert S[k] == exp, (nf, k)
