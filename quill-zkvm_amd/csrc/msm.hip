@@ -205,16 +205,10 @@ __global__ void __launch_bounds__(SORT_BLOCK)
   uint32_t* scr = gb + H;
   (void)scr;
   const uint32_t tb = xcd_tile(blockIdx.x, nblk);
-  // rows prepared by k_sortA_rows: the tile's local run starts and global bases
-  for (int g = threadIdx.x; g < H; g += blockDim.x) {
-    loff[g] = hrow[(size_t)tb * H + g];
-    gb[g] = orow[(size_t)tb * H + g];
-    cur[g] = 0;
-  }
-  __syncthreads();
   const size_t base = (size_t)tb * tile;
   const size_t end = base + tile < n ? base + tile : n;
-  // the thread's scalars (tile <= SORT_TILE_MAX) are loaded before the digit loops
+  // the thread's scalars (tile <= SORT_TILE_MAX) are loaded first: their round
+  // trip overlaps the row loads below
   constexpr int PER = SORT_TILE_MAX / SORT_BLOCK;
   Fr sv[PER];
 #pragma unroll
@@ -222,6 +216,13 @@ __global__ void __launch_bounds__(SORT_BLOCK)
     const size_t i = base + threadIdx.x + (size_t)j * SORT_BLOCK;
     if (i < end) sv[j] = canon[i];
   }
+  // rows prepared by k_sortA_rows: the tile's local run starts and global bases
+  for (int g = threadIdx.x; g < H; g += blockDim.x) {
+    loff[g] = hrow[(size_t)tb * H + g];
+    gb[g] = orow[(size_t)tb * H + g];
+    cur[g] = 0;
+  }
+  __syncthreads();
 #pragma unroll
   for (int j = 0; j < PER; j++) {
     const size_t i = base + threadIdx.x + (size_t)j * SORT_BLOCK;
@@ -372,16 +373,8 @@ __global__ void __launch_bounds__(SORT_BLOCK)
   const uint32_t g = chunk_group[k];
   const uint32_t s = gstart[g] + (k - cbase[g]) * SORT_CHUNK;
   const uint32_t e = min(s + SORT_CHUNK, gstart[g + 1]);
-  // the chunk's histogram was computed by k_sortB_hist (chist)
-  for (int l = threadIdx.x; l < NL; l += blockDim.x) {
-    loff[l] = chist[(size_t)k * NL + l];
-    cur[l] = 0;
-  }
-  __syncthreads();
-  lds_exscan(loff, NL, scr);
-  for (int l = threadIdx.x; l < NL; l += blockDim.x) cb[l] = coff[(size_t)k * NL + l] - loff[l];
-  // all of the thread's entries are loaded before the first LDS atomic, so the
-  // global loads overlap instead of one round trip per entry
+  // all of the thread's entries are loaded first: their round trip overlaps
+  // the histogram row, its scan and the offset row instead of following them
   constexpr int PER = SORT_CHUNK / SORT_BLOCK;
   uint32_t ev[PER], lv[PER];
 #pragma unroll
@@ -390,6 +383,14 @@ __global__ void __launch_bounds__(SORT_BLOCK)
     lv[j] = p < e ? (uint32_t)tmp_l[p] : 0xffffffffu;
     ev[j] = p < e ? tmp_e[p] : 0u;
   }
+  // the chunk's histogram was computed by k_sortB_hist (chist)
+  for (int l = threadIdx.x; l < NL; l += blockDim.x) {
+    loff[l] = chist[(size_t)k * NL + l];
+    cur[l] = 0;
+  }
+  __syncthreads();
+  lds_exscan(loff, NL, scr);
+  for (int l = threadIdx.x; l < NL; l += blockDim.x) cb[l] = coff[(size_t)k * NL + l] - loff[l];
 #pragma unroll
   for (int j = 0; j < PER; j++) {
     if (lv[j] == 0xffffffffu) continue;
