@@ -162,6 +162,46 @@ struct ShJobs {
   ShJob j[4];
 };
 
+// The apply pass on a full chunk runs software-pipelined: its coefficients
+// come in groups of SH_G, the next group's loads issued before the current
+// group's dependent products and stores (one load round trip per group instead
+// of per step, which the stores would otherwise pin in program order); a short
+// last chunk loops.  Every suffix value is written.
+static constexpr int SH_G = 4;
+__device__ __forceinline__ void sh_apply_chunk(const Fr* __restrict__ c, Fr* __restrict__ out,
+                                               size_t s, size_t e, const F29<FrP>& x,
+                                               F29<FrP> acc) {
+  if (e - s == SH_B) {
+    Fr cur[SH_G], nxt[SH_G];
+#pragma unroll
+    for (int j = 0; j < SH_G; j++) cur[j] = c[s + SH_B - SH_G + j];
+#pragma unroll
+    for (int g = SH_B / SH_G - 1; g >= 0; g--) {
+      if (g > 0) {
+#pragma unroll
+        for (int j = 0; j < SH_G; j++) nxt[j] = c[s + (size_t)(g - 1) * SH_G + j];
+      }
+      // keeps the scheduler from hoisting later groups' loads above this
+      // group's products
+      asm volatile("" ::: "memory");
+#pragma unroll
+      for (int j = SH_G - 1; j >= 0; j--) {
+        acc = red6p29(add29(to29(cur[j]), mul29(x, acc)));
+        out[s + (size_t)g * SH_G + j] = from29(canon29(acc));
+      }
+      if (g > 0) {
+#pragma unroll
+        for (int j = 0; j < SH_G; j++) cur[j] = nxt[j];
+      }
+    }
+  } else {
+    for (size_t i = e; i-- > s;) {
+      acc = red6p29(add29(to29(c[i]), mul29(x, acc)));
+      out[i] = from29(canon29(acc));
+    }
+  }
+}
+
 __global__ void k_sh_local_b(ShJobs jb) {
   const ShJob& J = jb.j[blockIdx.y];
   const size_t k = (size_t)blockIdx.x * blockDim.x + threadIdx.x;
@@ -170,6 +210,8 @@ __global__ void k_sh_local_b(ShJobs jb) {
   const size_t e = s + SH_B < J.L ? s + SH_B : J.L;
   const F29<FrP> x = F29<FrP>::from_l9(J.x);
   F29<FrP> acc = F29<FrP>::zero();
+  // no stores in this chain: an unrolled loop lets the loads run ahead
+#pragma unroll 4
   for (size_t i = e; i-- > s;) acc = red6p29(add29(to29(J.c[i]), mul29(x, acc)));
   J.A[k] = from29(canon29(acc));
 }
@@ -181,11 +223,8 @@ __global__ void k_sh_apply_b(ShJobs jb) {
   if (s >= J.L) return;
   const size_t e = s + SH_B < J.L ? s + SH_B : J.L;
   const F29<FrP> x = F29<FrP>::from_l9(J.x);
-  F29<FrP> acc = (k + 1 < J.nch) ? to29(J.T[k + 1]) : F29<FrP>::zero();
-  for (size_t i = e; i-- > s;) {
-    acc = red6p29(add29(to29(J.c[i]), mul29(x, acc)));
-    J.s[i] = from29(canon29(acc));
-  }
+  const F29<FrP> acc0 = (k + 1 < J.nch) ? to29(J.T[k + 1]) : F29<FrP>::zero();
+  sh_apply_chunk(J.c, J.s, s, e, x, acc0);
 }
 
 __global__ void k_sh_serial_b(ShJobs jb) {
