@@ -653,15 +653,19 @@ static void s_poly_device(qg_ctx* ctx, const Fr* f, size_t nf, const Fr* g, size
   Fr* F = ctx->scratch_as<Fr>("ntt_F", n);
   Fr* G = ctx->scratch_as<Fr>("ntt_G", n);
   Fr* H = ctx->scratch_as<Fr>("ntt_H", n);
-  Fr* twM = ctx->scratch_as<Fr>("ntt_twM", n);
-  Fr *tw, *twi;
-  ntt_twiddles(ctx, logn, &tw, &twi);
   // w^{j(M-1)} n^-1 2^266 for j < n: powers of w^{M-1} (x 2^256, staged in H),
   // then x n^-1 2^271 via mul29 into twM in bit-reversed order.  Depends on
-  // (logn, M) only: cached per context like the twiddles.
-  const std::string twm_memo = std::to_string(logn) + ":" + std::to_string(M) + "@" +
-                               std::to_string((uintptr_t)twM);
-  if (ctx->memo["ntt_twM"] != twm_memo) {
+  // (logn, M) only: cached per context in one of four slots by (logn, M), so a
+  // prover alternating between a few opening sizes (HyperPlonk: the witness
+  // and its public rows) does not rebuild it per opening.
+  const std::string twm_key = std::to_string(logn) + ":" + std::to_string(M);
+  const std::string twm_slot =
+      "ntt_twM#" + std::to_string(std::hash<std::string>{}(twm_key) % 4);
+  Fr* twM = ctx->scratch_as<Fr>(twm_slot, n);
+  Fr *tw, *twi;
+  ntt_twiddles(ctx, logn, &tw, &twi);
+  const std::string twm_memo = twm_key + "@" + std::to_string((uintptr_t)twM);
+  if (ctx->memo[twm_slot] != twm_memo) {
     const Fr w = root_of_unity(logn);
     const Fr wM = fpow_small(w, (uint64_t)(M - 1));
     const int K = 64;
@@ -678,7 +682,7 @@ static void s_poly_device(qg_ctx* ctx, const Fr* f, size_t nf, const Fr* g, size
     hipLaunchKernelGGL(k_fr_to261_br, dim3(div_up(n, 256)), dim3(256), 0, ctx->stream, H, logn, c9,
                        twM);
     QG_LAUNCH_CHECK();
-    ctx->memo["ntt_twM"] = twm_memo;
+    ctx->memo[twm_slot] = twm_memo;
   }
   // forward DIF of f and g (zero-extended), bit-reversed outputs
   const std::string fkey = std::to_string((uintptr_t)f) + ":" + std::to_string(nf) + ":" +
