@@ -122,6 +122,10 @@ struct F29P {
   static constexpr L9 P4 = l9_mul_small(P, 4);
   static constexpr L9 P8 = l9_mul_small(P, 8);
   static constexpr L9 K4 = l9_redundant(l9_mul_small(P, 4));
+  // 2p redundant: a + 2p - b for b < 2p (normalized) is exact in uint32 limb
+  // arithmetic even when the top limb wraps (the value is >= 0, so the carry
+  // into the top limb restores it in normfull29)
+  static constexpr L9 K2 = l9_redundant(l9_mul_small(P, 2));
   static constexpr uint32_t INV = l9_inv29(C::P[0]);
   static constexpr L9 ONE = l9_pow2_mod(P, 261);     // 1 in the R = 2^261 domain
   static constexpr L9 TO261 = l9_pow2_mod(P, 266);   // mul29(x 2^256, .) = x 2^261

@@ -416,7 +416,8 @@ __global__ void __launch_bounds__(NTT_THREADS)
           lds_put29(sh, e1[h], t[h]);
         } else {
           lds_put29(sh, e0[h], red2p29(add29(u[h], t[h])));
-          lds_put29(sh, e1[h], red6p29(sub29(u[h], t[h])));
+          // u + 2p - t in [0, 4p) (u, t < 2p): one conditional subtraction
+          lds_put29(sh, e1[h], red2p29(subk29(u[h], t[h], F29P<FrP>::K2)));
         }
       }
     }

@@ -180,3 +180,52 @@ def test_combine_res_bitrev_twiddle_index(lb):
         assert twb[p >> 1] == k2 & (half - 1)
         assert ((k2 & half) != 0) == bool(p & 1)
         assert bool(k2 & 1) == bool((p >> (lb - 1)) & 1)
+
+
+M29 = (1 << 29) - 1
+P_FR = R
+
+
+def _limbs29(x):
+    return [(x >> (29 * i)) & (M29 if i < 8 else 0xffffffff) for i in range(9)]
+
+
+def _redundant(kp):
+    """field29.h l9_redundant: limbs 0..7 raised by 2^29 (borrowed from above)"""
+    r = list(kp)
+    r[0] += 1 << 29
+    for i in range(1, 8):
+        r[i] += (1 << 29) - 1
+    r[8] -= 1
+    return r
+
+
+def _val(limbs):
+    return sum(l << (29 * i) for i, l in enumerate(limbs))
+
+
+@pytest.mark.parametrize("seed", range(4))
+def test_dit_butterfly_sub_2p_redundant(seed):
+    """k_ntt_pass DIT: v' = red2p29(subk29(u, t, K2)) with K2 = 2p in redundant
+    limbs, u, t < 2p normalized (csrc/field29.h).  Restated limb by limb in
+    uint32 arithmetic: the top limb may wrap below zero, normfull29's carry
+    brings it back (the value u + 2p - t is >= 0), one conditional subtraction
+    of 2p leaves [0, 2p) - equal to (u - t) mod p."""
+    rnd = random.Random(seed)
+    K2 = _redundant(_limbs29(2 * P_FR))
+    edge = [0, 1, P_FR - 1, P_FR, 2 * P_FR - 1]
+    cases = [(a, b) for a in edge for b in edge] + \
+            [(rnd.randrange(2 * P_FR), rnd.randrange(2 * P_FR)) for _ in range(2000)]
+    for u, t in cases:
+        ul, tl = _limbs29(u), _limbs29(t)
+        a = [(ul[i] + (K2[i] - tl[i])) & 0xffffffff for i in range(9)]
+        c, r = 0, []
+        for i in range(8):  # normfull29
+            x = (a[i] + c) & 0xffffffff
+            r.append(x & M29)
+            c = x >> 29
+        r.append((a[8] + c) & 0xffffffff)
+        v = _val(r)
+        assert 0 <= v < 4 * P_FR
+        v = v - 2 * P_FR if v >= 2 * P_FR else v  # condsub29(., 2p)
+        assert v < 2 * P_FR and v % P_FR == (u - t) % P_FR
