@@ -145,7 +145,8 @@ static void suffix_horner(qg_ctx* ctx, const Fr* c, size_t L, const Fr& x, Fr* s
 }
 
 // Batched form (up to 4 independent scans per launch, blockIdx.y = scan) in
-// 9 x 29-bit limbs: the per-chunk Horner chain is the latency of the whole
+// 9 x 29-bit limbs (each step c_i + x s_{i+1}: a canonical coefficient plus a
+// product < 2p, so one conditional subtraction keeps s < 2p): the per-chunk Horner chain is the latency of the whole
 // recursion, and the 29-bit multiply's dependent latency is half the 32-bit
 // one's.  x is passed as x 2^261 (plain limbs), so mul29 keeps the arkworks
 // scale of the coefficients.
@@ -186,7 +187,7 @@ __device__ __forceinline__ void sh_apply_chunk(const Fr* __restrict__ c, Fr* __r
       asm volatile("" ::: "memory");
 #pragma unroll
       for (int j = SH_G - 1; j >= 0; j--) {
-        acc = red6p29(add29(to29(cur[j]), mul29(x, acc)));
+        acc = red2p29(add29(to29(cur[j]), mul29(x, acc)));
         out[s + (size_t)g * SH_G + j] = from29(canon29(acc));
       }
       if (g > 0) {
@@ -196,7 +197,7 @@ __device__ __forceinline__ void sh_apply_chunk(const Fr* __restrict__ c, Fr* __r
     }
   } else {
     for (size_t i = e; i-- > s;) {
-      acc = red6p29(add29(to29(c[i]), mul29(x, acc)));
+      acc = red2p29(add29(to29(c[i]), mul29(x, acc)));
       out[i] = from29(canon29(acc));
     }
   }
@@ -212,7 +213,7 @@ __global__ void k_sh_local_b(ShJobs jb) {
   F29<FrP> acc = F29<FrP>::zero();
   // no stores in this chain: an unrolled loop lets the loads run ahead
 #pragma unroll 4
-  for (size_t i = e; i-- > s;) acc = red6p29(add29(to29(J.c[i]), mul29(x, acc)));
+  for (size_t i = e; i-- > s;) acc = red2p29(add29(to29(J.c[i]), mul29(x, acc)));
   J.A[k] = from29(canon29(acc));
 }
 
@@ -233,7 +234,7 @@ __global__ void k_sh_serial_b(ShJobs jb) {
   const F29<FrP> x = F29<FrP>::from_l9(J.x);
   F29<FrP> acc = F29<FrP>::zero();
   for (size_t i = J.L; i-- > 0;) {
-    acc = red6p29(add29(to29(J.c[i]), mul29(x, acc)));
+    acc = red2p29(add29(to29(J.c[i]), mul29(x, acc)));
     J.s[i] = from29(canon29(acc));
   }
 }
@@ -600,7 +601,8 @@ __global__ void k_eqdft_level(const Fr* __restrict__ qnext, L9 a261, L9 z261,
   if (k >= len) return;
   R29 w = to29(twb[k >> 1]);
   if (k & 1) w = sub29(R29::zero(), w);  // lazy 4p - w
-  const R29 f = red6p29(add29(R29::from_l9(a261), mul29(R29::from_l9(z261), w)));
+  // a261 < p (host-canonical), the product < 2p: one conditional subtraction
+  const R29 f = red2p29(add29(R29::from_l9(a261), mul29(R29::from_l9(z261), w)));
   const R29 qn = qnext ? to29(qnext[k >> 1]) : to29(Fr::one());
   q[k] = from29(canon29(mul29(f, qn)));
 }
@@ -959,7 +961,7 @@ __global__ void k_eqdft_res(const Fr* __restrict__ qnext, Fr q0, L9 a261, L9 zc2
   if (e >= len) return;
   R29 w = to29(twBb[e >> 1]);
   if (e & 1) w = sub29(R29::zero(), w);
-  const R29 fct = red6p29(add29(R29::from_l9(a261), mul29(R29::from_l9(zc261), w)));
+  const R29 fct = red2p29(add29(R29::from_l9(a261), mul29(R29::from_l9(zc261), w)));
   const R29 qn = qnext ? to29(qnext[e >> 1]) : to29(q0);
   q[e] = from29(canon29(mul29(fct, qn)));
 }
