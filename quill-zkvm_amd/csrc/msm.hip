@@ -261,13 +261,17 @@ __global__ void __launch_bounds__(SORT_BLOCK)
   }
 }
 
-// groups -> chunks (single block): gstart[g] = goff[g*nblk], chunk bases, chunk->group map
+// groups -> chunks (single block): gstart[g] = goff[g*nblk], chunk bases, chunk->group map;
+// misc[0] = chunk count, and the words the bucket scan accumulates into start
+// here (no fill launches): [1] max threads per bucket = 0, [2..3] skewed slot
+// range = empty
 __global__ void __launch_bounds__(1024)
     k_sort_chunks(const uint32_t* __restrict__ goff, uint32_t nblk, int H,
                   uint32_t* __restrict__ gstart, uint32_t* __restrict__ cbase,
-                  uint32_t* __restrict__ chunk_group, uint32_t* __restrict__ nchunks_out) {
+                  uint32_t* __restrict__ chunk_group, uint32_t* __restrict__ misc) {
   __shared__ uint32_t sh[1024];
   const int g = threadIdx.x;
+  if (threadIdx.x >= 1 && threadIdx.x <= 3) misc[threadIdx.x] = threadIdx.x == 2 ? 0xffffffffu : 0u;
   const uint32_t total = goff[(size_t)H * nblk];
   uint32_t gs = 0, ge = 0, nch = 0;
   if (g < H) {
@@ -292,7 +296,7 @@ __global__ void __launch_bounds__(1024)
   if (threadIdx.x == 1023) {
     gstart[H] = total;
     cbase[H] = sh[1023];
-    *nchunks_out = sh[1023];
+    misc[0] = sh[1023];
   }
 }
 
@@ -474,8 +478,8 @@ __device__ __forceinline__ uint2 scan_val(const uint32_t* counts, size_t i, size
 
 // per-tile exclusive scan; writes tile totals
 __global__ void k_scan_tiles(const uint32_t* __restrict__ counts, size_t nb, uint32_t L,
-                             uint32_t* __restrict__ bstart, uint32_t* __restrict__ tstart,
-                             uint2* __restrict__ tile_tot, uint32_t* __restrict__ max_tpb) {
+                             uint32_t* __restrict__ bstart, uint2* __restrict__ tile_tot,
+                             uint32_t* __restrict__ max_tpb) {
   __shared__ uint2 sh[SCAN_BLOCK];
   size_t base = (size_t)blockIdx.x * SCAN_TILE + threadIdx.x * SCAN_PER_THREAD;
   uint2 v[SCAN_PER_THREAD];
@@ -501,10 +505,7 @@ __global__ void k_scan_tiles(const uint32_t* __restrict__ counts, size_t nb, uin
   uint2 run = threadIdx.x ? sh[threadIdx.x - 1] : make_uint2(0, 0);
   for (int k = 0; k < SCAN_PER_THREAD; k++) {
     size_t i = base + k;
-    if (i < nb) {
-      bstart[i] = run.x;
-      tstart[i] = run.y;
-    }
+    if (i < nb) bstart[i] = run.x;
     run.x += v[k].x;
     run.y += v[k].y;
   }
@@ -513,7 +514,7 @@ __global__ void k_scan_tiles(const uint32_t* __restrict__ counts, size_t nb, uin
 
 // single block: exclusive scan of tile totals (ntiles <= 1024 * 8)
 __global__ void k_scan_top(uint2* __restrict__ tile_tot, int ntiles, uint32_t* __restrict__ bstart,
-                           uint32_t* __restrict__ tstart, size_t nb) {
+                           size_t nb) {
   __shared__ uint2 sh[1024];
   const int per = (ntiles + 1023) / 1024;
   int base = threadIdx.x * per;
@@ -542,17 +543,13 @@ __global__ void k_scan_top(uint2* __restrict__ tile_tot, int ntiles, uint32_t* _
       run.y += t.y;
     }
   }
-  if (threadIdx.x == 1023) {
-    bstart[nb] = sh[1023].x;
-    tstart[nb] = sh[1023].y;
-  }
+  if (threadIdx.x == 1023) bstart[nb] = sh[1023].x;
 }
 
 // final bucket starts; misc[2] / misc[3] = first / last partial slot of the
 // buckets with more than T partial slots (msm_combine_run: the reduction's
 // tree steps run over that range only)
 __global__ void k_scan_add(const uint2* __restrict__ tile_off, size_t nb, uint32_t* __restrict__ bstart,
-                           uint32_t* __restrict__ tstart, uint32_t* __restrict__ cursor,
                            const uint32_t* __restrict__ counts, uint32_t L, uint32_t T,
                            uint32_t* __restrict__ misc, uint32_t gen) {
   size_t i = (size_t)blockIdx.x * blockDim.x + threadIdx.x;
@@ -561,8 +558,6 @@ __global__ void k_scan_add(const uint2* __restrict__ tile_off, size_t nb, uint32
   uint2 off = tile_off[i / SCAN_TILE];
   uint32_t b = bstart[i] + off.x;
   bstart[i] = b;
-  cursor[i] = b;
-  tstart[i] += off.y;
   const uint32_t c = counts[i];
   if (c > (T - 1) * L) {  // may span more than T slots
     const uint32_t f = b / L + (uint32_t)i, l = (b + c - 1) / L + (uint32_t)i;
@@ -986,9 +981,16 @@ __global__ void __launch_bounds__(MSM_BLOCK)
 #endif
 }
 
+// R = 2^261 XYZZ -> R = 2^256 Montgomery XYZZ (canonical), the host's form
+QG_DEV G1Xyzz x29_export_xyzz(const X29& p) {
+  if (x29_is_inf(p)) return G1Xyzz::infinity();
+  return {q29_export(p.X), q29_export(p.Y), q29_export(p.ZZ), q29_export(p.ZZZ)};
+}
+
 // next levels: m elements (A_e, Y_e), total sum_e A_e + e Y_e; group w (16
 // elements on quads, or 64 single-lane elements) writes (A'_w, Y'_w) of the
-// same form, or only A'_w (the total) when Y_out is null
+// same form, or only A'_w (the total) when Y_out is null, then in the host's
+// form (x29_export_xyzz: the last level, no separate export launch)
 template <bool Q4>
 __global__ void __launch_bounds__(64)
     k_msm_wfold(const G1Xyzz* __restrict__ A_in, const G1Xyzz* __restrict__ Y_in, uint32_t m,
@@ -1008,23 +1010,14 @@ __global__ void __launch_bounds__(64)
   msm_fold<Q4>(A, Y, gl, mv, 0, Y_out ? gl : 0, Yw);
   if (threadIdx.x == 0) {
     const size_t w = (size_t)blockIdx.y * ostride + blockIdx.x;
-    A_out[w] = x29_store(A);
-    if (Y_out) Y_out[w] = x29_store(Yw);
+    if (Y_out) {
+      A_out[w] = x29_store(A);
+      Y_out[w] = x29_store(Yw);
+    } else {
+      A_out[w] = x29_export_xyzz(A);
+    }
   }
 #endif
-}
-
-// R = 2^261 XYZZ words -> R = 2^256 Montgomery XYZZ (canonical) for the host
-__global__ void k_msm_export(const G1Xyzz* __restrict__ in, size_t stride, uint32_t k,
-                             G1Xyzz* __restrict__ out) {
-  const uint32_t i = threadIdx.x;
-  if (i >= k) return;
-  const X29 p = x29_load(in[i * stride]);
-  if (x29_is_inf(p)) {
-    out[i] = G1Xyzz::infinity();
-    return;
-  }
-  out[i] = {q29_export(p.X), q29_export(p.Y), q29_export(p.ZZ), q29_export(p.ZZZ)};
 }
 
 // arkworks affine points (R = 2^256 words, (0,0) = infinity) -> table rows
@@ -1219,8 +1212,6 @@ static MsmRun msm_accumulate_phase(qg_ctx* ctx, const qg_srs* srs, const Fr* d_s
     Fr* canon = ctx->scratch_as<Fr>("msm_canon", n);
     uint32_t* counts = ctx->scratch_as<uint32_t>("msm_counts", nb);
     uint32_t* bstart = ctx->scratch_as<uint32_t>("msm_bstart" + sfx, nb + 1);
-    uint32_t* tstart = ctx->scratch_as<uint32_t>("msm_tstart", nb + 1);
-    uint32_t* cursor = ctx->scratch_as<uint32_t>("msm_cursor", nb);
     uint32_t* entries = ctx->scratch_as<uint32_t>("msm_entries", max_entries + 1);
     const int ntiles = (int)div_up(nb, SCAN_TILE);
     uint2* tile_tot = ctx->scratch_as<uint2>("msm_tiles", ntiles);
@@ -1304,8 +1295,6 @@ static MsmRun msm_accumulate_phase(qg_ctx* ctx, const qg_srs* srs, const Fr* d_s
                          canon, n, srs->n, srs_off, c, W, LO, H, nblk, tile, hrow, orow, tmp_e, tmp_l);
       QG_LAUNCH_CHECK();
       // pass B: sort every group by the low bits, in chunks
-      QG_HIP(hipMemsetAsync(misc, 0, 4 * sizeof(uint32_t), ctx->stream));
-      QG_HIP(hipMemsetAsync(misc + 2, 0xff, sizeof(uint32_t), ctx->stream));  // slot range: empty
       hipLaunchKernelGGL(k_sort_chunks, dim3(1), dim3(1024), 0, ctx->stream, goff, nblk, H,
                          gstart, cbase, cgroup, misc);
       QG_LAUNCH_CHECK();
@@ -1317,14 +1306,14 @@ static MsmRun msm_accumulate_phase(qg_ctx* ctx, const qg_srs* srs, const Fr* d_s
                          cbase, chist, LO, nb, counts);
       QG_LAUNCH_CHECK();
       hipLaunchKernelGGL(k_scan_tiles, dim3(ntiles), dim3(SCAN_BLOCK), 0, ctx->stream, counts,
-                         (size_t)nb, L, bstart, tstart, tile_tot, misc + 1);
+                         (size_t)nb, L, bstart, tile_tot, misc + 1);
       QG_LAUNCH_CHECK();
       hipLaunchKernelGGL(k_scan_top, dim3(1), dim3(1024), 0, ctx->stream, tile_tot, ntiles,
-                         bstart, tstart, (size_t)nb);
+                         bstart, (size_t)nb);
       QG_LAUNCH_CHECK();
       run.gen = ++ctx->msm_gen;
       hipLaunchKernelGGL(k_scan_add, dim3(div_up(nb, 256)), dim3(256), 0, ctx->stream, tile_tot,
-                         (size_t)nb, bstart, tstart, cursor, counts, L, T, misc, run.gen);
+                         (size_t)nb, bstart, counts, L, T, misc, run.gen);
       QG_LAUNCH_CHECK();
       {
         QG_CHECK(slot >= 0 && slot < MSM_MAX_BATCH, QG_ERR_UNSUPPORTED, "MSM batch too large");
@@ -1432,7 +1421,6 @@ static void msm_reduce_phase(qg_ctx* ctx, const qg_srs* srs, const std::vector<M
   G1Xyzz* Y1 = ctx->scratch_as<G1Xyzz>("msm_redY1", (size_t)kl * m1);
   G1Xyzz* A2 = ctx->scratch_as<G1Xyzz>("msm_redA2", (size_t)kl * m2);
   G1Xyzz* Y2 = ctx->scratch_as<G1Xyzz>("msm_redY2", (size_t)kl * m2);
-  G1Xyzz* fin = ctx->scratch_as<G1Xyzz>("msm_red_total", kl);
   G1Xyzz* d_out = ctx->scratch_as<G1Xyzz>("msm_out", kl);
   MsmRed* d_runs = ctx->scratch_as<MsmRed>("msm_runs", kl);
   std::vector<MsmRed> h_runs(kl);
@@ -1479,12 +1467,11 @@ static void msm_reduce_phase(qg_ctx* ctx, const qg_srs* srs, const std::vector<M
       istride = mo;
       m = mo;
     }
-    hipLaunchKernelGGL(fold, dim3(1, kl), dim3(64), 0, ctx->stream, Ai, Yi, m, istride, fin,
+    // the last fold writes the totals in the host's form
+    hipLaunchKernelGGL(fold, dim3(1, kl), dim3(64), 0, ctx->stream, Ai, Yi, m, istride, d_out,
                        (G1Xyzz*)nullptr, (size_t)1);
     QG_LAUNCH_CHECK();
   }
-  hipLaunchKernelGGL(k_msm_export, dim3(1), dim3(1024), 0, ctx->stream, fin, (size_t)1, kl, d_out);
-  QG_LAUNCH_CHECK();
   std::vector<G1Xyzz> h(kl);
   QG_HIP(hipMemcpyAsync(h.data(), d_out, kl * sizeof(G1Xyzz), hipMemcpyDeviceToHost, ctx->stream));
   ctx->sync();
