@@ -548,11 +548,14 @@ __global__ void k_scan_top(uint2* __restrict__ tile_tot, int ntiles, uint32_t* _
 
 // final bucket starts; misc[2] / misc[3] = first / last partial slot of the
 // buckets with more than T partial slots (msm_combine_run: the reduction's
-// tree steps run over that range only)
+// tree steps run over that range only); also resets the owner words of the
+// partial slots to ~0 (the accumulation marks the slots it writes; no fill launch)
 __global__ void k_scan_add(const uint2* __restrict__ tile_off, size_t nb, uint32_t* __restrict__ bstart,
                            const uint32_t* __restrict__ counts, uint32_t L, uint32_t T,
-                           uint32_t* __restrict__ misc, uint32_t gen) {
+                           uint32_t* __restrict__ misc, uint32_t gen, uint32_t* __restrict__ owner,
+                           size_t nslots) {
   size_t i = (size_t)blockIdx.x * blockDim.x + threadIdx.x;
+  for (size_t o = i; o < nslots; o += (size_t)gridDim.x * blockDim.x) owner[o] = 0xffffffffu;
   if (i >= nb) return;
   if (i == 0) misc[4] = gen;  // tag of this run's plan words (checked by the reader)
   uint2 off = tile_off[i / SCAN_TILE];
@@ -920,11 +923,11 @@ __device__ __forceinline__ void msm_fold(X29& A, X29 Y, int gl, uint32_t mv, int
 // level 1 (grid.y = MSM of the batch): fold group w (2^gl lanes) writes
 // A_out[w], Y_out[w] with sum_j (j + 1) B_j = sum_w A_w + w Y_w
 __global__ void __launch_bounds__(MSM_BLOCK)
-    k_msm_bsum(const MsmRed* __restrict__ runs, uint32_t nb, int slog, int gl,
+    k_msm_bsum(const MsmRed* __restrict__ runs, MsmRed r0, uint32_t nb, int slog, int gl,
                G1Xyzz* __restrict__ A_out, G1Xyzz* __restrict__ Y_out, size_t ostride) {
 #if defined(__HIP_DEVICE_COMPILE__)
   const uint32_t t = blockIdx.x * blockDim.x + threadIdx.x;
-  const MsmRed rr = runs[blockIdx.y];
+  const MsmRed rr = runs ? runs[blockIdx.y] : r0;  // a lone MSM's run comes by value
   X29 run = x29_inf(), wsum = x29_inf(), B = x29_inf();
   const uint64_t lo64 = (uint64_t)t << slog;
   const uint32_t lo = lo64 < nb ? (uint32_t)lo64 : nb;
@@ -1313,7 +1316,7 @@ static MsmRun msm_accumulate_phase(qg_ctx* ctx, const qg_srs* srs, const Fr* d_s
       QG_LAUNCH_CHECK();
       run.gen = ++ctx->msm_gen;
       hipLaunchKernelGGL(k_scan_add, dim3(div_up(nb, 256)), dim3(256), 0, ctx->stream, tile_tot,
-                         (size_t)nb, bstart, counts, L, T, misc, run.gen);
+                         (size_t)nb, bstart, counts, L, T, misc, run.gen, owner, nslots);
       QG_LAUNCH_CHECK();
       {
         QG_CHECK(slot >= 0 && slot < MSM_MAX_BATCH, QG_ERR_UNSUPPORTED, "MSM batch too large");
@@ -1334,7 +1337,6 @@ static MsmRun msm_accumulate_phase(qg_ctx* ctx, const qg_srs* srs, const Fr* d_s
                          entries);
       QG_LAUNCH_CHECK();
     }
-    QG_HIP(hipMemsetAsync(owner, 0xff, nslots * sizeof(uint32_t), ctx->stream));
     {
       QgTimed tm(ctx, "msm_accumulate");
       // the prefetching form for the largest MSMs only (2^27+ entries: 2^24
@@ -1443,10 +1445,12 @@ static void msm_reduce_phase(qg_ctx* ctx, const qg_srs* srs, const std::vector<M
       }
       h_runs[q] = {r.partial, r.bstart, r.L, r.T};
     }
-    QG_HIP(hipMemcpyAsync(d_runs, h_runs.data(), kl * sizeof(MsmRed), hipMemcpyHostToDevice,
-                          ctx->stream));
-    hipLaunchKernelGGL(k_msm_bsum, dim3(g1, kl), dim3(MSM_BLOCK), 0, ctx->stream, d_runs, nb,
-                       slog1, gl1, A1, Y1, (size_t)m1);
+    if (kl > 1)
+      QG_HIP(hipMemcpyAsync(d_runs, h_runs.data(), kl * sizeof(MsmRed), hipMemcpyHostToDevice,
+                            ctx->stream));
+    hipLaunchKernelGGL(k_msm_bsum, dim3(g1, kl), dim3(MSM_BLOCK), 0, ctx->stream,
+                       kl > 1 ? (const MsmRed*)d_runs : nullptr, h_runs[0], nb, slog1, gl1, A1, Y1,
+                       (size_t)m1);
     QG_LAUNCH_CHECK();
     // wave folds, 64 elements per wave, until one element per MSM is left
     G1Xyzz *Ai = A1, *Yi = Y1, *Ao = A2, *Yo = Y2;
