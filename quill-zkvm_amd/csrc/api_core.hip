@@ -1,4 +1,5 @@
 // C-ABI core: context, transcript, serialization, device Fr vectors.
+#include <atomic>
 #include <string.h>
 
 #include "blake3.h"
@@ -190,7 +191,7 @@ int qg_ctx_destroy(qg_ctx* ctx) {
   if (ctx->stream) (void)hipStreamSynchronize(ctx->stream);
   if (ctx->copy_stream) (void)hipStreamSynchronize(ctx->copy_stream);
   comm_release(ctx);
-  for (auto& kv : ctx->scratch) (void)hipFree(kv.second.first);
+  ctx->arena.release_all();
   for (auto& kv : ctx->pinned) (void)hipHostFree(kv.second.first);
   for (auto& kv : ctx->pending) {
     (void)hipEventDestroy(kv.second.a);
@@ -273,6 +274,12 @@ int qg_g1_serialize(const uint64_t xy[8], uint8_t infinity, uint8_t out[64]) {
 }
 
 // ---- device vectors -------------------------------------------------------
+// allocation ids of qg_buf (process-wide, never reused)
+static uint64_t next_buf_id() {
+  static std::atomic<uint64_t> next{0};
+  return ++next;
+}
+
 int qg_buf_create(qg_ctx* ctx, size_t n, qg_buf** out) {
   if (!ctx || !out) return QG_ERR_INVALID;
   *out = nullptr;
@@ -281,6 +288,7 @@ int qg_buf_create(qg_ctx* ctx, size_t n, qg_buf** out) {
     qg_buf* b = new qg_buf();
     b->ctx = ctx;
     b->n = n;
+    b->alloc_id = next_buf_id();
     hipError_t e = hipMalloc(&b->d, (n ? n : 1) * sizeof(Fr));
     if (e != hipSuccess) {
       delete b;
@@ -336,6 +344,8 @@ int qg_buf_view(qg_buf* base, size_t offset, size_t n, qg_buf** out) {
     b->n = n;
     b->d = base->d + offset;
     b->owned = false;
+    b->alloc_id = base->alloc_id;
+    b->base_off = base->base_off + offset;
     *out = b;
   });
 }

@@ -9,6 +9,7 @@
 #include <vector>
 
 #include "../../include/quill_gpu.h"
+#include "arena.h"
 #include "curve.h"
 #include "field.h"
 
@@ -37,6 +38,16 @@ struct Error : std::runtime_error {
 
 inline unsigned div_up(size_t a, size_t b) { return (unsigned)((a + b - 1) / b); }
 
+// device-memory backend of the scratch arena (arena.h)
+struct HipAlloc {
+  static void* alloc(size_t b) {
+    void* p = nullptr;
+    QG_HIP(hipMalloc(&p, b));
+    return p;
+  }
+  static void release(void* p) { (void)hipFree(p); }
+};
+
 }  // namespace qg
 
 struct qg_comm_state;  // RCCL (comm.hip)
@@ -46,8 +57,11 @@ struct qg_ctx {
   hipStream_t stream = nullptr;
   hipStream_t copy_stream = nullptr;  // host-to-device uploads overlapped with kernels (msm_host)
   std::string last_error;
-  // grow-only scratch arena, one slot per purpose
-  std::map<std::string, std::pair<void*, size_t>> scratch;
+  // grow-only scratch arena, one slot per purpose; every (re)allocation and
+  // every table build gets a fresh generation number (arena.h), which caches
+  // key on instead of device addresses
+  qg::ScratchArena<qg::HipAlloc> arena;
+  qg::LruSlots<4> twm_lru;  // S polynomial: w^{j(M-1)} tables per (logn, M)
   // timing
   bool timing = false;
   struct Ev {
@@ -80,19 +94,8 @@ struct qg_ctx {
     return cus;
   }
 
-  void* scratch_get(const std::string& slot, size_t bytes) {
-    auto it = scratch.find(slot);
-    if (it != scratch.end() && it->second.second >= bytes) return it->second.first;
-    if (it != scratch.end()) {
-      QG_HIP(hipFree(it->second.first));
-      scratch.erase(it);
-    }
-    void* p = nullptr;
-    size_t b = bytes ? bytes : 16;
-    QG_HIP(hipMalloc(&p, b));
-    scratch[slot] = {p, b};
-    return p;
-  }
+  void* scratch_get(const std::string& slot, size_t bytes) { return arena.get(slot, bytes); }
+  uint64_t scratch_gen(const std::string& slot) const { return arena.gen(slot); }
   template <class T>
   T* scratch_as(const std::string& slot, size_t count) {
     return reinterpret_cast<T*>(scratch_get(slot, count * sizeof(T)));
@@ -166,6 +169,10 @@ struct qg_buf {
   size_t n = 0;
   qg::Fr* d = nullptr;
   bool owned = true;  // false: a view into another buffer (qg_buf_view)
+  // identity of the allocation behind d (never reused, unlike the address) and
+  // d's offset in it: what transform caches key on (s_poly_device's F)
+  uint64_t alloc_id = 0;
+  size_t base_off = 0;
 };
 
 struct qg_srs {

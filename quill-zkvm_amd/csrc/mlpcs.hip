@@ -430,30 +430,33 @@ __global__ void __launch_bounds__(NTT_THREADS)
   }
 }
 
-// the stage pyramid of a flat twiddle table (cached per table and size)
-static const Fr* ntt_pyramid(qg_ctx* ctx, const Fr* flat, int logn) {
-  const std::string tag = "ntt_pyr_" + std::to_string((uintptr_t)flat);
+// the stage pyramid of the flat twiddle table in scratch slot `src` (one
+// derived slot per source slot; valid for the source's current build stamp and
+// its own allocation generation, never for an address)
+static const Fr* ntt_pyramid(qg_ctx* ctx, const Fr* flat, const std::string& src, int logn) {
+  const std::string tag = "ntt_pyr:" + src;
   const size_t n = (size_t)1 << logn;
   Fr* pyr = ctx->scratch_as<Fr>(tag, std::max<size_t>(1, n - 1));
-  const std::string memo = std::to_string(logn) + "@" + std::to_string((uintptr_t)pyr);
-  if (ctx->memo[tag] != memo) {
+  const uint64_t st = ctx->arena.stamp(src);
+  const std::string key = ctx->arena.derived_key(std::to_string(logn), st, ctx->scratch_gen(tag));
+  if (!ctx->arena.check_or_set(tag, key, st)) {
     hipLaunchKernelGGL(k_tw_pyramid, dim3(div_up(n, 256)), dim3(256), 0, ctx->stream, flat, logn,
                        pyr);
     QG_LAUNCH_CHECK();
-    ctx->memo[tag] = memo;
   }
   return pyr;
 }
 
 // runs every pass in place on `a` (the first pass reads `in`), direction by DIF
-static void ntt_run(qg_ctx* ctx, bool dif, const Fr* in, size_t nin, Fr* a, const Fr* tw, int logn,
-                    size_t win_lo, size_t win_hi, Fr* win_out) {
+static void ntt_run(qg_ctx* ctx, bool dif, const Fr* in, size_t nin, Fr* a, const Fr* tw,
+                    const std::string& tw_slot, int logn, size_t win_lo, size_t win_hi,
+                    Fr* win_out) {
   // QG_NTT_FLAT=1: twiddles from the flat table (A/B runs)
   static const bool flat = [] {
     const char* e = getenv("QG_NTT_FLAT");
     return e && atoi(e) != 0;
   }();
-  const Fr* pyr = flat ? tw : ntt_pyramid(ctx, tw, logn);
+  const Fr* pyr = flat ? tw : ntt_pyramid(ctx, tw, tw_slot, logn);
   const int pmode = flat ? 0 : 1;
   std::vector<NttPass> plan = ntt_plan(logn);
   if (dif) std::reverse(plan.begin(), plan.end());
@@ -548,15 +551,17 @@ static Fr root_of_unity(int logn) {
 static Fr ml_plain_mul(const Fr& x, const Fr& y) { return from_mont(to_mont(x) * to_mont(y)); }
 
 // twiddle tables w^k 2^261 (k < n/2) for w = root_of_unity(logn) and its
-// inverse, cached per transform size
+// inverse in scratch slots `tag` and `tag`+"i", cached per transform size and
+// allocation generation; every build stamps both slots, which invalidates the
+// tables derived from them (ntt_pyramid, ntt_tw_bitrev)
 static void ntt_twiddles(qg_ctx* ctx, int logn, Fr** tw, Fr** twi,
                          const std::string& tag = "ntt_tw") {
   const size_t n = (size_t)1 << logn, h = std::max<size_t>(n / 2, 1);
   *tw = ctx->scratch_as<Fr>(tag, h);
   *twi = ctx->scratch_as<Fr>(tag + "i", h);
-  const std::string memo = std::to_string(logn) + "@" + std::to_string((uintptr_t)*tw) + "," +
-                           std::to_string((uintptr_t)*twi);
-  if (ctx->memo[tag] == memo) return;
+  const std::string key = std::to_string(logn) + "|g" + std::to_string(ctx->scratch_gen(tag)) +
+                          "," + std::to_string(ctx->scratch_gen(tag + "i"));
+  if (ctx->arena.check_or_set(tag, key)) return;
   const Fr w = root_of_unity(logn), wi = finv(w);
   const int K = 64;
   const L9 c = F29P<FrP>::TO261;
@@ -570,15 +575,8 @@ static void ntt_twiddles(qg_ctx* ctx, int logn, Fr** tw, Fr** twi,
   QG_LAUNCH_CHECK();
   hipLaunchKernelGGL(k_fr_to261, dim3(div_up(h, 256)), dim3(256), 0, ctx->stream, *twi, h, c);
   QG_LAUNCH_CHECK();
-  ctx->memo[tag] = memo;
-  // the tables derived from a flat table (ntt_pyramid, ntt_tw_bitrev) are
-  // cached by its address: a table (re)built here may sit where another one
-  // was (scratch regrowth frees buffers and hipMalloc reuses addresses), with
-  // the same logn but other content (forward vs inverse) - drop them
-  for (const Fr* t : {*tw, *twi}) {
-    ctx->memo.erase("ntt_pyr_" + std::to_string((uintptr_t)t));
-    ctx->memo.erase("ntt_twb_" + std::to_string((uintptr_t)t));
-  }
+  ctx->arena.bump(tag);
+  ctx->arena.bump(tag + "i");
 }
 
 // Transform of the eq table without an NTT.  g = eq(., z) over nz variables is
@@ -615,17 +613,18 @@ __global__ void k_tw_bitrev(const Fr* __restrict__ tw, int logn, size_t h, Fr* _
   twb[i] = tw[j];
 }
 
-// the flat twiddle table in bit-reversed order (cached per table and size)
-static const Fr* ntt_tw_bitrev(qg_ctx* ctx, const Fr* tw, int logn) {
-  const std::string tag = "ntt_twb_" + std::to_string((uintptr_t)tw);
+// the flat twiddle table of scratch slot `src` in bit-reversed order (keyed
+// like ntt_pyramid)
+static const Fr* ntt_tw_bitrev(qg_ctx* ctx, const Fr* tw, const std::string& src, int logn) {
+  const std::string tag = "ntt_twb:" + src;
   const size_t h = logn > 1 ? (size_t)1 << (logn - 1) : 1;
   Fr* twb = ctx->scratch_as<Fr>(tag, h);
-  const std::string memo = std::to_string(logn) + "@" + std::to_string((uintptr_t)twb);
-  if (ctx->memo[tag] != memo) {
+  const uint64_t st = ctx->arena.stamp(src);
+  const std::string key = ctx->arena.derived_key(std::to_string(logn), st, ctx->scratch_gen(tag));
+  if (!ctx->arena.check_or_set(tag, key, st)) {
     hipLaunchKernelGGL(k_tw_bitrev, dim3(div_up(h, 256)), dim3(256), 0, ctx->stream, tw, logn, h,
                        twb);
     QG_LAUNCH_CHECK();
-    ctx->memo[tag] = memo;
   }
   return twb;
 }
@@ -640,11 +639,14 @@ static L9 l9_of29(const Fr& x) {
 // S polynomial (M - 1 coefficients, untrimmed) of f (nf) and g (ng), device in/out.
 // eq_z (nz variables, host Montgomery): g is eq(., eq_z) over 2^nz entries, and
 // its transform comes from the product formula (k_eqdft_level) instead of an NTT.
-// reuse_f: the caller guarantees f's contents are unchanged since the last call
-// that transformed this same buffer; F is then reused when this context still
-// holds that transform (memo "ntt_F_src": source pointer, length, size, F).
+// f_id: the allocation id of the qg_buf behind f (qg_buf::alloc_id, never
+// reused; 0 = unknown).  reuse_f: the caller guarantees f's contents are
+// unchanged since the last call that transformed this same buffer; F is then
+// reused when this context still holds that transform (arena memo "ntt_F_src":
+// f's allocation id and offset, length, size, and the generation of F's slot).
 static void s_poly_device(qg_ctx* ctx, const Fr* f, size_t nf, const Fr* g, size_t ng, Fr* S,
-                          const uint64_t* eq_z = nullptr, size_t nz = 0, bool reuse_f = false) {
+                          const uint64_t* eq_z = nullptr, size_t nz = 0, bool reuse_f = false,
+                          uint64_t f_id = 0, size_t f_off = 0) {
   const size_t M = nf > ng ? nf : ng;
   if (M <= 1) return;
   QgTimed tm(ctx, "s_polynomial");
@@ -662,13 +664,13 @@ static void s_poly_device(qg_ctx* ctx, const Fr* f, size_t nf, const Fr* g, size
   // prover alternating between a few opening sizes (HyperPlonk: the witness
   // and its public rows) does not rebuild it per opening.
   const std::string twm_key = std::to_string(logn) + ":" + std::to_string(M);
-  const std::string twm_slot =
-      "ntt_twM#" + std::to_string(std::hash<std::string>{}(twm_key) % 4);
+  bool twm_hit = false;  // the memo below decides; the LRU only picks the slot
+  const std::string twm_slot = "ntt_twM#" + std::to_string(ctx->twm_lru.slot_for(twm_key, &twm_hit));
   Fr* twM = ctx->scratch_as<Fr>(twm_slot, n);
   Fr *tw, *twi;
   ntt_twiddles(ctx, logn, &tw, &twi);
-  const std::string twm_memo = twm_key + "@" + std::to_string((uintptr_t)twM);
-  if (ctx->memo[twm_slot] != twm_memo) {
+  const std::string twm_memo = ctx->arena.derived_key(twm_key, 1, ctx->scratch_gen(twm_slot));
+  if (!ctx->arena.check_or_set(twm_slot, twm_memo)) {
     const Fr w = root_of_unity(logn);
     const Fr wM = fpow_small(w, (uint64_t)(M - 1));
     const int K = 64;
@@ -685,20 +687,22 @@ static void s_poly_device(qg_ctx* ctx, const Fr* f, size_t nf, const Fr* g, size
     hipLaunchKernelGGL(k_fr_to261_br, dim3(div_up(n, 256)), dim3(256), 0, ctx->stream, H, logn, c9,
                        twM);
     QG_LAUNCH_CHECK();
-    ctx->memo[twm_slot] = twm_memo;
   }
   // forward DIF of f and g (zero-extended), bit-reversed outputs
-  const std::string fkey = std::to_string((uintptr_t)f) + ":" + std::to_string(nf) + ":" +
-                           std::to_string(logn) + "@" + std::to_string((uintptr_t)F);
-  if (!(reuse_f && ctx->memo["ntt_F_src"] == fkey)) {
-    ctx->memo["ntt_F_src"].clear();
-    ntt_run(ctx, true, f, nf, F, tw, logn, 0, 0, nullptr);
-    ctx->memo["ntt_F_src"] = fkey;
+  const std::string fkey =
+      f_id ? ctx->arena.derived_key(std::to_string(f_id) + "+" + std::to_string(f_off) + ":" +
+                                        std::to_string(nf) + ":" + std::to_string(logn),
+                                    ctx->arena.stamp("ntt_tw"), ctx->scratch_gen("ntt_F"))
+           : std::string();
+  if (!(reuse_f && f_id && ctx->arena.memo["ntt_F_src"] == fkey)) {
+    ctx->arena.memo["ntt_F_src"].clear();
+    ntt_run(ctx, true, f, nf, F, tw, "ntt_tw", logn, 0, 0, nullptr);
+    ctx->arena.memo["ntt_F_src"] = fkey;
   }
   if (eq_z && nz >= 1 && ((size_t)1 << nz) == ng && (int)nz < logn) {
     // levels t = nz-1 .. 0 ping-pong between G and H (H is free until the combine),
     // ending in G (t = 0: 2^logn entries, bit-reversed order)
-    const Fr* twb = ntt_tw_bitrev(ctx, tw, logn);
+    const Fr* twb = ntt_tw_bitrev(ctx, tw, "ntt_tw", logn);
     for (int t = (int)nz - 1; t >= 0; t--) {
       const Fr z = fr_import(eq_z + 4 * t);
       const Fr zp = from_mont(z), ap = from_mont(Fr::one() - z);
@@ -712,14 +716,14 @@ static void s_poly_device(qg_ctx* ctx, const Fr* f, size_t nf, const Fr* g, size
       QG_LAUNCH_CHECK();
     }
   } else {
-    ntt_run(ctx, true, g, ng, G, tw, logn, 0, 0, nullptr);
+    ntt_run(ctx, true, g, ng, G, tw, "ntt_tw", logn, 0, 0, nullptr);
   }
   hipLaunchKernelGGL(k_s_combine_br, dim3(div_up(n, 256)), dim3(256), 0, ctx->stream, F, G, twM,
                      logn, H);
   QG_LAUNCH_CHECK();
   // inverse DIT of H (bit-reversed in, natural out); the last pass writes only
   // h[M .. 2M-1) = S
-  ntt_run(ctx, false, H, n, H, twi, logn, M, 2 * M - 1, S);
+  ntt_run(ctx, false, H, n, H, twi, "ntt_twi", logn, M, 2 * M - 1, S);
 }
 
 // highest nonzero index + 1: per-thread max over a grid-stride range of
@@ -1076,7 +1080,7 @@ static void s_poly_sharded(qg_ctx* ctx, const Fr* f, size_t M, const uint64_t* p
     hipLaunchKernelGGL(k_s_presum, dim3(div_up(B, ML_BLOCK)), dim3(ML_BLOCK), 0, ctx->stream, f, M,
                        B, hb, cw, pw, tmp);
     QG_LAUNCH_CHECK();
-    ntt_run(ctx, true, tmp, B, Fq, twB, lb, 0, 0, nullptr);
+    ntt_run(ctx, true, tmp, B, Fq, twB, "sp_tw", lb, 0, 0, nullptr);
     // G at residue cc: levels above the block collapse into a host constant,
     // then one launch per level t = lb - 1 .. 0 (ping-pong tmp / Gq; nz >= lb
     // whenever W >= 2; at W = 1, nz = lb - 1 and the top level starts from q0 = 1)
@@ -1087,7 +1091,7 @@ static void s_poly_sharded(qg_ctx* ctx, const Fr* f, size_t M, const uint64_t* p
       q0 = q0 * ((Fr::one() - zt) + zt * fpow_small(w, (uint64_t)cc << t));
     }
     const int top = (int)std::min<size_t>(nz, (size_t)lb);
-    const Fr* twBb = ntt_tw_bitrev(ctx, twB, lb);
+    const Fr* twBb = ntt_tw_bitrev(ctx, twB, "sp_tw", lb);
     const Fr* qn = nullptr;
     for (int t = top - 1; t >= 0; t--) {
       const Fr zt = fr_import(point + 4 * t);
@@ -1109,10 +1113,10 @@ static void s_poly_sharded(qg_ctx* ctx, const Fr* f, size_t M, const uint64_t* p
   if (c & 1) cst = fneg(cst);
   const L9 cst9 = l9_of29(ml_plain_mul(from_mont(cst), pow2_mod_plain<FrP>(266)));
   hipLaunchKernelGGL(k_s_combine_res, dim3(div_up(B, ML_BLOCK)), dim3(ML_BLOCK), 0, ctx->stream, Fb,
-                     Gb, Fm, Gm, (int)c, ntt_tw_bitrev(ctx, twiB, lb), lb, cst9, W == 1 ? 1 : 0,
+                     Gb, Fm, Gm, (int)c, ntt_tw_bitrev(ctx, twiB, "sp_twi", lb), lb, cst9, W == 1 ? 1 : 0,
                      H);
   QG_LAUNCH_CHECK();
-  ntt_run(ctx, false, H, B, H, twiB, lb, 0, 0, nullptr);
+  ntt_run(ctx, false, H, B, H, twiB, "sp_twi", lb, 0, 0, nullptr);
   Fr* P = tmp + B;
   hipLaunchKernelGGL(k_powers_ml, dim3(div_up(div_up(B, (size_t)K), ML_BLOCK)), dim3(ML_BLOCK), 0,
                      ctx->stream, fpow_small(wi, c), B, K, P);
@@ -1209,7 +1213,8 @@ static void mle_open_sharded(qg_ctx* ctx, const qg_srs* srs, const Fr* dpoly, si
 // MLEvalProof::prove (mlpcs.rs:83-124) on a device-resident evaluation vector
 static void mle_open_device(qg_ctx* ctx, const qg_srs* srs, const Fr* dpoly, size_t n,
                             const uint64_t* point, size_t nvars, uint8_t state[32],
-                            qg_mle_proof* out, bool unchanged = false) {
+                            qg_mle_proof* out, bool unchanged = false, uint64_t poly_id = 0,
+                            size_t poly_off = 0) {
   if (ctx->sharded) return mle_open_sharded(ctx, srs, dpoly, n, point, nvars, state, out);
   const size_t N = (size_t)1 << nvars;
   Fr* dz = ctx->scratch_as<Fr>("mle_z", nvars ? nvars : 1);
@@ -1224,7 +1229,7 @@ static void mle_open_device(qg_ctx* ctx, const qg_srs* srs, const Fr* dpoly, siz
   Fr* dS = ctx->scratch_as<Fr>("mle_S", M > 1 ? M - 1 : 1);
   size_t Slen = 0;
   if (M > 1) {
-    s_poly_device(ctx, dpoly, n, dpr, N, dS, point, nvars, unchanged);
+    s_poly_device(ctx, dpoly, n, dpr, N, dS, point, nvars, unchanged, poly_id, poly_off);
     Slen = trimmed_len(ctx, dS, M - 1);
   }
   QG_CHECK(Slen <= srs->n, QG_ERR_INVALID, "Polynomial degree exceeds max degree");
@@ -1338,7 +1343,7 @@ int qg_mle_open_dev_ex(qg_ctx* ctx, const qg_srs* srs, const qg_buf* poly, size_
     QG_CHECK(nvars <= 30, QG_ERR_INVALID, "too many variables");
     QG_HIP(hipSetDevice(ctx->device));
     mle_open_device(ctx, srs, poly->d, n, point, nvars, state, out,
-                    (flags & QG_OPEN_UNCHANGED) != 0);
+                    (flags & QG_OPEN_UNCHANGED) != 0, poly->alloc_id, poly->base_off);
   });
 }
 

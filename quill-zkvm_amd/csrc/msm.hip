@@ -3,23 +3,25 @@
 // (ark-ec 0.5.0 VariableBaseMSM) and the SRS handling of KZG::commit
 // (kzg.rs:61-73) / KZG::trusted_setup (kzg.rs:35-59).
 //
-// Design (MI355X-first; see DESIGN.md "MSM"):
-//  * The SRS lives in HBM as affine points (64 B each, (0,0) = infinity) together
-//    with W-1 window-shifted copies table[w][i] = 2^(c*w) * P_i.  288 GB of HBM
-//    makes this cheap (2^24 bases, c = 21: 13 tables, 14 GB) and it removes the
-//    serial window-combination doublings: every signed c-bit digit of every
-//    scalar lands in ONE shared set of 2^(c-1) buckets.
-//  * Bucketing is a counting sort: count (atomics) -> scan -> scatter (atomics).
-//    Digits are recomputed from the scalars in the scatter pass (32 B/scalar)
-//    instead of materializing n*W keys.
+// Design (MI355X-first):
+//  * The SRS lives in HBM as W window-shifted tables table[w][i] = 2^(c*w) * P_i,
+//    one 128-B row per point (x, y and p - y in 9 x 29-bit limbs + flags, so a
+//    negative digit costs no arithmetic).  288 GB of HBM makes this affordable
+//    (2^24 bases, c = 20: 13 tables, 27.9 GB, built once per SRS outside any
+//    commitment) and removes the serial window-combination doublings: every
+//    signed c-bit digit of every scalar lands in ONE shared set of 2^(c-1)
+//    buckets.
+//  * Bucketing is a two-pass LDS radix sort (pass A by bucket-high bits over
+//    512-scalar tiles, pass B by bucket-low bits within 8192-entry chunks);
+//    digits come from the canonical scalars by funnel shifts.
 //  * Accumulation is load-balanced: the bucket-sorted entries are cut into
-//    equal chunks (a whole number of waves of resident threads), one thread
-//    per chunk, so skewed digit distributions (small witness values, the
-//    short top window) do not serialize on one lane.  Mixed XYZZ + affine
-//    additions (8M + 2S), no inversions.
-//  * Bucket reduction sum_j (j+1) B_j: running sums over segments of S
-//    buckets, one per SIMD lane of the chip, then shuffle-only wave folds
-//    (suffix scan + tree) 64 elements at a time; no bucket array, no LDS.
+//    flat chunks of L entries, one thread per chunk, so skewed digit
+//    distributions (small witness values, the short top window) do not
+//    serialize on one lane.  Mixed XYZZ + affine additions (8M + 2S), no
+//    inversions; a raw partial is flushed at every bucket boundary.
+//  * Bucket reduction sum_j (j+1) B_j: each lane sums its buckets' partial
+//    slots on the fly with running sums from the top, then shuffle folds
+//    (suffix scan + tree) and three quad-cooperative folds of 16.
 #include <stdlib.h>
 
 #include "common.h"
@@ -769,6 +771,13 @@ struct MsmRed {
   const uint32_t* bstart;
   uint32_t L, T;
 };
+// the runs of a batch of up to MSM_RED_BYVAL MSMs travel as a kernel argument
+// (no host-to-device copy queued behind the accumulation: a pageable copy can
+// block the host until the stream drains); larger batches copy an array
+constexpr uint32_t MSM_RED_BYVAL = 8;
+struct MsmRedSet {
+  MsmRed r[MSM_RED_BYVAL];
+};
 
 #if defined(__HIP_DEVICE_COMPILE__)
 __device__ __forceinline__ Q29 q29_shfl_down(const Q29& a, uint32_t d, int width) {
@@ -923,11 +932,11 @@ __device__ __forceinline__ void msm_fold(X29& A, X29 Y, int gl, uint32_t mv, int
 // level 1 (grid.y = MSM of the batch): fold group w (2^gl lanes) writes
 // A_out[w], Y_out[w] with sum_j (j + 1) B_j = sum_w A_w + w Y_w
 __global__ void __launch_bounds__(MSM_BLOCK)
-    k_msm_bsum(const MsmRed* __restrict__ runs, MsmRed r0, uint32_t nb, int slog, int gl,
+    k_msm_bsum(const MsmRed* __restrict__ runs, MsmRedSet rs, uint32_t nb, int slog, int gl,
                G1Xyzz* __restrict__ A_out, G1Xyzz* __restrict__ Y_out, size_t ostride) {
 #if defined(__HIP_DEVICE_COMPILE__)
   const uint32_t t = blockIdx.x * blockDim.x + threadIdx.x;
-  const MsmRed rr = runs ? runs[blockIdx.y] : r0;  // a lone MSM's run comes by value
+  const MsmRed rr = runs ? runs[blockIdx.y] : rs.r[blockIdx.y];  // small batches by value
   X29 run = x29_inf(), wsum = x29_inf(), B = x29_inf();
   const uint64_t lo64 = (uint64_t)t << slog;
   const uint32_t lo = lo64 < nb ? (uint32_t)lo64 : nb;
@@ -1424,8 +1433,8 @@ static void msm_reduce_phase(qg_ctx* ctx, const qg_srs* srs, const std::vector<M
   G1Xyzz* A2 = ctx->scratch_as<G1Xyzz>("msm_redA2", (size_t)kl * m2);
   G1Xyzz* Y2 = ctx->scratch_as<G1Xyzz>("msm_redY2", (size_t)kl * m2);
   G1Xyzz* d_out = ctx->scratch_as<G1Xyzz>("msm_out", kl);
-  MsmRed* d_runs = ctx->scratch_as<MsmRed>("msm_runs", kl);
   std::vector<MsmRed> h_runs(kl);
+  MsmRedSet rset{};
   {
     QgTimed tm(ctx, "msm_reduce");
     // tree steps only until every bucket has <= T partials left;
@@ -1444,13 +1453,17 @@ static void msm_reduce_phase(qg_ctx* ctx, const qg_srs* srs, const std::vector<M
         st <<= 1;
       }
       h_runs[q] = {r.partial, r.bstart, r.L, r.T};
+      if (q < MSM_RED_BYVAL) rset.r[q] = h_runs[q];
     }
-    if (kl > 1)
-      QG_HIP(hipMemcpyAsync(d_runs, h_runs.data(), kl * sizeof(MsmRed), hipMemcpyHostToDevice,
+    const MsmRed* d_runs = nullptr;
+    if (kl > MSM_RED_BYVAL) {
+      MsmRed* d = ctx->scratch_as<MsmRed>("msm_runs", kl);
+      QG_HIP(hipMemcpyAsync(d, h_runs.data(), kl * sizeof(MsmRed), hipMemcpyHostToDevice,
                             ctx->stream));
-    hipLaunchKernelGGL(k_msm_bsum, dim3(g1, kl), dim3(MSM_BLOCK), 0, ctx->stream,
-                       kl > 1 ? (const MsmRed*)d_runs : nullptr, h_runs[0], nb, slog1, gl1, A1, Y1,
-                       (size_t)m1);
+      d_runs = d;
+    }
+    hipLaunchKernelGGL(k_msm_bsum, dim3(g1, kl), dim3(MSM_BLOCK), 0, ctx->stream, d_runs, rset, nb,
+                       slog1, gl1, A1, Y1, (size_t)m1);
     QG_LAUNCH_CHECK();
     // wave folds, 64 elements per wave, until one element per MSM is left
     G1Xyzz *Ai = A1, *Yi = Y1, *Ao = A2, *Yo = Y2;

@@ -2622,11 +2622,12 @@ static void sumcheck_run(qg_ctx* ctx, uint32_t nvars, uint32_t ntables,
   const size_t io_bytes = o_lens + sizeof(uint32_t) * nvars;
   uint8_t* io = ctx->scratch_as<uint8_t>("sc_io", io_bytes);
   SopDev* d_sp = ctx->scratch_as<SopDev>("sc_prog", 1);
-  const std::string memo = std::to_string(P->id) + "@" + std::to_string((uintptr_t)d_sp);
-  if (ctx->memo["sc_prog"] != memo) {
+  // the device copy holds program P->id while the slot's allocation generation
+  // is unchanged (arena.h: never an address)
+  const std::string memo =
+      ctx->arena.derived_key(std::to_string(P->id), 1, ctx->scratch_gen("sc_prog"));
+  if (!ctx->arena.check_or_set("sc_prog", memo))
     QG_HIP(hipMemcpyAsync(d_sp, &P->img, sizeof(SopDev), hipMemcpyHostToDevice, ctx->stream));
-    ctx->memo["sc_prog"] = memo;
-  }
   uint8_t* hio = reinterpret_cast<uint8_t*>(ctx->pinned_get("sc_io", io_bytes));
   memset(hio, 0, o_chal);
   memcpy(hio, &hs, sizeof hs);

@@ -128,3 +128,27 @@ def test_replicated_s_matches_split(world):
         rep = run_ranks(world, fn)
     assert split == rep
     assert all(x == split[0] for x in split)
+
+
+@pytest.mark.parametrize("n,small", [((1 << 11) + 3, False), (5000, False), (5000, True),
+                                     (1, False), (7, True), ((1 << 16) + 1, False)])
+def test_prefetch_accumulate_matches_default(n, small):
+    """k_msm_accumulate<true> (the prefetching loop the 2^24 headline takes) on
+    short and odd MSMs: chunks shorter than the prefetch distance,
+    bucket boundaries at a chunk's first entry (small scalars: few, crowded
+    buckets), a partial last group.  Bit-exact against the default loop and
+    against the trapdoor identity commit = [p(tau)] g."""
+    import quill_amd as q
+    rnd = random.Random(n * 7 + small)
+    tau = rnd.randrange(R)
+    scal = [rnd.randrange(1 << 12) if small else rnd.randrange(R) for _ in range(n)]
+    d = q.Device(0)
+    srs = q.Srs.generate(d, tau, n)
+    out = {}
+    for pf in ("0", "1"):
+        with env("QG_MSM_PF", pf):
+            out[pf] = srs.msm(scal)
+    srs.close()
+    d.close()
+    assert out["0"] == out["1"]
+    assert out["1"] == o.g1_mul(o.G1_GEN, o.poly_eval(scal, tau))
