@@ -34,6 +34,9 @@ HBM_PEAK_GBPS = 8000.0  # MI355X_MICROARCH.md: HBM3E 8.0 TB/s spec
 # partial products of one 9 x 9-limb Montgomery product (81 a*b + 81 m*p)
 VMAD_LANE_OPS_PER_S = 3.1186e13
 MADS_PER_FQ_MUL = 162
+# random whole-row (128 B, one coalesced request per row) gathers per second over a
+# 16 GiB table, micro/gather_bench.hip "coop 8 lanes x 16B of 128B" (profiles/r05_gather_bench.txt)
+COOP_GATHER_ROWS_PER_S = 3.37e10
 LOGUP_BYTES_PER_ROW = 128  # 3 x 32 B table reads + 32 B column write
 MSM_BYTES_PER_SCALAR = 96  # 32 B scalar + 64 B affine base
 MSM_FQMUL_PER_SCALAR = 176  # 16 signed windows x 11 Fq mults
@@ -310,16 +313,19 @@ def main():
         "dtype": "u256-montgomery (BN254 Fr scalars, Fq coordinates)",
         "data": "synthetic: SRS [tau^i]g from a fixed tau; uniform Fr scalars (xoshiro256**)",
         "config": {"workload": f"KZG commit / Pippenger G1 MSM, 2^{args.log_msm} BN254 scalars per GPU",
-                   "log_msm": args.log_msm, "parallelism": f"msm-shard-by-base-index x{world}"},
+                   "log_msm": args.log_msm, "parallelism": f"msm-shard-by-base-index x{world}",
+                   "srs": f"preprocessed once per SRS, outside the timed step: {n_win} "
+                          f"window-shifted tables 2^({c_bits}w) P_i (signed {c_bits}-bit digits), "
+                          f"128-B rows, {n_win * n * 128 / 1e9:.1f} GB"},
         "roofline": {"bound": "hbm", "kernel": "msm_accumulate", "achieved": achieved,
                      "peak": HBM_PEAK_GBPS, "unit": "GB/s", "frac": achieved / HBM_PEAK_GBPS,
                      "traffic": _headline_traffic(traffic),
                      "traffic_row_calibrated": _headline_traffic_row_calibrated(traffic),
                      "traffic_note": "traffic: FETCH_SIZE x2 (the guide's streaming-read "
                                      "correction) + WRITE_SIZE; traffic_row_calibrated: reads "
-                                     "rescaled so a calibration kernel's random 128-B row "
-                                     "gathers (k_msm_accumulate's load pattern) count 128 B "
-                                     "each (pmc._fetch_calibration)",
+                                     "rescaled so a calibration kernel's per-lane random 128-B "
+                                     "row gathers count 128 B each (pmc._fetch_calibration; "
+                                     "the cooperative kernel's whole-row reads need no rescale)",
                      "algorithmic_bytes": MSM_BYTES_PER_SCALAR * n,
                      "note": "MSM is integer-VALU bound (no MFMA form): see compute"},
         "compute": {"fq_mul_per_s_peak_microbench": fq_peak,
@@ -336,7 +342,13 @@ def main():
                     "issue_bound_note": "v_mad_u64_u32 lane-ops/s measured with every CU "
                                         "issuing (profiles/r01_isa_rates.json) / 162 partial "
                                         "products per 29-bit Montgomery multiply: a hardware "
-                                        "bound, independent of the microbenchmark"},
+                                        "bound, independent of the microbenchmark",
+                    "row_gathers_per_s": n_win * n / (acc_ms * 1e-3),
+                    "frac_gather_capacity": n_win * n / (acc_ms * 1e-3) / COOP_GATHER_ROWS_PER_S,
+                    "gather_note": "random 128-B table rows gathered per second (one per digit) / "
+                                   "the chip's measured capacity for whole-row coalesced "
+                                   "gathers over a 16 GiB table (micro/gather_bench.hip, "
+                                   "profiles/r05_gather_bench.txt)"},
         "kernels_ms": kern,
         "setup_s": setup_s,
         "commitment_x_low64": hex(0 if res is None else res[0] & ((1 << 64) - 1)),
@@ -880,36 +892,52 @@ def _kernel_traffic(traffic, kernel, grid=None):
     return d["read_bytes_per_launch"] + d["write_bytes_per_launch"]
 
 
+# the bucket-accumulation kernels, the headline's first: k_msm_accumulate_coop
+# (wave-cooperative row gathers, 2^25+ entries), k_msm_accumulate (per-lane)
+ACC_KERNELS = ("k_msm_accumulate_coop", "k_msm_accumulate")
+
+
+def _headline_acc(traffic):
+    """(kernel, PMC row) of the probe's headline-MSM accumulate: by its leg
+    marker, else the largest launch shape (the 2^log-msm MSM runs first)"""
+    for k in ACC_KERNELS:
+        leg = traffic.get(f"{k}#probe_msm")
+        if leg and "read_bytes_per_launch" in leg:
+            return k, leg
+    for k in ACC_KERNELS:
+        shapes = [x for x in traffic if x.startswith(f"{k}@")]
+        if shapes:
+            return k, traffic[max(shapes, key=lambda x: int(x.split("@")[1]))]
+    for k in ACC_KERNELS:
+        if k in traffic and "read_bytes_per_launch" in traffic[k]:
+            return k, traffic[k]
+    return None, None
+
+
 def _headline_traffic(traffic):
-    """PMC bytes per launch of the headline MSM's accumulate: the probe's FIRST
-    k_msm_accumulate launch shape (the 2^log-msm MSM runs first)"""
+    """PMC bytes per headline MSM of its accumulate (every launch of the probe's
+    headline leg / shape belongs to that MSM's pieces)"""
     if not traffic or "error" in traffic:
         return None
-    leg = traffic.get("k_msm_accumulate#probe_msm")
-    if leg and "read_bytes_per_launch" in leg:  # the probe's headline MSM, by its marker
-        return (leg["read_bytes_per_launch"] + leg["write_bytes_per_launch"]) * leg["launches"]
-    shapes = [k for k in traffic if k.startswith("k_msm_accumulate@")]
-    if not shapes:
-        return _kernel_traffic(traffic, "k_msm_accumulate")
-    big = max(shapes, key=lambda k: int(k.split("@")[1]))  # largest grid = 2^log-msm
-    d = traffic[big]
-    # per MSM: every launch of that shape in the probe belongs to its pieces
+    _, d = _headline_acc(traffic)
+    if d is None:
+        return None
     return (d["read_bytes_per_launch"] + d["write_bytes_per_launch"]) * max(d.get("launches", 1), 1)
 
 
 def _headline_traffic_row_calibrated(traffic):
     """the same bytes with the read side scaled by the row-gather calibration
-    (pmc_traffic.py CAL_*): random 128-B row gathers counted at 128 B each"""
+    (pmc_traffic.py CAL_*): per-lane random 128-B row gathers (five 16-B loads)
+    counted at 128 B each; the cooperative kernel reads whole 128-B rows in
+    coalesced requests, which FETCH_SIZE counts as they are (no rescaling)"""
     cal = (traffic or {}).get("_fetch_calibration")
     if not cal or "error" in traffic:
         return None
-    d = traffic.get("k_msm_accumulate#probe_msm")
-    if not d or "read_bytes_per_launch" not in d:
-        shapes = [k for k in traffic if k.startswith("k_msm_accumulate@")]
-        if not shapes:
-            return None
-        d = traffic[max(shapes, key=lambda k: int(k.split("@")[1]))]
-    return ((d["read_bytes_per_launch"] * cal["gather_read_factor"] + d["write_bytes_per_launch"])
+    k, d = _headline_acc(traffic)
+    if d is None:
+        return None
+    f = 1.0 if k == "k_msm_accumulate_coop" else cal["gather_read_factor"]
+    return ((d["read_bytes_per_launch"] * f + d["write_bytes_per_launch"])
             * max(d.get("launches", 1), 1))
 
 

@@ -605,6 +605,35 @@ __global__ void k_eqdft_level(const Fr* __restrict__ qnext, L9 a261, L9 z261,
   q[k] = from29(canon29(mul29(f, qn)));
 }
 
+// The small top levels of the same recursion in ONE launch (they were ~5 us
+// launches of a few thousand entries each): level tmin's entry k is
+//   Q_tmin[k] = prod_{t = tmin}^{nz-1} f_t(k >> (t - tmin)),
+// every factor from the same bit-reversed table (twb[k' >> 1], negated for odd
+// k'), two factors per step as interleaved products.  A thread per entry of
+// level tmin (2^(logn - tmin) <= EQ_TOP_LEN entries).
+static constexpr int EQ_TOP_MAXL = 32;
+static constexpr int EQ_TOP_LOG = 16;  // levels of <= 2^16 entries are fused
+struct EqTopConsts {
+  L9 a[EQ_TOP_MAXL], z[EQ_TOP_MAXL];  // level tmin + i: (1 - z_t), z_t in the 2^261 domain
+};
+__global__ void __launch_bounds__(256)
+    k_eqdft_top(EqTopConsts cs, uint32_t nlev, const Fr* __restrict__ twb, int logn, int tmin,
+                Fr* __restrict__ q) {
+  const size_t len = (size_t)1 << (logn - tmin);
+  const size_t k = (size_t)blockIdx.x * blockDim.x + threadIdx.x;
+  if (k >= len) return;
+  R29 acc = to29(Fr::one());
+  for (uint32_t i = 0; i < nlev; i++) {
+    const size_t kk = k >> i;
+    R29 w = to29(twb[kk >> 1]);
+    if (kk & 1) w = sub29(R29::zero(), w);  // lazy 4p - w
+    // a < p (host-canonical), the product < 2p: one conditional subtraction
+    const R29 f = red2p29(add29(R29::from_l9(cs.a[i]), mul29(R29::from_l9(cs.z[i]), w)));
+    acc = mul29(f, acc);  // arkworks form (x 2^256) kept: f carries 2^261
+  }
+  q[k] = from29(canon29(acc));
+}
+
 // twb[i] = tw[bitrev_{L-1}(i)] for i < 2^(L-1) (one entry for L <= 1)
 __global__ void k_tw_bitrev(const Fr* __restrict__ tw, int logn, size_t h, Fr* __restrict__ twb) {
   const size_t i = (size_t)blockIdx.x * blockDim.x + threadIdx.x;
@@ -703,13 +732,36 @@ static void s_poly_device(qg_ctx* ctx, const Fr* f, size_t nf, const Fr* g, size
     // levels t = nz-1 .. 0 ping-pong between G and H (H is free until the combine),
     // ending in G (t = 0: 2^logn entries, bit-reversed order)
     const Fr* twb = ntt_tw_bitrev(ctx, tw, "ntt_tw", logn);
-    for (int t = (int)nz - 1; t >= 0; t--) {
+    // the levels of <= 2^EQ_TOP_LOG entries (t >= tmin) in one launch into the
+    // array level tmin would have been written to, then one launch per level
+    static const bool eq_top = [] {
+      const char* e = getenv("QG_EQ_TOP");  // 0: one launch per level (A/B runs)
+      return !(e && atoi(e) == 0);
+    }();
+    int t_hi = (int)nz - 1;  // highest level still to run per launch
+    const int tmin = std::max(0, logn - EQ_TOP_LOG);
+    if (eq_top && tmin < (int)nz && (int)nz - tmin <= EQ_TOP_MAXL) {
+      EqTopConsts cs{};
+      for (int t = tmin; t < (int)nz; t++) {
+        const Fr z = fr_import(eq_z + 4 * t);
+        const Fr zp = from_mont(z), ap = from_mont(Fr::one() - z);
+        cs.z[t - tmin] = l9_of29(ml_plain_mul(zp, pow2_mod_plain<FrP>(261)));
+        cs.a[t - tmin] = l9_of29(ml_plain_mul(ap, pow2_mod_plain<FrP>(261)));
+      }
+      Fr* dst = (tmin & 1) == 0 ? G : H;
+      const size_t len = (size_t)1 << (logn - tmin);
+      hipLaunchKernelGGL(k_eqdft_top, dim3(div_up(len, 256)), dim3(256), 0, ctx->stream, cs,
+                         (uint32_t)(nz - tmin), twb, logn, tmin, dst);
+      QG_LAUNCH_CHECK();
+      t_hi = tmin - 1;
+    }
+    for (int t = t_hi; t >= 0; t--) {
       const Fr z = fr_import(eq_z + 4 * t);
       const Fr zp = from_mont(z), ap = from_mont(Fr::one() - z);
       const L9 z9 = l9_of29(ml_plain_mul(zp, pow2_mod_plain<FrP>(261)));
       const L9 a9 = l9_of29(ml_plain_mul(ap, pow2_mod_plain<FrP>(261)));
       Fr* dst = (t & 1) == 0 ? G : H;
-      const Fr* src = t == (int)nz - 1 ? nullptr : ((t & 1) == 0 ? H : G);
+      const Fr* src = t == (int)nz - 1 ? nullptr : ((t & 1) == 0 ? H : G);  // level t + 1
       const size_t len = (size_t)1 << (logn - t);
       hipLaunchKernelGGL(k_eqdft_level, dim3(div_up(len, 256)), dim3(256), 0, ctx->stream, src,
                          a9, z9, twb, logn, t, dst);

@@ -609,14 +609,19 @@ QG_DEV uint4 msm_entries4(const uint32_t* __restrict__ entries, uint32_t e, uint
 template <bool PF>
 __global__ void __launch_bounds__(MSM_BLOCK) __attribute__((amdgpu_waves_per_eu(PF ? 3 : 4)))
     k_msm_accumulate(const MsmPt* __restrict__ table, const uint32_t* __restrict__ entries,
-                     const uint32_t* __restrict__ bstart, uint32_t nb, uint32_t L,
+                     const uint32_t* __restrict__ bstart, uint32_t nb, uint32_t lgL,
                      X29Raw* __restrict__ partial, uint32_t* __restrict__ owner) {
   const uint32_t t = blockIdx.x * blockDim.x + threadIdx.x;
+  const uint32_t L = 1u << lgL;
   const uint32_t total = bstart[nb];
   const uint64_t e0w = (uint64_t)t * L;
   if (e0w >= total) return;
   const uint32_t e0 = (uint32_t)e0w;
   const uint32_t e1 = total - e0 < L ? total : e0 + L;
+  // the thread index is not kept live through the loop (it cost the
+  // non-prefetching form one VGPR spilled and reloaded per addition): a flush
+  // recovers it from the chunk end, t = (e1 - 1) >> lgL; chunks start at
+  // multiples of L (>= 4), so the group phase is e & 3
   // bucket of entry e0: the largest b with bstart[b] <= e0 (b < nb)
   uint32_t lo = 0, hi = nb;
   while (hi - lo > 1) {
@@ -634,21 +639,24 @@ __global__ void __launch_bounds__(MSM_BLOCK) __attribute__((amdgpu_waves_per_eu(
   uint4 g0 = msm_entries4(entries, e0, e1);
   uint4 g1 = e0 + 4 < e1 ? msm_entries4(entries, e0 + 4, e1) : g0;
   Q29 ax, ay;
-  bool pinf = msm_pt_load(table, g0.x & 0x7fffffffu, (g0.x >> 31) != 0u, ax, ay);
+#ifndef QG_MSM_ROWMASK
+#define QG_MSM_ROWMASK 0x7fffffffu  // experiment builds narrow the gathered span (timing only)
+#endif
+  bool pinf = msm_pt_load(table, g0.x & QG_MSM_ROWMASK, (g0.x >> 31) != 0u, ax, ay);
   for (uint32_t e = e0; e < e1; e++) {
-    const uint32_t k = (e - e0) & 3u;
+    const uint32_t k = e & 3u;
     Q29 bx = ax, by = ay;
     bool qinf = true;
     if (e + 1 < e1) {
       const uint32_t en = k == 0 ? g0.y : k == 1 ? g0.z : k == 2 ? g0.w : g1.x;
-      qinf = msm_pt_load(table, en & 0x7fffffffu, (en >> 31) != 0u, bx, by);
+      qinf = msm_pt_load(table, en & QG_MSM_ROWMASK, (en >> 31) != 0u, bx, by);
     }
     if (k == 3) {
       g0 = g1;
       if (e + 5 < e1) g1 = msm_entries4(entries, e + 5, e1);
     }
     if (e == next) {
-      msm_flush(partial, owner, t + b, b, acc, inf);
+      msm_flush(partial, owner, ((e1 - 1) >> lgL) + b, b, acc, inf);
       inf = true;
       do {
         b++;
@@ -670,7 +678,7 @@ __global__ void __launch_bounds__(MSM_BLOCK) __attribute__((amdgpu_waves_per_eu(
     ay = by;
     pinf = qinf;
   }
-  msm_flush(partial, owner, t + b, b, acc, inf);
+  msm_flush(partial, owner, ((e1 - 1) >> lgL) + b, b, acc, inf);
   return;
   }
   // entries arrive four at a time (one 16-B load per group of four, the next
@@ -679,12 +687,12 @@ __global__ void __launch_bounds__(MSM_BLOCK) __attribute__((amdgpu_waves_per_eu(
   // loads refetched a whole 128-B line per entry (as many bytes as the rows)
   uint4 cur = msm_entries4(entries, e0, e1), nxt = cur;
   for (uint32_t e = e0; e < e1; e++) {
-    const uint32_t k = (e - e0) & 3u;  // wave-uniform (same trip count per lane)
+    const uint32_t k = e & 3u;  // wave-uniform (chunks start at multiples of 4)
     if (k == 0 && e + 4 < e1) nxt = msm_entries4(entries, e + 4, e1);
     const uint32_t ent = k == 0 ? cur.x : k == 1 ? cur.y : k == 2 ? cur.z : cur.w;
     if (k == 3) cur = nxt;
     if (e == next) {  // bucket boundary (at most a few per thread)
-      msm_flush(partial, owner, t + b, b, acc, inf);
+      msm_flush(partial, owner, ((e1 - 1) >> lgL) + b, b, acc, inf);
       inf = true;
       do {
         b++;
@@ -704,7 +712,135 @@ __global__ void __launch_bounds__(MSM_BLOCK) __attribute__((amdgpu_waves_per_eu(
     }
     if (!x29_acc_madd_tp(acc, ax, ay)) x29_acc_madd_exc(acc, ax, ay, &inf);
   }
-  msm_flush(partial, owner, t + b, b, acc, inf);
+  msm_flush(partial, owner, ((e1 - 1) >> lgL) + b, b, acc, inf);
+}
+
+// Cooperative row gathers (COOP).  One 16-B load per lane of five per row
+// (msm_pt_load) puts 320 independent row requests on the memory path per wave
+// step; over a 27.9 GB table the chip then serves 1.6e10 random rows/s, about
+// what the accumulate consumes (micro/gather_bench.hip: 1.58e10 rows/s with
+// five 16-B loads per lane, 3.37e10 with eight lanes loading one 128-B row in
+// one coalesced request; the accumulate with its gathers confined to 2 GiB ran
+// 16.3 -> 14.9 ms, profiles/r05_gather_ab.txt).  Here each wave step gathers
+// the wave's 64 rows with eight LDS-DMA instructions (global_load_lds_dwordx4:
+// lane l of instruction k loads a 16-B word of the row of lane 8k + l/8, into a
+// per-wave 8 KiB LDS image), then every lane reads its own row's five words.
+// The next step's DMA is in flight during this step's addition.  Word w of
+// row m sits at position w ^ (m & 7) of the row's 128 B (the swizzle rides on
+// the DMA source address, the LDS image stays lane-linear): the readers of a
+// ds_read_b128 spread over 8 bank groups instead of 2.
+typedef __attribute__((address_space(3))) void* msm_lds_ptr;
+typedef __attribute__((address_space(1))) void* msm_glb_ptr;
+
+#if defined(__HIP_DEVICE_COMPILE__)
+// the eight DMA instructions of one wave step: lane l of instruction k loads
+// word (l & 7) ^ (l >> 3 & 7) of the row of lane 8k + (l >> 3) (entry `ent`,
+// row bits only; 0 for a lane without a next entry)
+__device__ __forceinline__ void msm_coop_issue(uint4* wbuf, const MsmPt* __restrict__ table,
+                                               uint32_t lane, uint32_t ent) {
+  const uint32_t pos = lane & 7u;
+  const uint32_t word = pos ^ ((lane >> 3) & 7u);
+  uint32_t r[8];
+#pragma unroll
+  for (int k = 0; k < 8; k++) r[k] = (uint32_t)__shfl((int)(ent & 0x7fffffffu), 8 * k + (int)(lane >> 3), 64);
+#pragma unroll
+  for (int k = 0; k < 8; k++) {
+    const uint4* g = reinterpret_cast<const uint4*>(table + r[k]) + word;
+    __builtin_amdgcn_global_load_lds((msm_glb_ptr)g, (msm_lds_ptr)(wbuf + 64 * k), 16, 0, 0);
+  }
+}
+
+// this lane's row from the wave image: x, y or p - y (neg), the infinity flag
+__device__ __forceinline__ bool msm_coop_read(const uint4* wbuf, uint32_t lane, bool neg, Q29& x,
+                                              Q29& y) {
+  const uint4* row = wbuf + 8 * lane;
+  const uint32_t sw = lane & 7u;
+  const uint32_t wy = neg ? 4u : 2u;
+  const uint4 x0 = row[0u ^ sw], x1 = row[1u ^ sw];
+  const uint4 y0 = row[wy ^ sw], y1 = row[(wy + 1u) ^ sw];
+  const uint4 top = row[6u ^ sw];
+  x.l[0] = x0.x; x.l[1] = x0.y; x.l[2] = x0.z; x.l[3] = x0.w;
+  x.l[4] = x1.x; x.l[5] = x1.y; x.l[6] = x1.z; x.l[7] = x1.w;
+  y.l[0] = y0.x; y.l[1] = y0.y; y.l[2] = y0.z; y.l[3] = y0.w;
+  y.l[4] = y1.x; y.l[5] = y1.y; y.l[6] = y1.z; y.l[7] = y1.w;
+  x.l[8] = top.x;
+  y.l[8] = neg ? top.z : top.y;
+  return (top.w & 1u) != 0u;
+}
+#endif
+
+#ifndef QG_COOP_WPE
+#define QG_COOP_WPE 3
+#endif
+__global__ void __launch_bounds__(MSM_BLOCK) __attribute__((amdgpu_waves_per_eu(QG_COOP_WPE)))
+    k_msm_accumulate_coop(const MsmPt* __restrict__ table, const uint32_t* __restrict__ entries,
+                          const uint32_t* __restrict__ bstart, uint32_t nb, uint32_t lgL,
+                          X29Raw* __restrict__ partial, uint32_t* __restrict__ owner) {
+#if defined(__HIP_DEVICE_COMPILE__)
+  __shared__ uint4 img[MSM_BLOCK / 64][64 * 8];
+  const uint32_t t = blockIdx.x * blockDim.x + threadIdx.x;
+  const uint32_t lane = threadIdx.x & 63u;
+  uint4* wbuf = img[threadIdx.x >> 6];
+  const uint32_t L = 1u << lgL;
+  const uint32_t total = bstart[nb];
+  const uint64_t e0w = (uint64_t)t * L;
+  // whole waves stay or leave together (the DMA steps are wave-wide); lanes
+  // past the end have an empty chunk and feed row 0 to the gathers
+  if (__builtin_amdgcn_readfirstlane((uint32_t)(e0w >= total))) return;
+  const uint32_t e0 = e0w < total ? (uint32_t)e0w : total;
+  const uint32_t e1 = total - e0 < L ? total : e0 + L;
+  uint32_t b = 0, next = 0;
+  if (e0 < e1) {
+    uint32_t lo = 0, hi = nb;
+    while (hi - lo > 1) {
+      const uint32_t mid = (lo + hi) >> 1;
+      if (bstart[mid] <= e0) lo = mid;
+      else hi = mid;
+    }
+    b = lo;
+    next = bstart[b + 1];
+  }
+  X29 acc;
+  bool inf = true;
+  uint4 g0 = msm_entries4(entries, e0, e1);
+  uint4 g1 = e0 + 4 < e1 ? msm_entries4(entries, e0 + 4, e1) : g0;
+  msm_coop_issue(wbuf, table, lane, e0 < e1 ? g0.x : 0u);
+  for (uint32_t i = 0; i < L; i++) {  // wave-uniform trip count
+    const uint32_t e = e0 + i;
+    const uint32_t k = i & 3u;
+    const uint32_t ent = k == 0 ? g0.x : k == 1 ? g0.y : k == 2 ? g0.z : g0.w;
+    const uint32_t en = k == 0 ? g0.y : k == 1 ? g0.z : k == 2 ? g0.w : g1.x;
+    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");  // this step's rows have landed
+    Q29 ax, ay;
+    const bool pinf = msm_coop_read(wbuf, lane, (ent >> 31) != 0u, ax, ay);
+    asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");  // read before the image is refilled
+    if (k == 3) {
+      g0 = g1;
+      if (e + 5 < e1) g1 = msm_entries4(entries, e + 5, e1);
+    }
+    if (i + 1 < L) msm_coop_issue(wbuf, table, lane, e + 1 < e1 ? en : 0u);
+    if (e >= e1) continue;
+    if (e == next) {
+      msm_flush(partial, owner, ((e1 - 1) >> lgL) + b, b, acc, inf);
+      inf = true;
+      do {
+        b++;
+        next = bstart[b + 1];
+      } while (next <= e);
+    }
+    if (pinf) continue;
+    if (inf) {
+      acc.X = ax;
+      acc.Y = ay;
+      acc.ZZ = Q29::from_l9(F29P<FqP>::ONE);
+      acc.ZZZ = acc.ZZ;
+      inf = false;
+      continue;
+    }
+    if (!x29_acc_madd_tp(acc, ax, ay)) x29_acc_madd_exc(acc, ax, ay, &inf);
+  }
+  if (e0 < e1) msm_flush(partial, owner, ((e1 - 1) >> lgL) + b, b, acc, inf);
+#endif
 }
 
 // first / last partial slot of bucket b (nonempty)
@@ -1238,7 +1374,8 @@ static MsmRun msm_accumulate_phase(qg_ctx* ctx, const qg_srs* srs, const Fr* d_s
       const int rounds = atoi(ov);
       QG_CHECK(rounds >= 1 && rounds <= 64, QG_ERR_INVALID, "QG_MSM_ROUNDS out of range");
       const size_t resident = (size_t)ctx->num_cus() * 16 * 64;
-      L = (uint32_t)((div_up(max_entries, resident * rounds) + 3) & ~(size_t)3);
+      L = 4;  // a power of two (k_msm_accumulate takes log2 L), rounded up
+      while ((size_t)L * resident * rounds < max_entries) L <<= 1;
     } else {
       int elog = max_entries >= ((size_t)1 << 27) ? 7 : 6;
       while (elog > 2 && (max_entries >> elog) < (size_t)ctx->num_cus() * 16 * 64 * 3) elog--;
@@ -1257,7 +1394,11 @@ static MsmRun msm_accumulate_phase(qg_ctx* ctx, const qg_srs* srs, const Fr* d_s
     // count + 1 (a bucket of c entries spans ceil(c / L) or one more slots);
     // skewed buckets beyond it are pre-summed by tree steps
     const uint32_t T = std::max<uint32_t>(4, (uint32_t)div_up(div_up(max_entries, nb), L) + 2);
-    QG_CHECK(L >= 1 && L <= 65536, QG_ERR_INVALID, "MSM chunk length out of range");
+    // k_msm_accumulate takes log2 L and the group phase of entry e as e & 3
+    QG_CHECK(L >= 4 && L <= 65536 && (L & (L - 1)) == 0, QG_ERR_INVALID,
+             "MSM chunk length out of range");
+    uint32_t lgL = 0;
+    while ((1u << lgL) < L) lgL++;
     const size_t max_threads = div_up(max_entries, L);
     const size_t nslots = max_threads + nb + 1;  // partial slot of (thread t, bucket b): t + b
     X29Raw* partial = ctx->scratch_as<X29Raw>("msm_partial" + sfx, nslots);
@@ -1348,17 +1489,26 @@ static MsmRun msm_accumulate_phase(qg_ctx* ctx, const qg_srs* srs, const Fr* d_s
     }
     {
       QgTimed tm(ctx, "msm_accumulate");
-      // the prefetching form for the largest MSMs only (2^27+ entries: 2^24
-      // scalars x 13 windows); QG_MSM_PF=0/1 forces it (A/B runs)
+      // the prefetching per-lane-gather form (QG_MSM_PF=1 with QG_MSM_COOP=0;
+      // the default for 2^27+ entries before the cooperative gathers)
       bool pf = max_entries >= ((size_t)1 << 27);
       if (const char* ov = getenv("QG_MSM_PF")) pf = atoi(ov) != 0;
-      if (pf)
+      // cooperative row gathers from 2^25 entries (2^22 scalars x 13 windows):
+      // 2^24 accumulate 16.4-16.6 -> 15.3 ms, 2^22 -4 %, 2^20 neutral
+      // (profiles/r05_msm_coop_ab.txt); QG_MSM_COOP=0/1 forces it (A/B runs)
+      bool coop = max_entries >= ((size_t)1 << 25);
+      if (const char* ov = getenv("QG_MSM_COOP")) coop = atoi(ov) != 0;
+      if (coop)
+        hipLaunchKernelGGL(k_msm_accumulate_coop, dim3(div_up(max_threads, MSM_BLOCK)),
+                           dim3(MSM_BLOCK), 0, ctx->stream, srs->d_table, entries, bstart, nb, lgL,
+                           partial, owner);
+      else if (pf)
         hipLaunchKernelGGL(k_msm_accumulate<true>, dim3(div_up(max_threads, MSM_BLOCK)),
-                           dim3(MSM_BLOCK), 0, ctx->stream, srs->d_table, entries, bstart, nb, L,
+                           dim3(MSM_BLOCK), 0, ctx->stream, srs->d_table, entries, bstart, nb, lgL,
                            partial, owner);
       else
         hipLaunchKernelGGL(k_msm_accumulate<false>, dim3(div_up(max_threads, MSM_BLOCK)),
-                           dim3(MSM_BLOCK), 0, ctx->stream, srs->d_table, entries, bstart, nb, L,
+                           dim3(MSM_BLOCK), 0, ctx->stream, srs->d_table, entries, bstart, nb, lgL,
                            partial, owner);
       QG_LAUNCH_CHECK();
     }

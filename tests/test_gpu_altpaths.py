@@ -132,11 +132,15 @@ def test_replicated_s_matches_split(world):
 
 @pytest.mark.parametrize("n,small", [((1 << 11) + 3, False), (5000, False), (5000, True),
                                      (1, False), (7, True), ((1 << 16) + 1, False)])
-def test_prefetch_accumulate_matches_default(n, small):
-    """k_msm_accumulate<true> (the prefetching loop the 2^24 headline takes) on
-    short and odd MSMs: chunks shorter than the prefetch distance,
-    bucket boundaries at a chunk's first entry (small scalars: few, crowded
-    buckets), a partial last group.  Bit-exact against the default loop and
+@pytest.mark.parametrize("mode", ["QG_MSM_PF", "QG_MSM_COOP"])
+def test_alternate_accumulate_matches_default(n, small, mode):
+    """The accumulate loops the large MSMs take, forced onto short and odd MSMs
+    (ADVICE r4): k_msm_accumulate<true> (prefetching per-lane gathers) and
+    k_msm_accumulate_coop (wave-cooperative LDS-DMA gathers, the 2^24 headline's
+    loop: whole waves step together, lanes past the last entry feed row 0).
+    Chunks shorter than the prefetch distance, bucket boundaries at a chunk's
+    first entry (small scalars: few, crowded buckets), a partial last group and
+    a partial last wave.  Bit-exact against the default loop of that size and
     against the trapdoor identity commit = [p(tau)] g."""
     import quill_amd as q
     rnd = random.Random(n * 7 + small)
@@ -145,9 +149,9 @@ def test_prefetch_accumulate_matches_default(n, small):
     d = q.Device(0)
     srs = q.Srs.generate(d, tau, n)
     out = {}
-    for pf in ("0", "1"):
-        with env("QG_MSM_PF", pf):
-            out[pf] = srs.msm(scal)
+    for on in ("0", "1"):
+        with env(mode, on), env("QG_MSM_COOP" if mode == "QG_MSM_PF" else "QG_MSM_PF", "0"):
+            out[on] = srs.msm(scal)
     srs.close()
     d.close()
     assert out["0"] == out["1"]
