@@ -126,6 +126,32 @@ def sumcheck_prod(nvars, tables, claimed, state: bytes, variant="eval", nthreads
     return r_polys, point, _unmont(ev[:], R_MOD), bytes(st)
 
 
+def sumcheck_prod_mont(nvars, mont_tables, claimed, state: bytes, variant="mt", nthreads=4):
+    """sumcheck_prod on tables given as (2^nvars, 4) uint64 numpy arrays of
+    Montgomery limbs (arkworks' in-memory Fr, as DeviceVec.to_numpy returns):
+    no per-entry Python conversion, for the 2^20-variable parity test"""
+    import numpy as np
+    k = len(mont_tables)
+    N = 1 << nvars
+    flat = np.ascontiguousarray(np.concatenate([np.asarray(t, dtype=np.uint64).reshape(N, 4)
+                                                for t in mont_tables]))
+    t = flat.ctypes.data_as(C.POINTER(C.c_uint64))
+    st = (C.c_uint8 * 32).from_buffer_copy(state)
+    co = (C.c_uint64 * (4 * nvars * (k + 1)))()
+    lens = (C.c_uint32 * nvars)()
+    pt = (C.c_uint64 * (4 * nvars))()
+    ev = (C.c_uint64 * 4)()
+    cl = (C.c_uint64 * 4)(*_mont(claimed, R_MOD))
+    if variant == "mt":
+        lib().oc_sumcheck_prod_mt(nvars, k, t, cl, st, co, lens, pt, ev, nthreads)
+    else:
+        lib().oc_sumcheck_prod(nvars, k, t, cl, st, co, lens, pt, ev)
+    r_polys = [[_unmont(co[4 * (j * (k + 1) + i):4 * (j * (k + 1) + i) + 4], R_MOD)
+                for i in range(lens[j])] for j in range(nvars)]
+    point = [_unmont(pt[4 * j:4 * j + 4], R_MOD) for j in range(nvars)]
+    return r_polys, point, _unmont(ev[:], R_MOD), bytes(st)
+
+
 def cpu_model():
     try:
         with open("/proc/cpuinfo") as f:

@@ -160,3 +160,25 @@ def test_sumcheck_2p18_matches_round_kernel_path(dev):
         v.close()
     orp, opt, oev, ost = oc.sumcheck_prod(nv, lists, claimed, o.Transcript(b"sumcheck_bench").state)
     assert r_polys == orp and point == opt and ev == oev and t.state == ost
+
+
+def test_sumcheck_2p20_bitexact_vs_c_oracle(dev):
+    """The headline size itself (config 3: 2^20 variables, h = g1 g2 g3): the
+    device proof (four big rounds + the slice tail) equals the evaluation-form
+    C restatement of sumcheck.rs:28-114 round message by round message, point,
+    final evaluation and transcript state — not only a verifier replay."""
+    from quill_amd import DeviceVec, Transcript, VirtualPolyExpr as E
+    from quill_amd.hyperplonk import _unpack_dev, sumcheck_prove_device
+    nv = 20
+    vecs = [DeviceVec(dev, 1 << nv).fill_random(0x5C20 + i) for i in range(3)]
+    mont = [v.to_numpy() for v in vecs]
+    claimed = random.Random(20).randrange(R)
+    expr = E.Input(0) * E.Input(1) * E.Input(2)
+    t = Transcript(b"sumcheck_bench")
+    r_polys, point, ev = _unpack_dev(nv, expr,
+                                     *sumcheck_prove_device(dev, nv, vecs, expr, claimed, t))
+    for v in vecs:
+        v.close()
+    orp, opt, oev, ost = oc.sumcheck_prod_mont(nv, mont, claimed,
+                                               o.Transcript(b"sumcheck_bench").state)
+    assert r_polys == orp and point == opt and ev == oev and t.state == ost

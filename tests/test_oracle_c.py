@@ -154,3 +154,16 @@ def test_c_hyperplonk_matches_oracle(rows):
                 (y.evaluation, y.s_comm, y.poly_opening, y.s_opening_inv)
     # the backend is restored
     assert o.KZG.commit is not hc._commit
+
+
+def test_c_sumcheck_mont_entry_matches_list_entry():
+    """sumcheck_prod_mont (numpy Montgomery limbs in, the 2^20 GPU parity
+    test's checker) = sumcheck_prod (Python ints in)"""
+    rnd = random.Random(31)
+    nv = 7
+    tabs = [[rnd.randrange(o.R_MOD) for _ in range(1 << nv)] for _ in range(3)]
+    st = o.Transcript(b"mont-entry").state
+    a = oc.sumcheck_prod(nv, tabs, 1234, st)
+    for variant in ("mt", "eval"):
+        b = oc.sumcheck_prod_mont(nv, [_to_limbs(t) for t in tabs], 1234, st, variant=variant)
+        assert a == b
