@@ -35,10 +35,18 @@ def test_msm_2p24_trapdoor(dev):
     m = (1 << 23) + 12345
     got_p = srs.msm_dev(v, m)
     want_p = oc.g1_mul(o.G1_GEN, oc.fr_horner(v.to_numpy(m), TAU))
+    # short prefixes on the long SRS's c = 20 tables (few entries per bucket,
+    # 16-entry chunks; a single base)
+    assert srs.window_info() == (20, 13)
+    short = {}
+    for k in (1, 4097, (1 << 20) - 7, (1 << 20) + 1):
+        short[k] = (srs.msm_dev(v, k), oc.g1_mul(o.G1_GEN, oc.fr_horner(v.to_numpy(k), TAU)))
     v.close()
     srs.close()
     assert got == want
     assert got_p == want_p
+    for k, (g, w) in short.items():
+        assert g == w, k
 
 
 def test_sumcheck_2p20_degree3(dev):
