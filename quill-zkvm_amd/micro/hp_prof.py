@@ -38,6 +38,20 @@ def main():
             q.DeviceVec.from_canonical(dev, col, out=buf, offset=i * rows)
         wits.append(TraceWitness.from_full(buf, c.num_cols()))
     hp.prove(pcs, wits)
+    if os.environ.get("HP_PROF_CPROFILE") == "1":  # host-side profile of the timed proofs
+        import cProfile
+        import pstats
+        pr = cProfile.Profile()
+        t0 = time.perf_counter()
+        pr.enable()
+        for _ in range(steps):
+            hp.prove(pcs, wits)
+        pr.disable()
+        print(f"2^{k}: {(time.perf_counter() - t0) / steps * 1e3:.1f} ms/proof under cProfile")
+        st = pstats.Stats(pr)
+        st.sort_stats("tottime").print_stats(35)
+        st.sort_stats("cumtime").print_stats(35)
+        return
     dev.enable_timing(True)
     t0 = time.perf_counter()
     for _ in range(steps):

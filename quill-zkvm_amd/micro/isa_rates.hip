@@ -53,6 +53,18 @@ __global__ void __launch_bounds__(256) k_rate(uint64_t* out, uint32_t seed) {
         asm volatile("v_fma_f32 %0, %0, %1, %2" : "+v"(a32[c]) : "v"(x), "v"(y));
       } else if constexpr (OP == 12) {
         asm volatile("v_add3_u32 %0, %0, %1, %2" : "+v"(a32[c]) : "v"(x), "v"(y));
+      } else if constexpr (OP == 13) {
+        asm volatile("v_lshrrev_b64 %0, 29, %0" : "+v"(a64[c]));
+      } else if constexpr (OP == 14) {
+        asm volatile("v_and_b32 %0, %1, %0" : "+v"(a32[c]) : "v"(x));
+      } else if constexpr (OP == 15) {
+        asm volatile("v_alignbit_b32 %0, %1, %0, 29" : "+v"(a32[c]) : "v"(x));
+      } else if constexpr (OP == 16) {
+        asm volatile("v_mov_b32 %0, %1" : "=v"(a32[c]) : "v"(a32[(c + 1) % CHAINS]));
+      } else if constexpr (OP == 17) {
+        asm volatile("v_sub_u32 %0, %1, %0" : "+v"(a32[c]) : "v"(x));
+      } else if constexpr (OP == 18) {
+        asm volatile("v_cndmask_b32 %0, %0, %1, vcc" : "+v"(a32[c]) : "v"(x) : "vcc");
       }
     }
   }
@@ -66,7 +78,9 @@ static const char* NAMES[] = {"v_mad_u64_u32",  "v_add_co_u32",   "v_mul_lo_u32"
                               "v_mul_hi_u32",   "v_fma_f64",      "v_mad_u32_u24",
                               "v_mul_hi_u32_u24", "add_co+addc(2)", "v_lshl_add_u64",
                               "v_mul_f64",      "v_add_f64",      "v_fma_f32",
-                              "v_add3_u32"};
+                              "v_add3_u32",     "v_lshrrev_b64",  "v_and_b32",
+                              "v_alignbit_b32", "v_mov_b32",      "v_sub_u32",
+                              "v_cndmask_b32"};
 
 template <int OP>
 static void run(uint64_t* d, int blocks) {
@@ -104,6 +118,12 @@ int main() {
   run<10>(d, blocks);
   run<11>(d, blocks);
   run<12>(d, blocks);
+  run<13>(d, blocks);
+  run<14>(d, blocks);
+  run<15>(d, blocks);
+  run<16>(d, blocks);
+  run<17>(d, blocks);
+  run<18>(d, blocks);
   hipFree(d);
   return 0;
 }
