@@ -70,6 +70,21 @@ __global__ void __launch_bounds__(ML_BLOCK)
   if (threadIdx.x == 0) *out = acc;
 }
 
+// <f, g> into device memory (no host round trip)
+static void dot_to_device(qg_ctx* ctx, const Fr* f, const Fr* g, size_t n, Fr* d_out) {
+  if (n == 0) {
+    QG_HIP(hipMemsetAsync(d_out, 0, sizeof(Fr), ctx->stream));
+    return;
+  }
+  QgTimed tm(ctx, "inner_product");
+  unsigned blocks = (unsigned)std::min<size_t>(2048, div_up(n, ML_BLOCK));
+  Fr* part = ctx->scratch_as<Fr>("dot_part", blocks);
+  hipLaunchKernelGGL(k_dot, dim3(blocks), dim3(ML_BLOCK), 0, ctx->stream, f, g, n, part);
+  QG_LAUNCH_CHECK();
+  hipLaunchKernelGGL(k_sum, dim3(1), dim3(ML_BLOCK), 0, ctx->stream, part, (size_t)blocks, d_out);
+  QG_LAUNCH_CHECK();
+}
+
 static Fr dot_device(qg_ctx* ctx, const Fr* f, const Fr* g, size_t n) {
   if (n == 0) return Fr::zero();
   QgTimed tm(ctx, "inner_product");
@@ -801,10 +816,9 @@ __global__ void __launch_bounds__(256)
 
 // trimmed length of a device vector: the last 16K entries first (8 blocks),
 // then the rest, skipped when the tail held a nonzero
-static size_t trimmed_len(qg_ctx* ctx, const Fr* a, size_t n) {
-  if (n == 0) return 0;
-  unsigned long long* d = ctx->scratch_as<unsigned long long>("trim_len", 1);
+static void trim_launch(qg_ctx* ctx, const Fr* a, size_t n, unsigned long long* d) {
   QG_HIP(hipMemsetAsync(d, 0, sizeof(unsigned long long), ctx->stream));
+  if (n == 0) return;
   constexpr size_t TAIL = 16384;
   const size_t body = n > TAIL ? n - TAIL : 0;
   hipLaunchKernelGGL(k_last_nonzero, dim3((unsigned)std::min<size_t>(8, div_up(n - body, 256))),
@@ -816,6 +830,12 @@ static size_t trimmed_len(qg_ctx* ctx, const Fr* a, size_t n) {
                        body, 1, d);
     QG_LAUNCH_CHECK();
   }
+}
+
+static size_t trimmed_len(qg_ctx* ctx, const Fr* a, size_t n) {
+  if (n == 0) return 0;
+  unsigned long long* d = ctx->scratch_as<unsigned long long>("trim_len", 1);
+  trim_launch(ctx, a, n, d);
   unsigned long long h = 0;
   QG_HIP(hipMemcpyAsync(&h, d, sizeof(h), hipMemcpyDeviceToHost, ctx->stream));
   ctx->sync();
@@ -823,18 +843,13 @@ static size_t trimmed_len(qg_ctx* ctx, const Fr* a, size_t n) {
 }
 
 // four KZG::open quotients at once (the ML opening's poly and S at r and
-// 1/r): one trimmed length per distinct polynomial, one batched suffix-Horner
-// recursion, one transfer of the four values y = s_0
+// 1/r) on their trimmed lengths `Lt` (the caller's), one batched
+// suffix-Horner recursion, and the four values y = s_0 queued into pinned
+// memory (h_y[4]) without a round trip: the caller reads them after its next
+// synchronization (the quotient MSMs')
 static void kzg_quotients_batch(qg_ctx* ctx, const qg_srs* srs, const Fr* const polys[4],
-                                const size_t lens[4], const Fr xs[4], qg_kzg_opening* const outs[4],
-                                std::vector<const Fr*>& qs, std::vector<size_t>& qns) {
-  size_t Lt[4];
-  for (int i = 0; i < 4; i++) {
-    int same = -1;
-    for (int k = 0; k < i; k++)
-      if (polys[k] == polys[i] && lens[k] == lens[i]) same = k;
-    Lt[i] = same >= 0 ? Lt[same] : trimmed_len(ctx, polys[i], lens[i]);
-  }
+                                const size_t Lt[4], const Fr xs[4], qg_kzg_opening* const outs[4],
+                                std::vector<const Fr*>& qs, std::vector<size_t>& qns, Fr* h_y) {
   std::vector<ShIn> jobs;
   Fr* s[4] = {nullptr, nullptr, nullptr, nullptr};
   for (int i = 0; i < 4; i++) {
@@ -849,16 +864,14 @@ static void kzg_quotients_batch(qg_ctx* ctx, const qg_srs* srs, const Fr* const 
     suffix_horner_batch(ctx, jobs);
   }
   Fr* d_y = ctx->scratch_as<Fr>("open_y", 4);
+  QG_HIP(hipMemsetAsync(d_y, 0, 4 * sizeof(Fr), ctx->stream));
   for (int i = 0; i < 4; i++)
     if (s[i])
       QG_HIP(hipMemcpyAsync(d_y + i, s[i], sizeof(Fr), hipMemcpyDeviceToDevice, ctx->stream));
-  Fr y[4];
-  QG_HIP(hipMemcpyAsync(y, d_y, sizeof(y), hipMemcpyDeviceToHost, ctx->stream));
-  ctx->sync();
+  QG_HIP(hipMemcpyAsync(h_y, d_y, 4 * sizeof(Fr), hipMemcpyDeviceToHost, ctx->stream));
   qs.clear();
   qns.clear();
   for (int i = 0; i < 4; i++) {
-    fr_export(s[i] ? y[i] : Fr::zero(), outs[i]->y);
     qs.push_back(s[i] ? s[i] + 1 : nullptr);
     qns.push_back(s[i] ? Lt[i] - 1 : 0);
   }
@@ -1262,30 +1275,71 @@ static void mle_open_sharded(qg_ctx* ctx, const qg_srs* srs, const Fr* dpoly, si
   kzg_open_sharded(ctx, srs, Sl, L, Slen, r_inv, &out->s_opening_inv);
 }
 
-// MLEvalProof::prove (mlpcs.rs:83-124) on a device-resident evaluation vector
+// MLEvalProof::prove (mlpcs.rs:83-124) on a device-resident evaluation vector.
+// Two host round trips per opening, both for values the transcript or the
+// caller needs: the S commitment and the four quotient commitments.  The
+// inner product, the trimmed lengths (DensePolynomial trims, kzg.rs / ipa.rs)
+// and the values y are queued into pinned memory and read after those
+// synchronizations; the trimmed length of the opened vector is reused while
+// the caller guarantees it unchanged (QG_OPEN_UNCHANGED contract, same
+// allocation id and offset).
 static void mle_open_device(qg_ctx* ctx, const qg_srs* srs, const Fr* dpoly, size_t n,
                             const uint64_t* point, size_t nvars, uint8_t state[32],
                             qg_mle_proof* out, bool unchanged = false, uint64_t poly_id = 0,
                             size_t poly_off = 0) {
   if (ctx->sharded) return mle_open_sharded(ctx, srs, dpoly, n, point, nvars, state, out);
   const size_t N = (size_t)1 << nvars;
+  unsigned long long* h_len =
+      reinterpret_cast<unsigned long long*>(ctx->pinned_get("mle_len_h", 2 * sizeof(unsigned long long)));
+  unsigned long long* d_len = ctx->scratch_as<unsigned long long>("mle_len", 2);
+  // trimmed length of the opened vector: queued first (or remembered)
+  const std::string lt_key = poly_id ? std::to_string(poly_id) + "+" + std::to_string(poly_off) +
+                                           ":" + std::to_string(n) + "="
+                                     : std::string();
+  std::string& lt_memo = ctx->arena.memo["mle_poly_len"];
+  const bool lt_known = unchanged && poly_id && lt_memo.compare(0, lt_key.size(), lt_key) == 0;
+  if (!lt_known) {
+    trim_launch(ctx, dpoly, n, d_len);
+    QG_HIP(hipMemcpyAsync(h_len, d_len, sizeof(unsigned long long), hipMemcpyDeviceToHost,
+                          ctx->stream));
+  }
   Fr* dz = ctx->scratch_as<Fr>("mle_z", nvars ? nvars : 1);
   Fr* dpr = ctx->scratch_as<Fr>("mle_pr", N);
   fr_upload(ctx, dz, point, nvars);
   // P_r coefficients = eq table (mlpcs.rs:68-78)
   eq_table_device(ctx, dz, (uint32_t)nvars, dpr);
   // evaluation = <poly, P_r> over the common prefix (mlpcs.rs:91-94)
-  Fr evaluation = dot_device(ctx, dpoly, dpr, n < N ? n : N);
-  // S polynomial and its commitment (mlpcs.rs:95-97)
+  Fr* d_eval = ctx->scratch_as<Fr>("mle_eval", 1);
+  Fr* h_eval = reinterpret_cast<Fr*>(ctx->pinned_get("mle_eval_h", sizeof(Fr)));
+  dot_to_device(ctx, dpoly, dpr, n < N ? n : N, d_eval);
+  QG_HIP(hipMemcpyAsync(h_eval, d_eval, sizeof(Fr), hipMemcpyDeviceToHost, ctx->stream));
+  // S polynomial (mlpcs.rs:95-97) and its trimmed length
   const size_t M = n > N ? n : N;
-  Fr* dS = ctx->scratch_as<Fr>("mle_S", M > 1 ? M - 1 : 1);
-  size_t Slen = 0;
-  if (M > 1) {
-    s_poly_device(ctx, dpoly, n, dpr, N, dS, point, nvars, unchanged, poly_id, poly_off);
-    Slen = trimmed_len(ctx, dS, M - 1);
+  const size_t Sn = M > 1 ? M - 1 : 0;
+  Fr* dS = ctx->scratch_as<Fr>("mle_S", Sn ? Sn : 1);
+  if (Sn) s_poly_device(ctx, dpoly, n, dpr, N, dS, point, nvars, unchanged, poly_id, poly_off);
+  trim_launch(ctx, dS, Sn, d_len + 1);
+  QG_HIP(hipMemcpyAsync(h_len + 1, d_len + 1, sizeof(unsigned long long), hipMemcpyDeviceToHost,
+                        ctx->stream));
+  // its commitment: over all Sn coefficients when they fit the SRS (trailing
+  // zeros add nothing), else the trimmed length first (the degree check)
+  size_t s_msm = Sn;
+  if (Sn > srs->n) {
+    ctx->sync();
+    s_msm = (size_t)h_len[1];
+    QG_CHECK(s_msm <= srs->n, QG_ERR_INVALID, "Polynomial degree exceeds max degree");
   }
-  QG_CHECK(Slen <= srs->n, QG_ERR_INVALID, "Polynomial degree exceeds max degree");
-  G1Affine s_comm = msm_device(ctx, srs, dS, Slen);
+  G1Affine s_comm = msm_device(ctx, srs, dS, s_msm);
+  ctx->sync();  // (drained already unless the MSM was empty)
+  const Fr evaluation = *h_eval;
+  const size_t Slen = (size_t)h_len[1];
+  size_t Lt = 0;
+  if (lt_known) {
+    Lt = (size_t)std::stoull(lt_memo.substr(lt_key.size()));
+  } else {
+    Lt = (size_t)h_len[0];
+    lt_memo = poly_id ? lt_key + std::to_string(Lt) : std::string();
+  }
   // transcript: point (Vec<Fr>), evaluation, s_comm; draw r (mlpcs.rs:100-107)
   std::vector<uint8_t> msg(8 + 32 * nvars);
   u64_to_bytes(nvars, msg.data());
@@ -1306,13 +1360,18 @@ static void mle_open_device(qg_ctx* ctx, const qg_srs* srs, const Fr* dpoly, siz
   qg_kzg_opening* outs[4] = {&out->poly_opening, &out->poly_opening_inv, &out->s_opening,
                              &out->s_opening_inv};
   const Fr* polys[4] = {dpoly, dpoly, dS, dS};
-  const size_t lens[4] = {n, n, Slen, Slen};
+  const size_t lts[4] = {Lt, Lt, Slen, Slen};
   const Fr xs[4] = {r, r_inv, r, r_inv};
   std::vector<const Fr*> qs;
   std::vector<size_t> qns;
-  kzg_quotients_batch(ctx, srs, polys, lens, xs, outs, qs, qns);
+  Fr* h_y = reinterpret_cast<Fr*>(ctx->pinned_get("open_y_h", 4 * sizeof(Fr)));
+  kzg_quotients_batch(ctx, srs, polys, lts, xs, outs, qs, qns, h_y);
   const std::vector<G1Affine> pis = msm_device_batch(ctx, srs, qs, qns);
-  for (int i = 0; i < 4; i++) g1_export(pis[i], outs[i]->proof_xy, &outs[i]->proof_inf);
+  ctx->sync();  // (drained already unless every quotient was empty)
+  for (int i = 0; i < 4; i++) {
+    fr_export(h_y[i], outs[i]->y);
+    g1_export(pis[i], outs[i]->proof_xy, &outs[i]->proof_inf);
+  }
 }
 
 }  // namespace qg
