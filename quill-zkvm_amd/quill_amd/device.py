@@ -2,11 +2,14 @@
 from __future__ import annotations
 
 import ctypes as C
+import os
 
 import numpy as np
 
 from ._lib import check, lib
 from .field import fr_array, fr_c, fr_list, g1_from_abi, g1_to_abi, u64p
+
+_NO_POOL = os.environ.get("QG_NO_POOL") == "1"  # A/B runs: every buffer freed on close
 
 
 class Device:
@@ -17,9 +20,17 @@ class Device:
         check(lib().qg_ctx_create(device, C.byref(self.h)))
         self.device = device
         self.rank, self.world = 0, 1
+        # freed pooled buffers by length (DeviceVec(..., pooled=True)): a prover's
+        # per-proof temporaries are reused instead of hipFree'd, which waits for
+        # the device to drain and then costs ~0.2 ms of host time each
+        self._pool = {}
 
     def close(self):
         if self.h:
+            for hs in self._pool.values():
+                for h in hs:
+                    lib().qg_buf_destroy(h)
+            self._pool = {}
             lib().qg_ctx_destroy(self.h)
             self.h = C.c_void_p()
 
@@ -123,7 +134,7 @@ class Device:
         """fast_eq_eval_hypercube (eq_eval.rs:6-31) into a device vector"""
         n = len(point)
         pt = fr_array(point) if n else np.zeros((1, 4), dtype=np.uint64)
-        out = out if out is not None else DeviceVec(self, (1 << n) // self.world)
+        out = out if out is not None else DeviceVec(self, (1 << n) // self.world, pooled=True)
         check(lib().qg_eq_table_dev(self.h, u64p(pt), n, out.h), self.h)
         return out
 
@@ -152,18 +163,25 @@ class Device:
 class DeviceVec:
     """Fr vector resident in HBM (qg_buf)."""
 
-    def __init__(self, dev: Device, n: int):
+    def __init__(self, dev: Device, n: int, pooled: bool = False):
+        """pooled: the buffer comes from / returns to the device's pool of freed
+        buffers of this length (contents undefined, like a fresh allocation)"""
         self.dev = dev
         self.n = n
         self.base = None  # the owning buffer when this is a view
-        self.h = C.c_void_p()
-        check(lib().qg_buf_create(dev.h, n, C.byref(self.h)), dev.h)
+        self.pooled = pooled and not _NO_POOL
+        free = dev._pool.get(n) if self.pooled else None
+        if free:
+            self.h = free.pop()
+        else:
+            self.h = C.c_void_p()
+            check(lib().qg_buf_create(dev.h, n, C.byref(self.h)), dev.h)
 
     def view(self, offset: int, n: int) -> "DeviceVec":
         """Entries [offset, offset+n) without a copy (qg_buf_view); keeps this
         buffer alive."""
         v = DeviceVec.__new__(DeviceVec)
-        v.dev, v.n, v.base = self.dev, n, self
+        v.dev, v.n, v.base, v.pooled = self.dev, n, self, False
         v.h = C.c_void_p()
         check(lib().qg_buf_view(self.h, offset, n, C.byref(v.h)), self.dev.h)
         return v
@@ -228,7 +246,10 @@ class DeviceVec:
 
     def close(self):
         if self.h:
-            lib().qg_buf_destroy(self.h)
+            if getattr(self, "pooled", False) and self.dev.h:
+                self.dev._pool.setdefault(self.n, []).append(self.h)
+            else:
+                lib().qg_buf_destroy(self.h)
             self.h = C.c_void_p()
 
     def __del__(self):

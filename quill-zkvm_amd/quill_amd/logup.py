@@ -41,7 +41,7 @@ def logup_column(store: VirtualPolynomialStore, h, beta: int, m=None, dev: Devic
     QuillGpuError(QG_ERR_ASSERT) on a zero denominator, where the reference
     panics in inverse().unwrap()."""
     if store.on_device:
-        out = DeviceVec(store.dev, store.local_len)
+        out = DeviceVec(store.dev, store.local_len, pooled=True)
         s = logup_column_device(store.dev, store.num_vars, store.polynomials,
                                 store.virtual_polys[h], beta, out,
                                 store.virtual_polys[m] if m is not None else None)
