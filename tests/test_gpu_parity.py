@@ -451,6 +451,47 @@ def test_mle_open_unchanged_reuses_transform(dev):
     assert kzg.open_dev(a, len(a), pts[1], t1) == kzg.open(a.to_list(), pts[1], t2)
 
 
+@pytest.mark.parametrize("n,nv,live", [(64, 6, 40), (64, 6, 0), (100, 5, 50), (64, 6, 1)])
+def test_mle_open_zero_tail_matches_oracle(dev, n, nv, live):
+    """Vectors whose trailing entries are zero (only the first `live` nonzero;
+    live = 0: the zero polynomial): the ML opening commits S over all its
+    coefficients and runs the quotients on the trimmed lengths read back after
+    the commitment's synchronization (mlpcs.hip mle_open_device), and every
+    field of the proof and the transcript state equal the oracle prover's
+    (DensePolynomial trims, kzg.rs:75-96).  The same buffer is then opened
+    again with QG_OPEN_UNCHANGED (the trimmed length remembered), and after
+    its tail changes, without the flag (the length recomputed)."""
+    from quill_amd import KZG, DeviceVec, Transcript
+    rnd = random.Random(7000 + 10 * n + live)
+    tau = rnd.randrange(R)
+    kzg = KZG.trusted_setup(max(n, 1 << nv), tau, dev)
+    okzg = o.KZG(max(n, 1 << nv), tau, points=[])
+
+    def check(poly, vec, point, unchanged):
+        t = Transcript(b"zero tail")
+        proof = kzg.open_dev(vec, n, point, t, unchanged=unchanged)
+        ot = o.Transcript(b"zero tail")
+        ref = o.MLEvalProof.prove(poly, point, okzg, ot)
+        assert proof.evaluation == ref.evaluation and proof.s_comm == ref.s_comm
+        for k in ("poly_opening", "poly_opening_inv", "s_opening", "s_opening_inv"):
+            op = getattr(proof, k)
+            assert (op.x, op.y, op.proof) == tuple(getattr(ref, k)), k
+        assert t.state == ot.state
+
+    poly = [rnd.randrange(R) for _ in range(live)] + [0] * (n - live)
+    vec = DeviceVec.from_list(dev, poly)
+    pts = [[rnd.randrange(R) for _ in range(nv)] for _ in range(3)]
+    check(poly, vec, pts[0], False)
+    check(poly, vec, pts[1], True)
+    poly2 = poly[:]
+    poly2[n - 1] = rnd.randrange(1, R)  # the tail now ends in a nonzero entry
+    vec2 = DeviceVec.from_list(dev, poly2)
+    vec.copy_from(vec2)
+    check(poly2, vec, pts[2], False)
+    vec.close()
+    vec2.close()
+
+
 def test_microbench_entry_points(dev):
     """qg_microbench_fq_mul / qg_microbench_fetch (the bench's compute peak and
     the PMC probe's FETCH_SIZE calibration) run and report positive rates"""
