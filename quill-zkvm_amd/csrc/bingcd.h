@@ -184,4 +184,16 @@ QG_HD Fp<C> inv_bingcd(const Fp<C>& y) {
   return r;
 }
 
+// Host finv (field.h): y = aR is inverted as a plain integer, z = (aR)^-1, and
+// one Montgomery product by R^3 mod P gives a^-1 R.  One more product checks
+// it (the iteration bound has little slack); Fermat if it ever did not converge.
+template <class C>
+inline Fp<C> finv_host(const Fp<C>& a) {
+  if (a.is_zero()) return a;
+  static const Fp<C> r3 = Fp<C>::from_raw(C::R2) * Fp<C>::from_raw(C::R2);  // R^3 mod P
+  const Fp<C> r = inv_bingcd<C>(a) * r3;
+  if (r * a == Fp<C>::one()) return r;
+  return finv_fermat(a);
+}
+
 }  // namespace qg
