@@ -669,14 +669,17 @@ def bench_mle(q, dev, args, barrier_sync, max_over_ranks, rank=0, world=1):
     names = ("eq_table", "inner_product", "s_polynomial", "kzg_division", "msm_bucketing",
              "msm_accumulate", "msm_reduce")
     steps = max(1, min(args.steps, 3))
-    dev.enable_timing(True)
+    # timed steps without the library's phase-timing events; one more step
+    # with them gives the phase split
     barrier_sync()
     t0 = time.perf_counter()
     for _ in range(steps):
         step()
     barrier_sync()
     dt = max_over_ranks(time.perf_counter() - t0)
-    parts = {nm: dev.kernel_time(nm)[0] / steps for nm in names}
+    dev.enable_timing(True)
+    step()
+    parts = {nm: dev.kernel_time(nm)[0] for nm in names}
     dev.enable_timing(False)
     poly.close()
     kzg.srs.close()
@@ -707,13 +710,17 @@ def bench_logup(q, dev, args, barrier_sync, max_over_ranks, rank=0, world=1, tra
     m = E.Input(2)
     for _ in range(max(1, args.warmup)):
         logup_column_device(dev, k + lw, tabs, h, LOGUP_BETA, out, m)
-    dev.enable_timing(True)
+    # wall time without the library's kernel-timing events, then the same
+    # calls with them for the kernel time
     barrier_sync()
     t0 = time.perf_counter()
     for _ in range(args.steps):
         s = logup_column_device(dev, k + lw, tabs, h, LOGUP_BETA, out, m)
     barrier_sync()
     dt = max_over_ranks(time.perf_counter() - t0)
+    dev.enable_timing(True)
+    for _ in range(args.steps):
+        logup_column_device(dev, k + lw, tabs, h, LOGUP_BETA, out, m)
     kms, kn = dev.kernel_time("logup_column")
     dev.enable_timing(False)
     # device time per column: denominators + block scan, then the inverses (the
