@@ -190,6 +190,7 @@ int qg_ctx_destroy(qg_ctx* ctx) {
   (void)hipSetDevice(ctx->device);
   if (ctx->stream) (void)hipStreamSynchronize(ctx->stream);
   if (ctx->copy_stream) (void)hipStreamSynchronize(ctx->copy_stream);
+  if (ctx->side_stream) (void)hipStreamSynchronize(ctx->side_stream);
   comm_release(ctx);
   ctx->arena.release_all();
   for (auto& kv : ctx->pinned) (void)hipHostFree(kv.second.first);
@@ -200,6 +201,7 @@ int qg_ctx_destroy(qg_ctx* ctx) {
   for (auto e : ctx->event_pool) (void)hipEventDestroy(e);
   if (ctx->stream) (void)hipStreamDestroy(ctx->stream);
   if (ctx->copy_stream) (void)hipStreamDestroy(ctx->copy_stream);
+  if (ctx->side_stream) (void)hipStreamDestroy(ctx->side_stream);
   delete ctx;
   return QG_OK;
 }

@@ -56,6 +56,7 @@ struct qg_ctx {
   int device = 0;
   hipStream_t stream = nullptr;
   hipStream_t copy_stream = nullptr;  // host-to-device uploads overlapped with kernels (msm_host)
+  hipStream_t side_stream = nullptr;  // MSM bucketing beside the previous accumulation (msm.hip)
   std::string last_error;
   // grow-only scratch arena, one slot per purpose; every (re)allocation and
   // every table build gets a fresh generation number (arena.h), which caches
@@ -68,6 +69,7 @@ struct qg_ctx {
     std::string name;
     hipEvent_t a, b;
     bool ended;
+    hipStream_t s;
   };
   std::map<int, Ev> pending;  // handle -> region (stable across nested syncs)
   int next_handle = 0;
@@ -126,11 +128,11 @@ struct qg_ctx {
     QG_HIP(hipEventCreate(&e));
     return e;
   }
-  // begin/end a timed region on the context stream
-  int tbegin(const char* name) {
+  // begin/end a timed region on the context stream (or on stream s)
+  int tbegin(const char* name, hipStream_t s = nullptr) {
     if (!timing) return -1;
-    Ev e{name, ev_get(), ev_get(), false};
-    QG_HIP(hipEventRecord(e.a, stream));
+    Ev e{name, ev_get(), ev_get(), false, s ? s : stream};
+    QG_HIP(hipEventRecord(e.a, e.s));
     const int h = next_handle++;
     pending[h] = e;
     return h;
@@ -138,7 +140,7 @@ struct qg_ctx {
   void tend(int h) noexcept {
     auto it = pending.find(h);
     if (h < 0 || it == pending.end()) return;
-    (void)hipEventRecord(it->second.b, stream);
+    (void)hipEventRecord(it->second.b, it->second.s);
     it->second.ended = true;
   }
   // resolve the closed regions (after a stream sync); open ones stay pending
@@ -188,7 +190,7 @@ struct qg_srs {
 struct QgTimed {
   qg_ctx* c;
   int h;
-  QgTimed(qg_ctx* ctx, const char* name) : c(ctx), h(ctx->tbegin(name)) {}
+  QgTimed(qg_ctx* ctx, const char* name, hipStream_t s = nullptr) : c(ctx), h(ctx->tbegin(name, s)) {}
   ~QgTimed() { c->tend(h); }
 };
 

@@ -1321,11 +1321,21 @@ static constexpr int MSM_MAX_BATCH = 1024;
 
 // bucketing (two-pass radix sort) + bucket accumulation of MSM `slot` of a
 // batch: sum_i d_scalars[i] * base[srs_off + i]
+//
+// bst: the stream the bucketing runs on.  ctx->stream (default): everything in
+// stream order.  Another stream (msm_device_batch): the caller has made bst wait
+// for the scalars; the bucketing kernels queue there, the accumulation waits
+// for them by an event on ctx->stream, and the entry list gets its own slot,
+// so the next MSM's bucketing - memory-bound radix passes - runs on bst
+// beside this accumulation, which is VALU-bound and leaves a wave slot and
+// LDS per CU free.
 static MsmRun msm_accumulate_phase(qg_ctx* ctx, const qg_srs* srs, const Fr* d_scalars, size_t n,
-                                   int slot, size_t srs_off = 0) {
+                                   int slot, size_t srs_off = 0, hipStream_t bst = nullptr) {
   QG_CHECK(srs_off <= srs->n && n <= srs->n - srs_off, QG_ERR_INVALID, "MSM length exceeds the SRS");
   MsmRun run;
   const std::string sfx = "#" + std::to_string(slot);
+  const bool side = bst != nullptr && bst != ctx->stream;
+  if (!bst) bst = ctx->stream;
   if (n > 0) {
     const int c = srs->c, W = srs->W;
     const uint32_t nb = 1u << (c - 1);
@@ -1360,7 +1370,8 @@ static MsmRun msm_accumulate_phase(qg_ctx* ctx, const qg_srs* srs, const Fr* d_s
     Fr* canon = ctx->scratch_as<Fr>("msm_canon", n);
     uint32_t* counts = ctx->scratch_as<uint32_t>("msm_counts", nb);
     uint32_t* bstart = ctx->scratch_as<uint32_t>("msm_bstart" + sfx, nb + 1);
-    uint32_t* entries = ctx->scratch_as<uint32_t>("msm_entries", max_entries + 1);
+    uint32_t* entries = ctx->scratch_as<uint32_t>(side ? "msm_entries" + sfx : std::string("msm_entries"),
+                                                  max_entries + 1);
     const int ntiles = (int)div_up(nb, SCAN_TILE);
     uint2* tile_tot = ctx->scratch_as<uint2>("msm_tiles", ntiles);
     // entries per accumulation thread (flat chunks, k_msm_accumulate): 64, or
@@ -1409,29 +1420,29 @@ static MsmRun msm_accumulate_phase(qg_ctx* ctx, const qg_srs* srs, const Fr* d_s
              "MSM too large");
 
     {
-      QgTimed tm(ctx, "msm_bucketing");
+      QgTimed tm(ctx, "msm_bucketing", bst);
       // pass A: partition digits by the high bucket bits
       hipLaunchKernelGGL(k_sortA_hist, dim3(nblk), dim3(SORT_BLOCK), H * sizeof(uint32_t),
-                         ctx->stream, d_scalars, n, c, W, LO, H, nblk, tile, hrow, canon);
+                         bst, d_scalars, n, c, W, LO, H, nblk, tile, hrow, canon);
       QG_LAUNCH_CHECK();
       hipLaunchKernelGGL(k_transpose32, dim3(div_up(H, 32), div_up(nblk, 32)), dim3(256), 0,
-                         ctx->stream, hrow, nblk, (uint32_t)H, ghist);
+                         bst, hrow, nblk, (uint32_t)H, ghist);
       QG_LAUNCH_CHECK();
       const unsigned gt = div_up(nghist, 2048);
       QG_CHECK(gt <= 1024u * 1024u, QG_ERR_UNSUPPORTED, "histogram too large");
-      hipLaunchKernelGGL(k_scan32_tiles, dim3(gt), dim3(256), 0, ctx->stream, ghist, nghist, goff,
+      hipLaunchKernelGGL(k_scan32_tiles, dim3(gt), dim3(256), 0, bst, ghist, nghist, goff,
                          gtiles);
       QG_LAUNCH_CHECK();
-      hipLaunchKernelGGL(k_scan32_top, dim3(1), dim3(1024), 0, ctx->stream, gtiles, (int)gt,
+      hipLaunchKernelGGL(k_scan32_top, dim3(1), dim3(1024), 0, bst, gtiles, (int)gt,
                          goff + nghist);
       QG_LAUNCH_CHECK();
-      hipLaunchKernelGGL(k_scan32_add, dim3(div_up(nghist, 256)), dim3(256), 0, ctx->stream, gtiles,
+      hipLaunchKernelGGL(k_scan32_add, dim3(div_up(nghist, 256)), dim3(256), 0, bst, gtiles,
                          nghist, goff);
       QG_LAUNCH_CHECK();
       hipLaunchKernelGGL(k_transpose32, dim3(div_up(nblk, 32), div_up(H, 32)), dim3(256), 0,
-                         ctx->stream, goff, (uint32_t)H, nblk, orow);
+                         bst, goff, (uint32_t)H, nblk, orow);
       QG_LAUNCH_CHECK();
-      hipLaunchKernelGGL(k_sortA_rows, dim3(nblk), dim3(SORT_BLOCK), 0, ctx->stream, hrow, orow, H);
+      hipLaunchKernelGGL(k_sortA_rows, dim3(nblk), dim3(SORT_BLOCK), 0, bst, hrow, orow, H);
       QG_LAUNCH_CHECK();
       const size_t smemA = (size_t)tile * W * 8 + (3 * (size_t)H + SORT_BLOCK) * 4;
       QG_CHECK(smemA <= 160 * 1024, QG_ERR_UNSUPPORTED, "pass-A tile exceeds LDS");
@@ -1444,28 +1455,28 @@ static MsmRun msm_accumulate_phase(qg_ctx* ctx, const qg_srs* srs, const Fr* d_s
                                    hipFuncAttributeMaxDynamicSharedMemorySize, 160 * 1024));
         ctx->memo["msm_lds_attr"] = "1";
       }
-      hipLaunchKernelGGL(k_sortA_scatter, dim3(nblk), dim3(SORT_BLOCK), smemA, ctx->stream,
+      hipLaunchKernelGGL(k_sortA_scatter, dim3(nblk), dim3(SORT_BLOCK), smemA, bst,
                          canon, n, srs->n, srs_off, c, W, LO, H, nblk, tile, hrow, orow, tmp_e, tmp_l);
       QG_LAUNCH_CHECK();
       // pass B: sort every group by the low bits, in chunks
-      hipLaunchKernelGGL(k_sort_chunks, dim3(1), dim3(1024), 0, ctx->stream, goff, nblk, H,
+      hipLaunchKernelGGL(k_sort_chunks, dim3(1), dim3(1024), 0, bst, goff, nblk, H,
                          gstart, cbase, cgroup, misc);
       QG_LAUNCH_CHECK();
       hipLaunchKernelGGL(k_sortB_hist, dim3((unsigned)max_chunks), dim3(SORT_BLOCK),
-                         NL * sizeof(uint32_t), ctx->stream, tmp_l, gstart, cbase, cgroup, misc, NL,
+                         NL * sizeof(uint32_t), bst, tmp_l, gstart, cbase, cgroup, misc, NL,
                          chist);
       QG_LAUNCH_CHECK();
-      hipLaunchKernelGGL(k_sort_bucket_count, dim3(div_up(nb, 256)), dim3(256), 0, ctx->stream,
+      hipLaunchKernelGGL(k_sort_bucket_count, dim3(div_up(nb, 256)), dim3(256), 0, bst,
                          cbase, chist, LO, nb, counts);
       QG_LAUNCH_CHECK();
-      hipLaunchKernelGGL(k_scan_tiles, dim3(ntiles), dim3(SCAN_BLOCK), 0, ctx->stream, counts,
+      hipLaunchKernelGGL(k_scan_tiles, dim3(ntiles), dim3(SCAN_BLOCK), 0, bst, counts,
                          (size_t)nb, L, bstart, tile_tot, misc + 1);
       QG_LAUNCH_CHECK();
-      hipLaunchKernelGGL(k_scan_top, dim3(1), dim3(1024), 0, ctx->stream, tile_tot, ntiles,
+      hipLaunchKernelGGL(k_scan_top, dim3(1), dim3(1024), 0, bst, tile_tot, ntiles,
                          bstart, (size_t)nb);
       QG_LAUNCH_CHECK();
       run.gen = ++ctx->msm_gen;
-      hipLaunchKernelGGL(k_scan_add, dim3(div_up(nb, 256)), dim3(256), 0, ctx->stream, tile_tot,
+      hipLaunchKernelGGL(k_scan_add, dim3(div_up(nb, 256)), dim3(256), 0, bst, tile_tot,
                          (size_t)nb, bstart, counts, L, T, misc, run.gen, owner, nslots);
       QG_LAUNCH_CHECK();
       {
@@ -1473,19 +1484,25 @@ static MsmRun msm_accumulate_phase(qg_ctx* ctx, const qg_srs* srs, const Fr* d_s
         uint32_t* hmx =
             reinterpret_cast<uint32_t*>(ctx->pinned_get("msm_mx", MSM_MAX_BATCH * 4 * sizeof(uint32_t)));
         QG_HIP(hipMemcpyAsync(hmx + 4 * slot, misc + 1, 4 * sizeof(uint32_t), hipMemcpyDeviceToHost,
-                              ctx->stream));
+                              bst));
         run.ev_mx = ctx->ev_get();
-        QG_HIP(hipEventRecord(run.ev_mx, ctx->stream));
+        QG_HIP(hipEventRecord(run.ev_mx, bst));
         run.h_mx = hmx + 4 * slot;
       }
-      hipLaunchKernelGGL(k_sort_chunk_offsets, dim3(div_up(nb, 256)), dim3(256), 0, ctx->stream,
+      hipLaunchKernelGGL(k_sort_chunk_offsets, dim3(div_up(nb, 256)), dim3(256), 0, bst,
                          cbase, chist, LO, nb, bstart, coff);
       QG_LAUNCH_CHECK();
       const size_t smemB = (size_t)SORT_CHUNK * 6 + (3 * (size_t)NL + SORT_BLOCK) * 4;
       hipLaunchKernelGGL(k_sortB_scatter, dim3((unsigned)max_chunks), dim3(SORT_BLOCK), smemB,
-                         ctx->stream, tmp_e, tmp_l, gstart, cbase, cgroup, misc, NL, chist, coff,
+                         bst, tmp_e, tmp_l, gstart, cbase, cgroup, misc, NL, chist, coff,
                          entries);
       QG_LAUNCH_CHECK();
+    }
+    if (side) {  // the accumulation (ctx->stream) after this bucketing
+      hipEvent_t ev = ctx->ev_get();
+      QG_HIP(hipEventRecord(ev, bst));
+      QG_HIP(hipStreamWaitEvent(ctx->stream, ev, 0));
+      ctx->event_pool.push_back(ev);
     }
     {
       QgTimed tm(ctx, "msm_accumulate");
@@ -1665,13 +1682,33 @@ static G1Affine msm_finish_ranks(qg_ctx* ctx, G1Xyzz acc) {
 
 // k MSMs over the same SRS (KZG openings of one proof); results per MSM,
 // summed over the RCCL ranks when a communicator is attached
+//
+// Batches of two or more MSMs bucket on ctx->side_stream: MSM i + 1's radix
+// passes (memory-bound) run beside MSM i's accumulation (VALU-bound), which
+// slows by ~0.3 ms per 1 ms of bucketing it hosts.  HyperPlonk proof
+// 929 / 935 -> 907 / 912 ms, same transcript (profiles/r05_msm_pipe_ab.txt).
+// A lone MSM split into pieces to get the same overlap is slower (2^24:
+// 18.15 -> 18.7 ms with 2 pieces: each piece pays its own bucket reduction,
+// and the accumulation slows by 0.85 ms under the second piece's bucketing).
+// QG_MSM_PIPE=0 keeps every bucketing on ctx->stream (A/B runs).
 std::vector<G1Affine> msm_device_batch(qg_ctx* ctx, const qg_srs* srs,
                                        const std::vector<const Fr*>& scalars,
                                        const std::vector<size_t>& ns) {
   QG_CHECK(scalars.size() == ns.size(), QG_ERR_INVALID, "MSM batch shape");
+  bool pipe = scalars.size() >= 2;
+  if (const char* ov = getenv("QG_MSM_PIPE")) pipe = pipe && atoi(ov) != 0;
+  hipStream_t bst = nullptr;
+  if (pipe) {
+    if (!ctx->side_stream) QG_HIP(hipStreamCreateWithFlags(&ctx->side_stream, hipStreamNonBlocking));
+    bst = ctx->side_stream;
+    hipEvent_t ev = ctx->ev_get();  // the scalars are ready in ctx->stream order
+    QG_HIP(hipEventRecord(ev, ctx->stream));
+    QG_HIP(hipStreamWaitEvent(bst, ev, 0));
+    ctx->event_pool.push_back(ev);
+  }
   std::vector<MsmRun> runs;
   for (size_t i = 0; i < scalars.size(); i++)
-    runs.push_back(msm_accumulate_phase(ctx, srs, scalars[i], ns[i], (int)i));
+    runs.push_back(msm_accumulate_phase(ctx, srs, scalars[i], ns[i], (int)i, 0, bst));
   std::vector<G1Xyzz> local;
   msm_reduce_phase(ctx, srs, runs, local);
   std::vector<G1Affine> res(local.size());
