@@ -1420,7 +1420,9 @@ static MsmRun msm_accumulate_phase(qg_ctx* ctx, const qg_srs* srs, const Fr* d_s
              "MSM too large");
 
     {
-      QgTimed tm(ctx, "msm_bucketing", bst);
+      // on the side stream the region is the bucketing's span there, overlapped
+      // with the previous MSM's accumulation: its own name
+      QgTimed tm(ctx, side ? "msm_bucketing_side" : "msm_bucketing", bst);
       // pass A: partition digits by the high bucket bits
       hipLaunchKernelGGL(k_sortA_hist, dim3(nblk), dim3(SORT_BLOCK), H * sizeof(uint32_t),
                          bst, d_scalars, n, c, W, LO, H, nblk, tile, hrow, canon);

@@ -35,8 +35,9 @@ pytestmark = pytest.mark.gpu
 ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
 TIMES = os.path.join(ROOT, "gpurun_out", "sharded_full_times.json")
 TAU = 0x5155494C4C2D53525321  # bench.py's synthetic trapdoor
-PHASES = ("msm_bucketing", "msm_accumulate", "msm_reduce", "sumcheck_round", "sumcheck_tail",
-          "logup_column", "eq_table", "inner_product", "s_polynomial", "kzg_division")
+PHASES = ("msm_bucketing", "msm_bucketing_side", "msm_accumulate", "msm_reduce", "sumcheck_round",
+          "sumcheck_tail", "logup_column", "eq_table", "inner_product", "s_polynomial",
+          "kzg_division")
 
 
 def _record(key, value):
