@@ -5,6 +5,8 @@ for bit against the default path on the same inputs:
     tables at nvars >= 15 over 8 loopback ranks, ADVICE r3 medium);
   * k_logup_fused, the one-pass Logup column (QG_LOGUP_FUSED=1);
   * the replicated S polynomial in the sharded ML opening (QG_S_REPLICATED=1).
+  * an MSM batch's bucketing in stream order instead of on the side stream
+    (QG_MSM_PIPE=0).
 The switches are read per call, so the tests toggle them in-process."""
 import contextlib
 import os
@@ -156,3 +158,31 @@ def test_alternate_accumulate_matches_default(n, small, mode):
     d.close()
     assert out["0"] == out["1"]
     assert out["1"] == o.g1_mul(o.G1_GEN, o.poly_eval(scal, tau))
+
+
+@pytest.mark.parametrize("nv", [9, 14, 17])
+def test_side_stream_bucketing_matches_stream_order(dev, nv):
+    """An ML opening runs its quotient MSMs as one batch whose 2nd.. MSMs bucket
+    on the context's side stream beside the previous MSM's accumulation
+    (msm_device_batch); QG_MSM_PIPE=0 keeps every bucketing on the context
+    stream.  Same proof and transcript state, and the opened value is the MLE
+    evaluation."""
+    import quill_amd as q
+    from quill_amd import KZG, Transcript
+    rnd = random.Random(4100 + nv)
+    N = 1 << nv
+    tau = rnd.randrange(R)
+    kzg = KZG(dev, q.Srs.generate(dev, tau, N), N - 1)
+    poly = [rnd.randrange(R) for _ in range(N)]
+    vec = q.DeviceVec.from_list(dev, poly)
+    point = [rnd.randrange(R) for _ in range(nv)]
+    res = []
+    for pipe in ("1", "0"):
+        with env("QG_MSM_PIPE", pipe):
+            t = Transcript(b"pipe")
+            pr = kzg.open_dev(vec, N, point, t)
+            res.append((pr, t.state))
+    vec.close()
+    kzg.srs.close()
+    assert res[0] == res[1]
+    assert res[0][0].evaluation == o.mle_evaluate(poly, point)
