@@ -220,6 +220,23 @@ int qg_mle_open_dev(qg_ctx* ctx, const qg_srs* srs, const qg_buf* poly, size_t n
 int qg_mle_open_dev_ex(qg_ctx* ctx, const qg_srs* srs, const qg_buf* poly, size_t n,
                        const uint64_t* point, size_t nvars, uint8_t state[32], uint32_t flags,
                        qg_mle_proof* out);
+/* K openings in one call (at most 256), item k exactly as the k-th of K
+ * successive qg_mle_open_dev_ex calls on the same transcript: same proofs, same
+ * final `state`.  The S polynomial, its commitment and the evaluation depend
+ * on (poly, point) only and no quotient commitment enters the transcript
+ * (mlpcs.rs:83-124), so the device runs the K S commitments as one MSM batch,
+ * the K transcript steps on the host, then all 4K quotient commitments as one
+ * MSM batch.  HyperPlonk's openings of one trace (proof.rs:203-224). */
+typedef struct qg_mle_open_item {
+  const qg_buf* poly;     /* device evaluations (first n entries) */
+  size_t n;
+  const uint64_t* point;  /* nvars Fr */
+  size_t nvars;
+  uint32_t flags;         /* QG_OPEN_UNCHANGED or 0 */
+  uint32_t _pad;
+} qg_mle_open_item;
+int qg_mle_open_batch_dev(qg_ctx* ctx, const qg_srs* srs, const qg_mle_open_item* items,
+                          size_t k, uint8_t state[32], qg_mle_proof* outs);
 
 /* ---------------------------------------------------------------- verifiers (host) */
 /* BN254 G2 affine points on the D-type twist E'/Fq2 (y^2 = x^3 + 3/(9 + u)):

@@ -45,7 +45,13 @@ struct HipAlloc {
     QG_HIP(hipMalloc(&p, b));
     return p;
   }
-  static void release(void* p) { (void)hipFree(p); }
+  // a slot that grows is released while kernels queued on any of the
+  // context's streams (the MSM batch's side stream included) may still read
+  // it: drain the device first
+  static void release(void* p) {
+    (void)hipDeviceSynchronize();
+    (void)hipFree(p);
+  }
 };
 
 }  // namespace qg

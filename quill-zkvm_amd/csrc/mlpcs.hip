@@ -847,23 +847,26 @@ static size_t trimmed_len(qg_ctx* ctx, const Fr* a, size_t n) {
 // suffix-Horner recursion, and the four values y = s_0 queued into pinned
 // memory (h_y[4]) without a round trip: the caller reads them after its next
 // synchronization (the quotient MSMs')
+// `slot` keeps the quotient buffers of several openings apart (a batch of
+// openings commits all of its quotients at once, mle_open_batch_device).
 static void kzg_quotients_batch(qg_ctx* ctx, const qg_srs* srs, const Fr* const polys[4],
                                 const size_t Lt[4], const Fr xs[4], qg_kzg_opening* const outs[4],
-                                std::vector<const Fr*>& qs, std::vector<size_t>& qns, Fr* h_y) {
+                                std::vector<const Fr*>& qs, std::vector<size_t>& qns, Fr* h_y,
+                                size_t slot = 0) {
   std::vector<ShIn> jobs;
   Fr* s[4] = {nullptr, nullptr, nullptr, nullptr};
   for (int i = 0; i < 4; i++) {
     fr_export(xs[i], outs[i]->x);
     if (Lt[i] == 0) continue;
     QG_CHECK(Lt[i] - 1 <= srs->n, QG_ERR_INVALID, "Polynomial degree exceeds max degree");
-    s[i] = ctx->scratch_as<Fr>("open_s#" + std::to_string(i), Lt[i]);
+    s[i] = ctx->scratch_as<Fr>("open_s#" + std::to_string(4 * slot + i), Lt[i]);
     jobs.push_back({polys[i], Lt[i], xs[i], s[i]});
   }
   {
     QgTimed tm(ctx, "kzg_division");
     suffix_horner_batch(ctx, jobs);
   }
-  Fr* d_y = ctx->scratch_as<Fr>("open_y", 4);
+  Fr* d_y = ctx->scratch_as<Fr>("open_y#" + std::to_string(slot), 4);
   QG_HIP(hipMemsetAsync(d_y, 0, 4 * sizeof(Fr), ctx->stream));
   for (int i = 0; i < 4; i++)
     if (s[i])
@@ -1374,6 +1377,153 @@ static void mle_open_device(qg_ctx* ctx, const qg_srs* srs, const Fr* dpoly, siz
   }
 }
 
+// K ML openings with the transcript steps in item order — the same proofs and
+// final state as K successive mle_open_device calls — restructured around the
+// protocol's data flow (mlpcs.rs:83-124): S, its commitment, the evaluation
+// and the trimmed lengths depend on the polynomial and the point only, and
+// the transcript absorbs no quotient commitment, so
+//   1. every item's evaluation, S polynomial and trimmed lengths (queued),
+//   2. the K S commitments as ONE MSM batch (one synchronization),
+//   3. the K transcript steps on the host (append point, evaluation, s_comm;
+//      draw r),
+//   4. the 4K quotients and their commitments as ONE MSM batch.
+// Inside a batch the bucketing of MSM i + 1 runs on the side stream beside
+// MSM i's accumulation, and the batch pays one set of reduction launches and
+// one host round trip (msm.hip).  Sharded contexts open item by item.
+struct MleOpenItem {
+  const Fr* poly;
+  size_t n;
+  const uint64_t* point;
+  size_t nvars;
+  bool unchanged;
+  uint64_t id;
+  size_t off;
+};
+
+static void mle_open_batch_device(qg_ctx* ctx, const qg_srs* srs,
+                                  const std::vector<MleOpenItem>& items, uint8_t state[32],
+                                  qg_mle_proof* outs) {
+  const size_t K = items.size();
+  if (ctx->sharded || K <= 1) {
+    for (size_t k = 0; k < K; k++)
+      mle_open_device(ctx, srs, items[k].poly, items[k].n, items[k].point, items[k].nvars, state,
+                      &outs[k], items[k].unchanged, items[k].id, items[k].off);
+    return;
+  }
+  unsigned long long* h_len = reinterpret_cast<unsigned long long*>(
+      ctx->pinned_get("mleb_len_h", 2 * K * sizeof(unsigned long long)));
+  unsigned long long* d_len = ctx->scratch_as<unsigned long long>("mleb_len", 2 * K);
+  Fr* h_eval = reinterpret_cast<Fr*>(ctx->pinned_get("mleb_eval_h", K * sizeof(Fr)));
+  Fr* d_eval = ctx->scratch_as<Fr>("mleb_eval", K);
+  QG_HIP(hipMemsetAsync(d_len, 0, 2 * K * sizeof(unsigned long long), ctx->stream));
+  // the opened vectors' trimmed lengths: remembered for the QG_OPEN_UNCHANGED
+  // contract exactly as K successive mle_open_device calls would (the memo
+  // holds the last opened vector's key and length): item k reuses it when
+  // flagged and item k - 1 (item 0: the memo from before this call) opened
+  // the same vector
+  std::string& lt_memo = ctx->arena.memo["mle_poly_len"];
+  const std::string memo_in = lt_memo;
+  std::vector<std::string> lt_key(K);
+  std::vector<char> lt_known(K, 0);
+  std::vector<Fr*> dS(K, nullptr);
+  std::vector<size_t> Sn(K, 0), s_msm(K, 0);
+  bool s_trim_first = false;
+  for (size_t k = 0; k < K; k++) {
+    const MleOpenItem& it = items[k];
+    QG_CHECK(it.nvars <= 30, QG_ERR_INVALID, "too many variables");
+    const size_t N = (size_t)1 << it.nvars;
+    lt_key[k] = it.id ? std::to_string(it.id) + "+" + std::to_string(it.off) + ":" +
+                            std::to_string(it.n) + "="
+                      : std::string();
+    lt_known[k] = it.unchanged && it.id &&
+                  (k == 0 ? memo_in.compare(0, lt_key[k].size(), lt_key[k]) == 0
+                          : lt_key[k - 1] == lt_key[k]);
+    if (!lt_known[k]) trim_launch(ctx, it.poly, it.n, d_len + 2 * k);
+    Fr* dz = ctx->scratch_as<Fr>("mleb_z#" + std::to_string(k), it.nvars ? it.nvars : 1);
+    Fr* dpr = ctx->scratch_as<Fr>("mle_pr", N);
+    fr_upload(ctx, dz, it.point, it.nvars);
+    eq_table_device(ctx, dz, (uint32_t)it.nvars, dpr);
+    dot_to_device(ctx, it.poly, dpr, it.n < N ? it.n : N, d_eval + k);
+    const size_t M = it.n > N ? it.n : N;
+    Sn[k] = M > 1 ? M - 1 : 0;
+    dS[k] = ctx->scratch_as<Fr>("mleb_S#" + std::to_string(k), Sn[k] ? Sn[k] : 1);
+    if (Sn[k])
+      s_poly_device(ctx, it.poly, it.n, dpr, N, dS[k], it.point, it.nvars, it.unchanged, it.id,
+                    it.off);
+    trim_launch(ctx, dS[k], Sn[k], d_len + 2 * k + 1);
+    s_msm[k] = Sn[k];
+    s_trim_first = s_trim_first || Sn[k] > srs->n;
+  }
+  QG_HIP(hipMemcpyAsync(h_len, d_len, 2 * K * sizeof(unsigned long long), hipMemcpyDeviceToHost,
+                        ctx->stream));
+  QG_HIP(hipMemcpyAsync(h_eval, d_eval, K * sizeof(Fr), hipMemcpyDeviceToHost, ctx->stream));
+  if (s_trim_first) {  // an S longer than the SRS: its trimmed length decides
+    ctx->sync();
+    for (size_t k = 0; k < K; k++)
+      if (Sn[k] > srs->n) {
+        s_msm[k] = (size_t)h_len[2 * k + 1];
+        QG_CHECK(s_msm[k] <= srs->n, QG_ERR_INVALID, "Polynomial degree exceeds max degree");
+      }
+  }
+  std::vector<const Fr*> sp(dS.begin(), dS.end());
+  const std::vector<G1Affine> s_comm = msm_device_batch(ctx, srs, sp, s_msm);
+  ctx->sync();  // (drained already unless every MSM was empty)
+  // the transcript steps in item order (mlpcs.rs:100-107)
+  std::vector<Fr> rs(K), rinv(K);
+  std::vector<size_t> Lt(K);
+  for (size_t k = 0; k < K; k++) {
+    const MleOpenItem& it = items[k];
+    if (lt_known[k])
+      Lt[k] = k == 0 ? (size_t)std::stoull(memo_in.substr(lt_key[k].size())) : Lt[k - 1];
+    else
+      Lt[k] = (size_t)h_len[2 * k];
+    lt_memo = it.id ? lt_key[k] + std::to_string(Lt[k]) : std::string();
+    const Fr evaluation = h_eval[k];
+    std::vector<uint8_t> msg(8 + 32 * it.nvars);
+    u64_to_bytes(it.nvars, msg.data());
+    for (size_t i = 0; i < it.nvars; i++)
+      fr_to_bytes(fr_import(it.point + 4 * i), msg.data() + 8 + 32 * i);
+    transcript_append(state, msg.data(), msg.size());
+    uint8_t b32[32], b64[64];
+    fr_to_bytes(evaluation, b32);
+    transcript_append(state, b32, 32);
+    g1_serialize(s_comm[k], b64);
+    transcript_append(state, b64, 64);
+    rs[k] = transcript_draw_fr(state);
+    QG_CHECK(!rs[k].is_zero(), QG_ERR_ASSERT, "challenge r = 0");
+    rinv[k] = finv(rs[k]);
+    fr_export(evaluation, outs[k].evaluation);
+    g1_export(s_comm[k], outs[k].s_comm_xy, &outs[k].s_comm_inf);
+  }
+  // every item's four quotients (mlpcs.rs:108-113), then all 4K commitments
+  Fr* h_y = reinterpret_cast<Fr*>(ctx->pinned_get("mleb_y_h", 4 * K * sizeof(Fr)));
+  std::vector<const Fr*> qs_all;
+  std::vector<size_t> qns_all;
+  for (size_t k = 0; k < K; k++) {
+    qg_kzg_opening* o4[4] = {&outs[k].poly_opening, &outs[k].poly_opening_inv,
+                             &outs[k].s_opening, &outs[k].s_opening_inv};
+    const Fr* polys[4] = {items[k].poly, items[k].poly, dS[k], dS[k]};
+    const size_t slen = (size_t)h_len[2 * k + 1];
+    const size_t lts[4] = {Lt[k], Lt[k], slen, slen};
+    const Fr xs[4] = {rs[k], rinv[k], rs[k], rinv[k]};
+    std::vector<const Fr*> qs;
+    std::vector<size_t> qns;
+    kzg_quotients_batch(ctx, srs, polys, lts, xs, o4, qs, qns, h_y + 4 * k, k);
+    qs_all.insert(qs_all.end(), qs.begin(), qs.end());
+    qns_all.insert(qns_all.end(), qns.begin(), qns.end());
+  }
+  const std::vector<G1Affine> pis = msm_device_batch(ctx, srs, qs_all, qns_all);
+  ctx->sync();  // (drained already unless every quotient was empty)
+  for (size_t k = 0; k < K; k++) {
+    qg_kzg_opening* o4[4] = {&outs[k].poly_opening, &outs[k].poly_opening_inv,
+                             &outs[k].s_opening, &outs[k].s_opening_inv};
+    for (int i = 0; i < 4; i++) {
+      fr_export(h_y[4 * k + i], o4[i]->y);
+      g1_export(pis[4 * k + i], o4[i]->proof_xy, &o4[i]->proof_inf);
+    }
+  }
+}
+
 }  // namespace qg
 
 extern "C" {
@@ -1441,6 +1591,25 @@ int qg_mle_open_dev(qg_ctx* ctx, const qg_srs* srs, const qg_buf* poly, size_t n
     QG_CHECK(nvars <= 30, QG_ERR_INVALID, "too many variables");
     QG_HIP(hipSetDevice(ctx->device));
     mle_open_device(ctx, srs, poly->d, n, point, nvars, state, out);
+  });
+}
+
+int qg_mle_open_batch_dev(qg_ctx* ctx, const qg_srs* srs, const qg_mle_open_item* items,
+                          size_t k, uint8_t state[32], qg_mle_proof* outs) {
+  if (!ctx || !srs || (!items && k) || !state || (!outs && k)) return QG_ERR_INVALID;
+  for (size_t i = 0; i < k; i++)
+    if (!items[i].poly || items[i].n > items[i].poly->n || (!items[i].point && items[i].nvars) ||
+        (items[i].flags & ~(uint32_t)QG_OPEN_UNCHANGED))
+      return QG_ERR_INVALID;
+  return qg_guard(ctx, [&] {
+    QG_CHECK(k <= 256, QG_ERR_UNSUPPORTED, "too many openings in one batch (at most 256)");
+    QG_HIP(hipSetDevice(ctx->device));
+    std::vector<MleOpenItem> v(k);
+    for (size_t i = 0; i < k; i++)
+      v[i] = {items[i].poly->d, items[i].n, items[i].point, items[i].nvars,
+              (items[i].flags & QG_OPEN_UNCHANGED) != 0, items[i].poly->alloc_id,
+              items[i].poly->base_off};
+    mle_open_batch_device(ctx, srs, v, state, outs);
   });
 }
 

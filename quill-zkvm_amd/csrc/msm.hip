@@ -1316,6 +1316,9 @@ struct MsmRun {
   const uint32_t* h_mx = nullptr;
   hipEvent_t ev_mx = nullptr;
   uint32_t gen = 0;  // misc[4] of this run: h_mx[3] must equal it
+  // side mode: the end of this MSM's bucketing on the side stream (the
+  // accumulation waits for it); back to the pool once the batch is done
+  hipEvent_t ev_b = nullptr;
 };
 static constexpr int MSM_MAX_BATCH = 1024;
 
@@ -1329,8 +1332,18 @@ static constexpr int MSM_MAX_BATCH = 1024;
 // so the next MSM's bucketing - memory-bound radix passes - runs on bst
 // beside this accumulation, which is VALU-bound and leaves a wave slot and
 // LDS per CU free.
+// side mode: the entry list lives in one of two slots by MSM parity; the
+// bucketing first waits for `reuse_wait` (the accumulation of MSM slot - 2,
+// the slot's last reader), and `acc_done` receives an event after this
+// accumulation (both owned by the caller).
+// reserve: only size the shared bucketing scratch and both entry-list slots
+// for an MSM of length n, launching nothing.  A batch reserves for its
+// longest MSM first: a slot that grew in the middle of a batch would be
+// freed while an earlier MSM's kernels, queued on either stream, still read it.
 static MsmRun msm_accumulate_phase(qg_ctx* ctx, const qg_srs* srs, const Fr* d_scalars, size_t n,
-                                   int slot, size_t srs_off = 0, hipStream_t bst = nullptr) {
+                                   int slot, size_t srs_off = 0, hipStream_t bst = nullptr,
+                                   hipEvent_t reuse_wait = nullptr, hipEvent_t acc_done = nullptr,
+                                   bool reserve = false) {
   QG_CHECK(srs_off <= srs->n && n <= srs->n - srs_off, QG_ERR_INVALID, "MSM length exceeds the SRS");
   MsmRun run;
   const std::string sfx = "#" + std::to_string(slot);
@@ -1370,8 +1383,13 @@ static MsmRun msm_accumulate_phase(qg_ctx* ctx, const qg_srs* srs, const Fr* d_s
     Fr* canon = ctx->scratch_as<Fr>("msm_canon", n);
     uint32_t* counts = ctx->scratch_as<uint32_t>("msm_counts", nb);
     uint32_t* bstart = ctx->scratch_as<uint32_t>("msm_bstart" + sfx, nb + 1);
-    uint32_t* entries = ctx->scratch_as<uint32_t>(side ? "msm_entries" + sfx : std::string("msm_entries"),
-                                                  max_entries + 1);
+    uint32_t* entries = ctx->scratch_as<uint32_t>(
+        side ? "msm_entries#p" + std::to_string(slot & 1) : std::string("msm_entries"), max_entries + 1);
+    if (reserve) {
+      if (side) ctx->scratch_as<uint32_t>("msm_entries#p" + std::to_string((slot & 1) ^ 1), max_entries + 1);
+      return run;
+    }
+    if (side && reuse_wait) QG_HIP(hipStreamWaitEvent(bst, reuse_wait, 0));
     const int ntiles = (int)div_up(nb, SCAN_TILE);
     uint2* tile_tot = ctx->scratch_as<uint2>("msm_tiles", ntiles);
     // entries per accumulation thread (flat chunks, k_msm_accumulate): 64, or
@@ -1501,10 +1519,9 @@ static MsmRun msm_accumulate_phase(qg_ctx* ctx, const qg_srs* srs, const Fr* d_s
       QG_LAUNCH_CHECK();
     }
     if (side) {  // the accumulation (ctx->stream) after this bucketing
-      hipEvent_t ev = ctx->ev_get();
-      QG_HIP(hipEventRecord(ev, bst));
-      QG_HIP(hipStreamWaitEvent(ctx->stream, ev, 0));
-      ctx->event_pool.push_back(ev);
+      run.ev_b = ctx->ev_get();
+      QG_HIP(hipEventRecord(run.ev_b, bst));
+      QG_HIP(hipStreamWaitEvent(ctx->stream, run.ev_b, 0));
     }
     {
       QgTimed tm(ctx, "msm_accumulate");
@@ -1531,6 +1548,7 @@ static MsmRun msm_accumulate_phase(qg_ctx* ctx, const qg_srs* srs, const Fr* d_s
                            partial, owner);
       QG_LAUNCH_CHECK();
     }
+    if (side && acc_done) QG_HIP(hipEventRecord(acc_done, ctx->stream));
     run.empty = n == 0;
     run.L = L;
     run.T = T;
@@ -1685,34 +1703,54 @@ static G1Affine msm_finish_ranks(qg_ctx* ctx, G1Xyzz acc) {
 // k MSMs over the same SRS (KZG openings of one proof); results per MSM,
 // summed over the RCCL ranks when a communicator is attached
 //
-// Batches of two or more MSMs bucket on ctx->side_stream: MSM i + 1's radix
-// passes (memory-bound) run beside MSM i's accumulation (VALU-bound), which
-// slows by ~0.3 ms per 1 ms of bucketing it hosts.  HyperPlonk proof
-// 929 / 935 -> 907 / 912 ms, same transcript (profiles/r05_msm_pipe_ab.txt).
-// A lone MSM split into pieces to get the same overlap is slower (2^24:
-// 18.15 -> 18.7 ms with 2 pieces: each piece pays its own bucket reduction,
-// and the accumulation slows by 0.85 ms under the second piece's bucketing).
-// QG_MSM_PIPE=0 keeps every bucketing on ctx->stream (A/B runs).
+// QG_MSM_PIPE=1 (opt-in, off by default): batches of two or more MSMs bucket
+// on ctx->side_stream, MSM i + 1's radix passes (memory-bound) beside MSM i's
+// accumulation (VALU-bound), which slows by ~0.3 ms per 1 ms of bucketing it
+// hosts.  HyperPlonk proof 929 / 935 -> 907 / 912 ms with the openings' batches
+// of four (profiles/r05_msm_pipe_ab.txt).  Not the default: in the batches of
+// 4K quotients of a batched opening (mle_open_batch_device) some commitments
+// came out wrong with it, intermittently (micro/open_batch_dbg.py, 2^14 rows;
+// profiles/r05_open_batch_ab.txt), and the cause is not found yet.  A lone
+// MSM split into pieces to get the same overlap is slower (2^24: 18.15 ->
+// 18.7 ms with 2 pieces: each piece pays its own bucket reduction, and the
+// accumulation slows by 0.85 ms under the second piece's bucketing).
 std::vector<G1Affine> msm_device_batch(qg_ctx* ctx, const qg_srs* srs,
                                        const std::vector<const Fr*>& scalars,
                                        const std::vector<size_t>& ns) {
   QG_CHECK(scalars.size() == ns.size(), QG_ERR_INVALID, "MSM batch shape");
-  bool pipe = scalars.size() >= 2;
-  if (const char* ov = getenv("QG_MSM_PIPE")) pipe = pipe && atoi(ov) != 0;
+  bool pipe = false;
+  if (const char* ov = getenv("QG_MSM_PIPE")) pipe = scalars.size() >= 2 && atoi(ov) != 0;
   hipStream_t bst = nullptr;
+  hipEvent_t ev_in = nullptr;
   if (pipe) {
     if (!ctx->side_stream) QG_HIP(hipStreamCreateWithFlags(&ctx->side_stream, hipStreamNonBlocking));
     bst = ctx->side_stream;
-    hipEvent_t ev = ctx->ev_get();  // the scalars are ready in ctx->stream order
-    QG_HIP(hipEventRecord(ev, ctx->stream));
-    QG_HIP(hipStreamWaitEvent(bst, ev, 0));
-    ctx->event_pool.push_back(ev);
+    ev_in = ctx->ev_get();  // the scalars are ready in ctx->stream order
+    QG_HIP(hipEventRecord(ev_in, ctx->stream));
+    QG_HIP(hipStreamWaitEvent(bst, ev_in, 0));
+  }
+  if (scalars.size() >= 2) {  // size the shared scratch for the longest MSM first
+    size_t im = 0;
+    for (size_t i = 1; i < ns.size(); i++)
+      if (ns[i] > ns[im]) im = i;
+    msm_accumulate_phase(ctx, srs, scalars[im], ns[im], 0, 0, bst, nullptr, nullptr, true);
   }
   std::vector<MsmRun> runs;
-  for (size_t i = 0; i < scalars.size(); i++)
-    runs.push_back(msm_accumulate_phase(ctx, srs, scalars[i], ns[i], (int)i, 0, bst));
+  std::vector<hipEvent_t> acc_done;  // side mode: after each accumulation
+  for (size_t i = 0; i < scalars.size(); i++) {
+    if (pipe) acc_done.push_back(ctx->ev_get());
+    runs.push_back(msm_accumulate_phase(ctx, srs, scalars[i], ns[i], (int)i, 0, bst,
+                                        pipe && i >= 2 ? acc_done[i - 2] : nullptr,
+                                        pipe ? acc_done[i] : nullptr));
+  }
   std::vector<G1Xyzz> local;
-  msm_reduce_phase(ctx, srs, runs, local);
+  msm_reduce_phase(ctx, srs, runs, local);  // ends with a stream synchronization
+  // every event this batch waited on goes back only now: a recycled event
+  // re-recorded before a queued wait on it ran would move that wait
+  for (hipEvent_t e : acc_done) ctx->event_pool.push_back(e);
+  for (const MsmRun& r : runs)
+    if (r.ev_b) ctx->event_pool.push_back(r.ev_b);
+  if (ev_in) ctx->event_pool.push_back(ev_in);
   std::vector<G1Affine> res(local.size());
   for (size_t i = 0; i < local.size(); i++) res[i] = msm_finish_ranks(ctx, local[i]);
   return res;

@@ -40,6 +40,11 @@ class MleProof(C.Structure):
                 ("s_opening", KzgOpening), ("s_opening_inv", KzgOpening)]
 
 
+class MleOpenItem(C.Structure):
+    _fields_ = [("poly", C.c_void_p), ("n", C.c_size_t), ("point", C.POINTER(C.c_uint64)),
+                ("nvars", C.c_size_t), ("flags", C.c_uint32), ("_pad", C.c_uint32)]
+
+
 class KzgVk(C.Structure):
     _fields_ = [("g1_xy", C.c_uint64 * 8), ("g2_xy", C.c_uint64 * 16),
                 ("g2_tau_xy", C.c_uint64 * 16)]
@@ -111,6 +116,8 @@ PROTOTYPES = {
     "qg_mle_open_dev": (C.c_int, [P, P, P, SZ, U64P, SZ, U8P, C.POINTER(MleProof)]),
     "qg_mle_open_dev_ex": (C.c_int, [P, P, P, SZ, U64P, SZ, U8P, C.c_uint32,
                                      C.POINTER(MleProof)]),
+    "qg_mle_open_batch_dev": (C.c_int, [P, P, C.POINTER(MleOpenItem), SZ, U8P,
+                                        C.POINTER(MleProof)]),
     "qg_eq_table": (C.c_int, [P, U64P, SZ, U64P]),
     "qg_eq_table_dev": (C.c_int, [P, U64P, SZ, P]),
     "qg_s_polynomial": (C.c_int, [P, U64P, SZ, U64P, SZ, U64P]),

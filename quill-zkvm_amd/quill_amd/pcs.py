@@ -9,7 +9,7 @@ from dataclasses import dataclass
 
 import numpy as np
 
-from ._lib import KzgOpening, KzgVk, MleProof, QuillGpuError, check, lib
+from ._lib import KzgOpening, KzgVk, MleOpenItem, MleProof, QuillGpuError, check, lib
 from .device import Device, DeviceVec, Srs
 from .field import (fq_from_mont_limbs, fr_array, fr_c, fr_from_mont_limbs, g1_from_abi,
                     g1_to_abi, g2_from_abi, g2_to_abi, u64p)
@@ -255,6 +255,30 @@ class KZG:
                            g1_from_abi(out.s_comm_xy, out.s_comm_inf),
                            _opening(out.poly_opening), _opening(out.poly_opening_inv),
                            _opening(out.s_opening), _opening(out.s_opening_inv))
+
+    def open_batch_dev(self, items, transcript: Transcript) -> list:
+        """K openings [(vec, n, eval_point, unchanged), ...] in one call
+        (qg_mle_open_batch_dev): the same proofs and transcript as K successive
+        open_dev calls, with the S and quotient commitments as two MSM batches.
+        Sharded devices open item by item (each rank's shard SRS)."""
+        if self.dev.world > 1 or len(items) <= 1:
+            return [self.open_dev(v, n, pt, transcript, unch) for v, n, pt, unch in items]
+        k = len(items)
+        arr = (MleOpenItem * k)()
+        pts = []
+        for i, (vec, n, pt, unch) in enumerate(items):
+            a = fr_array(pt) if len(pt) else np.zeros((1, 4), dtype=np.uint64)
+            pts.append(a)  # kept alive through the call
+            arr[i] = MleOpenItem(vec.h.value, n, a.ctypes.data_as(C.POINTER(C.c_uint64)), len(pt),
+                                 1 if unch else 0, 0)
+        outs = (MleProof * k)()
+        check(lib().qg_mle_open_batch_dev(self.dev.h, self.srs.h, arr, k, transcript.c_state(),
+                                          outs), self.dev.h)
+        return [MLEvalProof(list(pt), fr_from_mont_limbs(list(o.evaluation)),
+                            g1_from_abi(o.s_comm_xy, o.s_comm_inf),
+                            _opening(o.poly_opening), _opening(o.poly_opening_inv),
+                            _opening(o.s_opening), _opening(o.s_opening_inv))
+                for (_, _, pt, _), o in zip(items, outs)]
 
     def open(self, poly, eval_point, transcript: Transcript,
              unchanged: bool = False) -> MLEvalProof:

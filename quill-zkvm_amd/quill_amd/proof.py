@@ -13,6 +13,7 @@ the C-ABI (qg_mle_verify)."""
 from __future__ import annotations
 
 import ctypes as C
+import os
 from dataclasses import dataclass, field
 
 import numpy as np
@@ -281,15 +282,27 @@ class HyperPlonk:
                                                      pk.permutation_poly, transcript, pcs)
 
         # `full` stays unchanged through these openings: its NTT transform is
-        # computed once (unchanged=True, qg_mle_open_dev_ex), proofs identical
-        open_zc = []
+        # computed once (unchanged=True, qg_mle_open_dev_ex), proofs identical.
+        # On one device they run as one batch (qg_mle_open_batch_dev: the same
+        # proofs and transcript, the S and quotient commitments as two MSM
+        # batches); QUILL_OPEN_BATCH=0 opens one by one.
+        items = []
         for col in range(cols):
             point = list(zclaim.point) + [(col >> i) & 1 for i in range(log2_cols)]
-            open_zc.append(pcs.open(full, point, transcript, unchanged=col > 0))
-        open_pub = [pcs.open(p, zclaim.point, transcript) for p in pk.public_rows]
-        o_id = pcs.open(pk.id_poly, ppoint, transcript)
-        o_perm = pcs.open(pk.permutation_poly, ppoint, transcript)
-        o_pt = pcs.open(full, ppoint, transcript, unchanged=True)
+            items.append((full, point, col > 0))
+        items += [(p, list(zclaim.point), False) for p in pk.public_rows]
+        items += [(pk.id_poly, list(ppoint), False), (pk.permutation_poly, list(ppoint), False),
+                  (full, list(ppoint), True)]
+        batch = (os.environ.get("QUILL_OPEN_BATCH", "1") != "0" and dev is not None
+                 and dev.world == 1 and all(isinstance(v, DeviceVec) for v, _, _ in items))
+        if batch:
+            opens = pcs.open_batch_dev([(v, len(v), pt, u) for v, pt, u in items], transcript)
+        else:
+            opens = [pcs.open(v, pt, transcript, unchanged=u) for v, pt, u in items]
+        npub = len(pk.public_rows)
+        open_zc = opens[:cols]
+        open_pub = opens[cols:cols + npub]
+        o_id, o_perm, o_pt = opens[cols + npub:]
         for p in store.polynomials[cols + len(pk.public_rows):]:
             p.close()  # eq table (zero-check)
         for p in store2.polynomials[3:]:

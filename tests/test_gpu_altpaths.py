@@ -5,8 +5,8 @@ for bit against the default path on the same inputs:
     tables at nvars >= 15 over 8 loopback ranks, ADVICE r3 medium);
   * k_logup_fused, the one-pass Logup column (QG_LOGUP_FUSED=1);
   * the replicated S polynomial in the sharded ML opening (QG_S_REPLICATED=1).
-  * an MSM batch's bucketing in stream order instead of on the side stream
-    (QG_MSM_PIPE=0).
+  * an MSM batch's bucketing on the side stream (QG_MSM_PIPE=1, opt-in)
+    instead of in stream order.
 The switches are read per call, so the tests toggle them in-process."""
 import contextlib
 import os
@@ -177,7 +177,7 @@ def test_side_stream_bucketing_matches_stream_order(dev, nv):
     vec = q.DeviceVec.from_list(dev, poly)
     point = [rnd.randrange(R) for _ in range(nv)]
     res = []
-    for pipe in ("1", "0"):
+    for pipe in ("1", "0"):  # (the side stream is opt-in: QG_MSM_PIPE=1)
         with env("QG_MSM_PIPE", pipe):
             t = Transcript(b"pipe")
             pr = kzg.open_dev(vec, N, point, t)

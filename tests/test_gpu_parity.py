@@ -533,3 +533,63 @@ def test_s_polynomial_size_cycle_keeps_twiddles_fresh(dev):
         for k in (0, nf // 3, nf - 2):
             exp = sum(f[i + k + 1] * gp[i] + gp[i + k + 1] * f[i] for i in range(nf - k - 1)) % R
             assert S[k] == exp, (nf, k)
+
+
+@pytest.mark.parametrize("seed", [0, 1])
+def test_mle_open_batch_matches_sequential_and_oracle(dev, seed):
+    """qg_mle_open_batch_dev: K openings with the S and quotient commitments
+    as two MSM batches and the transcript steps in item order.  Items of
+    different lengths and variable counts (n < 2^nv, n = 2^nv, n > 2^nv),
+    zero-tailed and zero vectors, one vector opened twice (the second with
+    QG_OPEN_UNCHANGED, as HyperPlonk opens its witness per column).  Every
+    proof and the final transcript state equal K successive open_dev calls,
+    and the oracle prover's (mlpcs.rs:83-124) on the same transcript."""
+    from quill_amd import KZG, DeviceVec, Transcript
+    rnd = random.Random(9100 + seed)
+    tau = rnd.randrange(R)
+    kzg = KZG.trusted_setup(1 << 9, tau, dev)
+    okzg = o.KZG(1 << 9, tau, points=[])
+    shapes = [(256, 8, 256), (200, 8, 120), (64, 6, 0), (300, 8, 300), (512, 9, 511), (32, 6, 32)]
+    polys, vecs, items = [], [], []
+    for n, nv, live in shapes:
+        p = [rnd.randrange(R) for _ in range(live)] + [0] * (n - live)
+        polys.append(p)
+        vecs.append(DeviceVec.from_list(dev, p))
+        items.append((len(polys) - 1, nv, False))
+    items.append((0, 8, True))  # vector 0 again, unchanged
+    pts = [[rnd.randrange(R) for _ in range(nv)] for _, nv, _ in items]
+    batch_in = [(vecs[i], len(polys[i]), pt, u) for (i, _, u), pt in zip(items, pts)]
+    tb = Transcript(b"open batch")
+    got = kzg.open_batch_dev(batch_in, tb)
+    ts = Transcript(b"open batch")
+    seq = [kzg.open_dev(v, n, pt, ts, unchanged=u) for v, n, pt, u in batch_in]
+    assert got == seq
+    assert tb.state == ts.state
+    ot = o.Transcript(b"open batch")
+    for (i, _, _), pt, proof in zip(items, pts, got):
+        ref = o.MLEvalProof.prove(polys[i], pt, okzg, ot)
+        assert proof.evaluation == ref.evaluation and proof.s_comm == ref.s_comm
+        for k in ("poly_opening", "poly_opening_inv", "s_opening", "s_opening_inv"):
+            op = getattr(proof, k)
+            assert (op.x, op.y, op.proof) == tuple(getattr(ref, k)), k
+    assert tb.state == ot.state
+    # a second batch on the same context: its first item reuses the length the
+    # first batch left remembered (vector 0, unchanged), its last one must not
+    # (vector 1 was opened in between), as with successive single openings
+    batch2 = [(vecs[0], len(polys[0]), pts[0], True), (vecs[1], len(polys[1]), pts[1], False),
+              (vecs[0], len(polys[0]), [rnd.randrange(R) for _ in range(8)], True)]
+    got2 = kzg.open_batch_dev(batch2, tb)
+    ts2 = Transcript(b"open batch 2")
+    tb2 = Transcript(b"open batch 2")
+    got2b = kzg.open_batch_dev(batch2, tb2)
+    seq2 = [kzg.open_dev(v, n, pt, ts2, unchanged=u) for v, n, pt, u in batch2]
+    assert got2b == seq2 and tb2.state == ts2.state
+    for (v, n, pt, _), proof in zip(batch2, got2):
+        ref = o.MLEvalProof.prove(polys[vecs.index(v)], pt, okzg, ot)
+        assert proof.evaluation == ref.evaluation
+        for k in ("poly_opening", "poly_opening_inv", "s_opening", "s_opening_inv"):
+            op = getattr(proof, k)
+            assert (op.x, op.y, op.proof) == tuple(getattr(ref, k)), k
+    assert tb.state == ot.state
+    for v in vecs:
+        v.close()
