@@ -1710,7 +1710,14 @@ static G1Affine msm_finish_ranks(qg_ctx* ctx, G1Xyzz acc) {
 // of four (profiles/r05_msm_pipe_ab.txt).  Not the default: in the batches of
 // 4K quotients of a batched opening (mle_open_batch_device) some commitments
 // came out wrong with it, intermittently (micro/open_batch_dbg.py, 2^14 rows;
-// profiles/r05_open_batch_ab.txt), and the cause is not found yet.  A lone
+// profiles/r05_open_batch_ab.txt).  Debug builds narrowed it: right only
+// when the host both drains ctx->stream before each bucketing and waits for
+// the bucketing before the accumulation is launched; wrong with either one
+// alone, i.e. with the event-ordered cross-stream hand-over of the entry
+// lists, or with a bucketing running beside another MSM's accumulation.  No
+// buffer is shared between the two in the code, so the suspect is the
+// visibility of one queue's writes to the other's kernels (8 XCD L2s); the
+// cause is not confirmed.  A lone
 // MSM split into pieces to get the same overlap is slower (2^24: 18.15 ->
 // 18.7 ms with 2 pieces: each piece pays its own bucket reduction, and the
 // accumulation slows by 0.85 ms under the second piece's bucketing).
