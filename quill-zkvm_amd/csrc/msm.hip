@@ -1717,7 +1717,8 @@ static G1Affine msm_finish_ranks(qg_ctx* ctx, G1Xyzz acc) {
 // lists, or with a bucketing running beside another MSM's accumulation.  No
 // buffer is shared between the two in the code, so the suspect is the
 // visibility of one queue's writes to the other's kernels (8 XCD L2s); the
-// cause is not confirmed.  A lone
+// cause is not confirmed (a blocking side stream, timing-free events and a
+// host synchronization before the batch change nothing).  A lone
 // MSM split into pieces to get the same overlap is slower (2^24: 18.15 ->
 // 18.7 ms with 2 pieces: each piece pays its own bucket reduction, and the
 // accumulation slows by 0.85 ms under the second piece's bucketing).
