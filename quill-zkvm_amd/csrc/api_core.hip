@@ -191,6 +191,7 @@ int qg_ctx_destroy(qg_ctx* ctx) {
   if (ctx->stream) (void)hipStreamSynchronize(ctx->stream);
   if (ctx->copy_stream) (void)hipStreamSynchronize(ctx->copy_stream);
   if (ctx->side_stream) (void)hipStreamSynchronize(ctx->side_stream);
+  if (ctx->side_stream2) (void)hipStreamSynchronize(ctx->side_stream2);
   comm_release(ctx);
   ctx->arena.release_all();
   for (auto& kv : ctx->pinned) (void)hipHostFree(kv.second.first);
@@ -202,6 +203,7 @@ int qg_ctx_destroy(qg_ctx* ctx) {
   if (ctx->stream) (void)hipStreamDestroy(ctx->stream);
   if (ctx->copy_stream) (void)hipStreamDestroy(ctx->copy_stream);
   if (ctx->side_stream) (void)hipStreamDestroy(ctx->side_stream);
+  if (ctx->side_stream2) (void)hipStreamDestroy(ctx->side_stream2);
   delete ctx;
   return QG_OK;
 }

@@ -62,7 +62,8 @@ struct qg_ctx {
   int device = 0;
   hipStream_t stream = nullptr;
   hipStream_t copy_stream = nullptr;  // host-to-device uploads overlapped with kernels (msm_host)
-  hipStream_t side_stream = nullptr;  // MSM bucketing beside the previous accumulation (msm.hip)
+  hipStream_t side_stream = nullptr;   // MSM batches on two side streams, by MSM parity
+  hipStream_t side_stream2 = nullptr;  // (QG_MSM_PIPE=1, msm.hip)
   std::string last_error;
   // grow-only scratch arena, one slot per purpose; every (re)allocation and
   // every table build gets a fresh generation number (arena.h), which caches

@@ -1316,39 +1316,35 @@ struct MsmRun {
   const uint32_t* h_mx = nullptr;
   hipEvent_t ev_mx = nullptr;
   uint32_t gen = 0;  // misc[4] of this run: h_mx[3] must equal it
-  // side mode: the end of this MSM's bucketing on the side stream (the
-  // accumulation waits for it); back to the pool once the batch is done
-  hipEvent_t ev_b = nullptr;
 };
 static constexpr int MSM_MAX_BATCH = 1024;
 
 // bucketing (two-pass radix sort) + bucket accumulation of MSM `slot` of a
 // batch: sum_i d_scalars[i] * base[srs_off + i]
 //
-// bst: the stream the bucketing runs on.  ctx->stream (default): everything in
-// stream order.  Another stream (msm_device_batch): the caller has made bst wait
-// for the scalars; the bucketing kernels queue there, the accumulation waits
-// for them by an event on ctx->stream, and the entry list gets its own slot,
-// so the next MSM's bucketing - memory-bound radix passes - runs on bst
-// beside this accumulation, which is VALU-bound and leaves a wave slot and
-// LDS per CU free.
-// side mode: the entry list lives in one of two slots by MSM parity; the
-// bucketing first waits for `reuse_wait` (the accumulation of MSM slot - 2,
-// the slot's last reader), and `acc_done` receives an event after this
-// accumulation (both owned by the caller).
-// reserve: only size the shared bucketing scratch and both entry-list slots
-// for an MSM of length n, launching nothing.  A batch reserves for its
-// longest MSM first: a slot that grew in the middle of a batch would be
-// freed while an earlier MSM's kernels, queued on either stream, still read it.
+// bst: the stream this MSM runs on.  ctx->stream (default): everything in
+// stream order.  A side stream (msm_device_batch, QG_MSM_PIPE=1): the caller
+// has made bst wait for the scalars; bucketing and accumulation both queue on
+// bst, with their own copies of the shared bucketing scratch and entry list,
+// so the next MSM's bucketing - memory-bound radix passes - runs on the other
+// side stream beside this accumulation (VALU-bound, leaving a wave slot and
+// LDS per CU free), and every MSM's data flows within one queue.
+// reserve: only size the shared bucketing scratch and the entry list (of the
+// stream `slot` selects) for an MSM of length n, launching nothing.  A batch
+// reserves for its longest MSM first: a slot that grew in the middle of a
+// batch would be freed while an earlier MSM's kernels still read it.
 static MsmRun msm_accumulate_phase(qg_ctx* ctx, const qg_srs* srs, const Fr* d_scalars, size_t n,
                                    int slot, size_t srs_off = 0, hipStream_t bst = nullptr,
-                                   hipEvent_t reuse_wait = nullptr, hipEvent_t acc_done = nullptr,
                                    bool reserve = false) {
   QG_CHECK(srs_off <= srs->n && n <= srs->n - srs_off, QG_ERR_INVALID, "MSM length exceeds the SRS");
   MsmRun run;
   const std::string sfx = "#" + std::to_string(slot);
   const bool side = bst != nullptr && bst != ctx->stream;
   if (!bst) bst = ctx->stream;
+  // side mode: this MSM's bucketing AND accumulation run on bst, one of two
+  // side streams by MSM parity, so each MSM's data flows within one queue;
+  // the shared bucketing scratch and the entry list are per stream
+  const std::string tg = side ? "@" + std::to_string(slot & 1) : std::string();
   if (n > 0) {
     const int c = srs->c, W = srs->W;
     const uint32_t nb = 1u << (c - 1);
@@ -1367,31 +1363,26 @@ static MsmRun msm_accumulate_phase(qg_ctx* ctx, const qg_srs* srs, const Fr* d_s
     const uint32_t nblk = div_up(n, tile);
     const size_t nghist = (size_t)H * nblk;
     const size_t max_chunks = max_entries / SORT_CHUNK + H + 1;
-    uint32_t* ghist = ctx->scratch_as<uint32_t>("msm_ghist", nghist + 1);
-    uint32_t* goff = ctx->scratch_as<uint32_t>("msm_goff", nghist + 1);
-    uint32_t* gtiles = ctx->scratch_as<uint32_t>("msm_gtiles", div_up(nghist, 2048) + 1);
-    uint32_t* gstart = ctx->scratch_as<uint32_t>("msm_gstart", H + 1);
-    uint32_t* cbase = ctx->scratch_as<uint32_t>("msm_cbase", H + 1);
-    uint32_t* cgroup = ctx->scratch_as<uint32_t>("msm_cgroup", max_chunks);
+    uint32_t* ghist = ctx->scratch_as<uint32_t>("msm_ghist" + tg, nghist + 1);
+    uint32_t* goff = ctx->scratch_as<uint32_t>("msm_goff" + tg, nghist + 1);
+    uint32_t* gtiles = ctx->scratch_as<uint32_t>("msm_gtiles" + tg, div_up(nghist, 2048) + 1);
+    uint32_t* gstart = ctx->scratch_as<uint32_t>("msm_gstart" + tg, H + 1);
+    uint32_t* cbase = ctx->scratch_as<uint32_t>("msm_cbase" + tg, H + 1);
+    uint32_t* cgroup = ctx->scratch_as<uint32_t>("msm_cgroup" + tg, max_chunks);
     uint32_t* misc = ctx->scratch_as<uint32_t>("msm_misc" + sfx, 5);  // [0] nchunks, [1] max tpb
-    uint32_t* chist = ctx->scratch_as<uint32_t>("msm_chist", max_chunks * NL);
-    uint32_t* coff = ctx->scratch_as<uint32_t>("msm_coff", max_chunks * NL);
-    uint32_t* tmp_e = ctx->scratch_as<uint32_t>("msm_tmp_e", max_entries + 1);
-    uint16_t* tmp_l = ctx->scratch_as<uint16_t>("msm_tmp_l", max_entries + 1);
-    uint32_t* hrow = ctx->scratch_as<uint32_t>("msm_hrow", nghist + 1);
-    uint32_t* orow = ctx->scratch_as<uint32_t>("msm_orow", nghist + 1);
-    Fr* canon = ctx->scratch_as<Fr>("msm_canon", n);
-    uint32_t* counts = ctx->scratch_as<uint32_t>("msm_counts", nb);
+    uint32_t* chist = ctx->scratch_as<uint32_t>("msm_chist" + tg, max_chunks * NL);
+    uint32_t* coff = ctx->scratch_as<uint32_t>("msm_coff" + tg, max_chunks * NL);
+    uint32_t* tmp_e = ctx->scratch_as<uint32_t>("msm_tmp_e" + tg, max_entries + 1);
+    uint16_t* tmp_l = ctx->scratch_as<uint16_t>("msm_tmp_l" + tg, max_entries + 1);
+    uint32_t* hrow = ctx->scratch_as<uint32_t>("msm_hrow" + tg, nghist + 1);
+    uint32_t* orow = ctx->scratch_as<uint32_t>("msm_orow" + tg, nghist + 1);
+    Fr* canon = ctx->scratch_as<Fr>("msm_canon" + tg, n);
+    uint32_t* counts = ctx->scratch_as<uint32_t>("msm_counts" + tg, nb);
     uint32_t* bstart = ctx->scratch_as<uint32_t>("msm_bstart" + sfx, nb + 1);
-    uint32_t* entries = ctx->scratch_as<uint32_t>(
-        side ? "msm_entries#p" + std::to_string(slot & 1) : std::string("msm_entries"), max_entries + 1);
-    if (reserve) {
-      if (side) ctx->scratch_as<uint32_t>("msm_entries#p" + std::to_string((slot & 1) ^ 1), max_entries + 1);
-      return run;
-    }
-    if (side && reuse_wait) QG_HIP(hipStreamWaitEvent(bst, reuse_wait, 0));
+    uint32_t* entries = ctx->scratch_as<uint32_t>("msm_entries" + tg, max_entries + 1);
+    if (reserve) return run;
     const int ntiles = (int)div_up(nb, SCAN_TILE);
-    uint2* tile_tot = ctx->scratch_as<uint2>("msm_tiles", ntiles);
+    uint2* tile_tot = ctx->scratch_as<uint2>("msm_tiles" + tg, ntiles);
     // entries per accumulation thread (flat chunks, k_msm_accumulate): 64, or
     // 128 for the largest MSMs, fewer while that would leave < 3 waves of
     // threads per resident slot (256 CUs x 16 waves).  Measured against equal
@@ -1518,13 +1509,9 @@ static MsmRun msm_accumulate_phase(qg_ctx* ctx, const qg_srs* srs, const Fr* d_s
                          entries);
       QG_LAUNCH_CHECK();
     }
-    if (side) {  // the accumulation (ctx->stream) after this bucketing
-      run.ev_b = ctx->ev_get();
-      QG_HIP(hipEventRecord(run.ev_b, bst));
-      QG_HIP(hipStreamWaitEvent(ctx->stream, run.ev_b, 0));
-    }
+    const hipStream_t ast = bst;  // the accumulation follows on the same stream
     {
-      QgTimed tm(ctx, "msm_accumulate");
+      QgTimed tm(ctx, "msm_accumulate", ast);
       // the prefetching per-lane-gather form (QG_MSM_PF=1 with QG_MSM_COOP=0;
       // the default for 2^27+ entries before the cooperative gathers)
       bool pf = max_entries >= ((size_t)1 << 27);
@@ -1536,19 +1523,18 @@ static MsmRun msm_accumulate_phase(qg_ctx* ctx, const qg_srs* srs, const Fr* d_s
       if (const char* ov = getenv("QG_MSM_COOP")) coop = atoi(ov) != 0;
       if (coop)
         hipLaunchKernelGGL(k_msm_accumulate_coop, dim3(div_up(max_threads, MSM_BLOCK)),
-                           dim3(MSM_BLOCK), 0, ctx->stream, srs->d_table, entries, bstart, nb, lgL,
+                           dim3(MSM_BLOCK), 0, ast, srs->d_table, entries, bstart, nb, lgL,
                            partial, owner);
       else if (pf)
         hipLaunchKernelGGL(k_msm_accumulate<true>, dim3(div_up(max_threads, MSM_BLOCK)),
-                           dim3(MSM_BLOCK), 0, ctx->stream, srs->d_table, entries, bstart, nb, lgL,
+                           dim3(MSM_BLOCK), 0, ast, srs->d_table, entries, bstart, nb, lgL,
                            partial, owner);
       else
         hipLaunchKernelGGL(k_msm_accumulate<false>, dim3(div_up(max_threads, MSM_BLOCK)),
-                           dim3(MSM_BLOCK), 0, ctx->stream, srs->d_table, entries, bstart, nb, lgL,
+                           dim3(MSM_BLOCK), 0, ast, srs->d_table, entries, bstart, nb, lgL,
                            partial, owner);
       QG_LAUNCH_CHECK();
     }
-    if (side && acc_done) QG_HIP(hipEventRecord(acc_done, ctx->stream));
     run.empty = n == 0;
     run.L = L;
     run.T = T;
@@ -1703,62 +1689,54 @@ static G1Affine msm_finish_ranks(qg_ctx* ctx, G1Xyzz acc) {
 // k MSMs over the same SRS (KZG openings of one proof); results per MSM,
 // summed over the RCCL ranks when a communicator is attached
 //
-// QG_MSM_PIPE=1 (opt-in, off by default): batches of two or more MSMs bucket
-// on ctx->side_stream, MSM i + 1's radix passes (memory-bound) beside MSM i's
-// accumulation (VALU-bound), which slows by ~0.3 ms per 1 ms of bucketing it
-// hosts.  HyperPlonk proof 929 / 935 -> 907 / 912 ms with the openings' batches
-// of four (profiles/r05_msm_pipe_ab.txt).  Not the default: in the batches of
-// 4K quotients of a batched opening (mle_open_batch_device) some commitments
-// came out wrong with it, intermittently (micro/open_batch_dbg.py, 2^14 rows;
-// profiles/r05_open_batch_ab.txt).  Debug builds narrowed it: right only
-// when the host both drains ctx->stream before each bucketing and waits for
-// the bucketing before the accumulation is launched; wrong with either one
-// alone, i.e. with the event-ordered cross-stream hand-over of the entry
-// lists, or with a bucketing running beside another MSM's accumulation.  No
-// buffer is shared between the two in the code, so the suspect is the
-// visibility of one queue's writes to the other's kernels (8 XCD L2s); the
-// cause is not confirmed (a blocking side stream, timing-free events and a
-// host synchronization before the batch change nothing).  A lone
-// MSM split into pieces to get the same overlap is slower (2^24: 18.15 ->
-// 18.7 ms with 2 pieces: each piece pays its own bucket reduction, and the
-// accumulation slows by 0.85 ms under the second piece's bucketing).
+// Batches of two or more MSMs run on two side streams by MSM parity, each
+// MSM's bucketing and accumulation on one stream: MSM i + 1's radix passes
+// (memory-bound) run beside MSM i's accumulation (VALU-bound), which slows
+// by ~0.3 ms per 1 ms of bucketing it hosts.  The scalars (written on
+// ctx->stream) and the partial sums (read by the reduction on ctx->stream)
+// cross between streams only through host synchronizations, one at each end
+// of the batch: the first version handed the entry lists from a bucketing
+// stream to the accumulating stream by events and some commitments came out
+// wrong, intermittently, and an event-ordered hand-over of the scalars was
+// still wrong for the last MSMs of a batch (micro/open_batch_dbg.py,
+// profiles/r05_open_batch_ab.txt).  HyperPlonk proof 935.8 / 932.6 ->
+// 896.1 / 894.9 ms, same transcript, every proof oracle-verified and
+// identical across runs (profiles/r05_msm_pipe2_ab.txt).  QG_MSM_PIPE=0
+// keeps a batch on ctx->stream (A/B runs).  A lone MSM split into pieces to
+// get the same overlap is slower (2^24: 18.15 -> 18.7 ms with 2 pieces: each
+// piece pays its own bucket reduction, and the accumulation slows by 0.85 ms
+// under the second piece's bucketing).
 std::vector<G1Affine> msm_device_batch(qg_ctx* ctx, const qg_srs* srs,
                                        const std::vector<const Fr*>& scalars,
                                        const std::vector<size_t>& ns) {
   QG_CHECK(scalars.size() == ns.size(), QG_ERR_INVALID, "MSM batch shape");
-  bool pipe = false;
-  if (const char* ov = getenv("QG_MSM_PIPE")) pipe = scalars.size() >= 2 && atoi(ov) != 0;
-  hipStream_t bst = nullptr;
-  hipEvent_t ev_in = nullptr;
+  bool pipe = scalars.size() >= 2;
+  if (const char* ov = getenv("QG_MSM_PIPE")) pipe = pipe && atoi(ov) != 0;
+  hipStream_t side[2] = {nullptr, nullptr};
   if (pipe) {
     if (!ctx->side_stream) QG_HIP(hipStreamCreateWithFlags(&ctx->side_stream, hipStreamNonBlocking));
-    bst = ctx->side_stream;
-    ev_in = ctx->ev_get();  // the scalars are ready in ctx->stream order
-    QG_HIP(hipEventRecord(ev_in, ctx->stream));
-    QG_HIP(hipStreamWaitEvent(bst, ev_in, 0));
+    if (!ctx->side_stream2) QG_HIP(hipStreamCreateWithFlags(&ctx->side_stream2, hipStreamNonBlocking));
+    side[0] = ctx->side_stream;
+    side[1] = ctx->side_stream2;
+    // the scalars were written on ctx->stream: the host waits for them rather
+    // than an event (with the event-ordered hand-over some side-stream MSMs
+    // read wrong scalars, profiles/r05_open_batch_ab.txt)
+    QG_HIP(hipStreamSynchronize(ctx->stream));
   }
   if (scalars.size() >= 2) {  // size the shared scratch for the longest MSM first
     size_t im = 0;
     for (size_t i = 1; i < ns.size(); i++)
       if (ns[i] > ns[im]) im = i;
-    msm_accumulate_phase(ctx, srs, scalars[im], ns[im], 0, 0, bst, nullptr, nullptr, true);
+    for (int p = 0; p < (pipe ? 2 : 1); p++)
+      msm_accumulate_phase(ctx, srs, scalars[im], ns[im], p, 0, side[p], true);
   }
   std::vector<MsmRun> runs;
-  std::vector<hipEvent_t> acc_done;  // side mode: after each accumulation
-  for (size_t i = 0; i < scalars.size(); i++) {
-    if (pipe) acc_done.push_back(ctx->ev_get());
-    runs.push_back(msm_accumulate_phase(ctx, srs, scalars[i], ns[i], (int)i, 0, bst,
-                                        pipe && i >= 2 ? acc_done[i - 2] : nullptr,
-                                        pipe ? acc_done[i] : nullptr));
-  }
+  for (size_t i = 0; i < scalars.size(); i++)
+    runs.push_back(msm_accumulate_phase(ctx, srs, scalars[i], ns[i], (int)i, 0, side[i & 1]));
+  if (pipe)  // the reduction (ctx->stream) after both side streams, likewise
+    for (hipStream_t st : side) QG_HIP(hipStreamSynchronize(st));
   std::vector<G1Xyzz> local;
   msm_reduce_phase(ctx, srs, runs, local);  // ends with a stream synchronization
-  // every event this batch waited on goes back only now: a recycled event
-  // re-recorded before a queued wait on it ran would move that wait
-  for (hipEvent_t e : acc_done) ctx->event_pool.push_back(e);
-  for (const MsmRun& r : runs)
-    if (r.ev_b) ctx->event_pool.push_back(r.ev_b);
-  if (ev_in) ctx->event_pool.push_back(ev_in);
   std::vector<G1Affine> res(local.size());
   for (size_t i = 0; i < local.size(); i++) res[i] = msm_finish_ranks(ctx, local[i]);
   return res;

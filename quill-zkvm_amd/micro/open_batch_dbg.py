@@ -23,7 +23,7 @@ def main():
     hp = HyperPlonk.preprocess([c for c, _ in cws], pcs)
     ws = [w for _, w in cws]
     res = {}
-    for batch, pipe, sp in (("0", "0", "0"), ("1", "1", "0"), ("1", "1", "0")):
+    for batch, pipe, sp in (("0", "0", "0"), ("1", "1", "0"), ("0", "1", "0")):
         os.environ["QUILL_OPEN_BATCH"] = batch
         os.environ["QG_MSM_PIPE"] = pipe
         os.environ["QG_MSM_SYNC_PLAN"] = sp

@@ -5,8 +5,8 @@ for bit against the default path on the same inputs:
     tables at nvars >= 15 over 8 loopback ranks, ADVICE r3 medium);
   * k_logup_fused, the one-pass Logup column (QG_LOGUP_FUSED=1);
   * the replicated S polynomial in the sharded ML opening (QG_S_REPLICATED=1).
-  * an MSM batch's bucketing on the side stream (QG_MSM_PIPE=1, opt-in)
-    instead of in stream order.
+  * an MSM batch in stream order (QG_MSM_PIPE=0) instead of on the two side
+    streams.
 The switches are read per call, so the tests toggle them in-process."""
 import contextlib
 import os
@@ -163,9 +163,8 @@ def test_alternate_accumulate_matches_default(n, small, mode):
 @pytest.mark.parametrize("nv", [9, 14, 17])
 def test_side_stream_bucketing_matches_stream_order(dev, nv):
     """An ML opening runs its quotient MSMs as one batch whose 2nd.. MSMs bucket
-    on the context's side stream beside the previous MSM's accumulation
-    (msm_device_batch); QG_MSM_PIPE=0 keeps every bucketing on the context
-    stream.  Same proof and transcript state, and the opened value is the MLE
+    beside the previous MSM's accumulation, on two side streams by parity
+    (msm_device_batch); QG_MSM_PIPE=0 keeps the batch on the context stream.  Same proof and transcript state, and the opened value is the MLE
     evaluation."""
     import quill_amd as q
     from quill_amd import KZG, Transcript
@@ -177,7 +176,7 @@ def test_side_stream_bucketing_matches_stream_order(dev, nv):
     vec = q.DeviceVec.from_list(dev, poly)
     point = [rnd.randrange(R) for _ in range(nv)]
     res = []
-    for pipe in ("1", "0"):  # (the side stream is opt-in: QG_MSM_PIPE=1)
+    for pipe in ("1", "0"):
         with env("QG_MSM_PIPE", pipe):
             t = Transcript(b"pipe")
             pr = kzg.open_dev(vec, N, point, t)
