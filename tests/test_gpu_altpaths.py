@@ -164,7 +164,8 @@ def test_alternate_accumulate_matches_default(n, small, mode):
 def test_side_stream_bucketing_matches_stream_order(dev, nv):
     """An ML opening runs its quotient MSMs as one batch whose 2nd.. MSMs bucket
     beside the previous MSM's accumulation, on two side streams by parity
-    (msm_device_batch); QG_MSM_PIPE=0 keeps the batch on the context stream.  Same proof and transcript state, and the opened value is the MLE
+    (msm_device_batch); QG_MSM_PIPE=0 keeps the batch on the context stream.
+    Same proof and transcript state, and the opened value is the MLE
     evaluation."""
     import quill_amd as q
     from quill_amd import KZG, Transcript
