@@ -764,9 +764,9 @@ def bench_logup(q, dev, args, barrier_sync, max_over_ranks, rank=0, world=1, tra
 
 LOGUP_MULS_PER_ROW = 8.6
 
-# msm_bucketing_side: the bucketing of the 2nd.. MSM of a batch, timed as its
-# span on the side stream beside the previous MSM's accumulation (overlapped:
-# not additive with the other phases)
+# msm_bucketing_side: the bucketing of the MSMs of a batch, which run on two
+# side streams by parity; it and msm_accumulate are per-stream spans that
+# overlap (a bucketing beside the other stream's accumulation): not additive
 HP_PHASES = ("msm_bucketing", "msm_bucketing_side", "msm_accumulate", "msm_reduce",
              "sumcheck_round", "sumcheck_tail", "logup_column", "eq_table", "inner_product",
              "s_polynomial", "kzg_division")
