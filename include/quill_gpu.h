@@ -413,7 +413,10 @@ int qg_ctx_kernel_time(const qg_ctx* ctx, const char* name, double* total_ms, ui
 int qg_trace_marker(qg_ctx* ctx, uint32_t tag);
 /* Diagnostic counters of the context by name; unknown names give 0.
  * "msm_plan_refetch": MSM bucket-scan plan copies (pinned, event-ordered) that
- * did not carry their run's generation tag and were re-read synchronously. */
+ * did not carry their run's generation tag and were re-read synchronously.
+ * "msm_handover_violation": MSM batches whose event-ordered hand-over between
+ * the context stream and the side streams the device guard found unordered
+ * (each was recomputed in stream order; 0 while the event ordering holds). */
 int qg_ctx_counter(const qg_ctx* ctx, const char* name, uint64_t* value);
 /* Self-test of the binary-GCD field inversion the Logup column uses per block
  * (csrc/bingcd.h): out[i] = in[i]^-1 (plain canonical integers, 4 x u64 LE;

@@ -169,6 +169,8 @@ int qg_ctx_create(int device, qg_ctx** out) {
   if (!out) return QG_ERR_INVALID;
   *out = nullptr;
   qg_ctx* ctx = new qg_ctx();
+  ctx->arena.backend.drain = &qg_ctx::drain_streams;
+  ctx->arena.backend.owner = ctx;
   int rc = qg_guard(ctx, [&] {
     int ndev = 0;
     QG_HIP(hipGetDeviceCount(&ndev));
@@ -193,7 +195,10 @@ int qg_ctx_destroy(qg_ctx* ctx) {
   if (ctx->side_stream) (void)hipStreamSynchronize(ctx->side_stream);
   if (ctx->side_stream2) (void)hipStreamSynchronize(ctx->side_stream2);
   comm_release(ctx);
-  ctx->arena.release_all();
+  try {
+    ctx->arena.release_all();
+  } catch (...) {  // destroy frees what it can; errors were reported by the calls before
+  }
   for (auto& kv : ctx->pinned) (void)hipHostFree(kv.second.first);
   for (auto& kv : ctx->pending) {
     (void)hipEventDestroy(kv.second.a);
@@ -227,7 +232,10 @@ int qg_ctx_kernel_time(const qg_ctx* ctx, const char* name, double* total_ms, ui
 
 int qg_ctx_counter(const qg_ctx* ctx, const char* name, uint64_t* value) {
   if (!ctx || !name || !value) return QG_ERR_INVALID;
-  *value = std::string(name) == "msm_plan_refetch" ? ctx->msm_plan_refetch : 0;
+  const std::string n(name);
+  *value = n == "msm_plan_refetch"         ? ctx->msm_plan_refetch
+           : n == "msm_handover_violation" ? ctx->msm_handover_violation
+                                           : 0;
   return QG_OK;
 }
 

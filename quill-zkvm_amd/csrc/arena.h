@@ -32,17 +32,18 @@ struct ScratchArena {
   std::map<std::string, uint64_t> stamps;
   std::map<std::string, std::string> memo;
   uint64_t counter = 0;
+  Backend backend;  // alloc / release (the device backend drains its context's streams)
 
   // the slot's buffer, (re)allocated when absent or smaller than `bytes`
   void* get(const std::string& slot, size_t bytes) {
     auto it = slots.find(slot);
     if (it != slots.end() && it->second.bytes >= bytes) return it->second.p;
     if (it != slots.end()) {
-      Backend::release(it->second.p);
+      backend.release(it->second.p);
       slots.erase(it);
     }
     const size_t b = bytes ? bytes : 16;
-    void* p = Backend::alloc(b);
+    void* p = backend.alloc(b);
     slots[slot] = Slot{p, b, ++counter};
     return p;
   }
@@ -61,16 +62,21 @@ struct ScratchArena {
   static std::string derived_key(const std::string& params, uint64_t src_stamp, uint64_t own_gen) {
     return params + "|s" + std::to_string(src_stamp) + "|g" + std::to_string(own_gen);
   }
-  // true when memo[tag] == key; otherwise records key and returns false (the
-  // caller rebuilds).  A source never stamped (0) is never valid.
-  bool check_or_set(const std::string& tag, const std::string& key, uint64_t src_stamp = 1) {
-    std::string& m = memo[tag];
-    if (src_stamp != 0 && m == key) return true;
-    m = key;
+  // true when memo[tag] == key (the table behind tag is valid).  A source
+  // never stamped (0) is never valid.  On false the caller rebuilds and then
+  // calls commit(tag, key) - only once the build's launches succeeded, so a
+  // build that throws leaves the memo invalid - and a stale memo
+  // is cleared here first, so a failed rebuild can never match it later.
+  bool check(const std::string& tag, const std::string& key, uint64_t src_stamp = 1) {
+    auto it = memo.find(tag);
+    if (it == memo.end()) return false;
+    if (src_stamp != 0 && it->second == key) return true;
+    memo.erase(it);
     return false;
   }
+  void commit(const std::string& tag, const std::string& key) { memo[tag] = key; }
   void release_all() {
-    for (auto& kv : slots) Backend::release(kv.second.p);
+    for (auto& kv : slots) backend.release(kv.second.p);
     slots.clear();
   }
 };

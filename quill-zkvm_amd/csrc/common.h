@@ -40,17 +40,23 @@ inline unsigned div_up(size_t a, size_t b) { return (unsigned)((a + b - 1) / b);
 
 // device-memory backend of the scratch arena (arena.h)
 struct HipAlloc {
+  // a slot that grows is released while kernels queued on the context's
+  // streams (the MSM batch's side streams included) may still read it: the
+  // owning context drains exactly those streams (not the device: loopback
+  // ranks share it), and a failure surfaces as an error
+  void (*drain)(void* owner) = nullptr;
+  void* owner = nullptr;
   static void* alloc(size_t b) {
     void* p = nullptr;
     QG_HIP(hipMalloc(&p, b));
     return p;
   }
-  // a slot that grows is released while kernels queued on any of the
-  // context's streams (the MSM batch's side stream included) may still read
-  // it: drain the device first
-  static void release(void* p) {
-    (void)hipDeviceSynchronize();
-    (void)hipFree(p);
+  void release(void* p) {
+    if (drain)
+      drain(owner);
+    else
+      QG_HIP(hipDeviceSynchronize());
+    QG_HIP(hipFree(p));
   }
 };
 
@@ -68,7 +74,7 @@ struct qg_ctx {
   // grow-only scratch arena, one slot per purpose; every (re)allocation and
   // every table build gets a fresh generation number (arena.h), which caches
   // key on instead of device addresses
-  qg::ScratchArena<qg::HipAlloc> arena;
+  qg::ScratchArena<qg::HipAlloc> arena;  // backend.drain = drain_streams (qg_ctx_create)
   qg::LruSlots<4> twm_lru;  // S polynomial: w^{j(M-1)} tables per (logn, M)
   // timing
   bool timing = false;
@@ -96,6 +102,18 @@ struct qg_ctx {
   // ordering holds)
   uint32_t msm_gen = 0;
   uint64_t msm_plan_refetch = 0;
+  // MSM batches whose event-ordered cross-stream hand-over the device guard
+  // found unordered (recomputed in stream order; msm.hip, msm_device_batch)
+  uint64_t msm_handover_violation = 0;
+  // trim_launch's call generation (mlpcs.hip: the tail launch's stamp)
+  uint64_t trim_gen = 0;
+
+  // every stream of this context, synchronized (scratch release, destroy)
+  static void drain_streams(void* self) {
+    qg_ctx* c = static_cast<qg_ctx*>(self);
+    for (hipStream_t s : {c->stream, c->copy_stream, c->side_stream, c->side_stream2})
+      if (s) QG_HIP(hipStreamSynchronize(s));
+  }
 
   int cus = 0;  // compute units of `device` (cached)
   int num_cus() {

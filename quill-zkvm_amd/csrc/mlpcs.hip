@@ -454,10 +454,11 @@ static const Fr* ntt_pyramid(qg_ctx* ctx, const Fr* flat, const std::string& src
   Fr* pyr = ctx->scratch_as<Fr>(tag, std::max<size_t>(1, n - 1));
   const uint64_t st = ctx->arena.stamp(src);
   const std::string key = ctx->arena.derived_key(std::to_string(logn), st, ctx->scratch_gen(tag));
-  if (!ctx->arena.check_or_set(tag, key, st)) {
+  if (!ctx->arena.check(tag, key, st)) {
     hipLaunchKernelGGL(k_tw_pyramid, dim3(div_up(n, 256)), dim3(256), 0, ctx->stream, flat, logn,
                        pyr);
     QG_LAUNCH_CHECK();
+    ctx->arena.commit(tag, key);
   }
   return pyr;
 }
@@ -576,7 +577,7 @@ static void ntt_twiddles(qg_ctx* ctx, int logn, Fr** tw, Fr** twi,
   *twi = ctx->scratch_as<Fr>(tag + "i", h);
   const std::string key = std::to_string(logn) + "|g" + std::to_string(ctx->scratch_gen(tag)) +
                           "," + std::to_string(ctx->scratch_gen(tag + "i"));
-  if (ctx->arena.check_or_set(tag, key)) return;
+  if (ctx->arena.check(tag, key)) return;
   const Fr w = root_of_unity(logn), wi = finv(w);
   const int K = 64;
   const L9 c = F29P<FrP>::TO261;
@@ -592,6 +593,7 @@ static void ntt_twiddles(qg_ctx* ctx, int logn, Fr** tw, Fr** twi,
   QG_LAUNCH_CHECK();
   ctx->arena.bump(tag);
   ctx->arena.bump(tag + "i");
+  ctx->arena.commit(tag, key);
 }
 
 // Transform of the eq table without an NTT.  g = eq(., z) over nz variables is
@@ -665,10 +667,11 @@ static const Fr* ntt_tw_bitrev(qg_ctx* ctx, const Fr* tw, const std::string& src
   Fr* twb = ctx->scratch_as<Fr>(tag, h);
   const uint64_t st = ctx->arena.stamp(src);
   const std::string key = ctx->arena.derived_key(std::to_string(logn), st, ctx->scratch_gen(tag));
-  if (!ctx->arena.check_or_set(tag, key, st)) {
+  if (!ctx->arena.check(tag, key, st)) {
     hipLaunchKernelGGL(k_tw_bitrev, dim3(div_up(h, 256)), dim3(256), 0, ctx->stream, tw, logn, h,
                        twb);
     QG_LAUNCH_CHECK();
+    ctx->arena.commit(tag, key);
   }
   return twb;
 }
@@ -714,7 +717,7 @@ static void s_poly_device(qg_ctx* ctx, const Fr* f, size_t nf, const Fr* g, size
   Fr *tw, *twi;
   ntt_twiddles(ctx, logn, &tw, &twi);
   const std::string twm_memo = ctx->arena.derived_key(twm_key, 1, ctx->scratch_gen(twm_slot));
-  if (!ctx->arena.check_or_set(twm_slot, twm_memo)) {
+  if (!ctx->arena.check(twm_slot, twm_memo)) {
     const Fr w = root_of_unity(logn);
     const Fr wM = fpow_small(w, (uint64_t)(M - 1));
     const int K = 64;
@@ -731,6 +734,7 @@ static void s_poly_device(qg_ctx* ctx, const Fr* f, size_t nf, const Fr* g, size
     hipLaunchKernelGGL(k_fr_to261_br, dim3(div_up(n, 256)), dim3(256), 0, ctx->stream, H, logn, c9,
                        twM);
     QG_LAUNCH_CHECK();
+    ctx->arena.commit(twm_slot, twm_memo);
   }
   // forward DIF of f and g (zero-extended), bit-reversed outputs
   const std::string fkey =
@@ -795,14 +799,30 @@ static void s_poly_device(qg_ctx* ctx, const Fr* f, size_t nf, const Fr* g, size
 
 // highest nonzero index + 1: per-thread max over a grid-stride range of
 // [lo, hi), wave max by shuffles, one atomic per wave (a contended atomic per
-// element cost 0.75 ms at 2^22).  With skip set, a block whose start finds
-// *out already nonzero exits: the tail launch covered the higher indices, so
-// any body index is below the answer (a full body scan at 2^23 is 110 us;
-// most vectors end in a nonzero value).
+// element cost 0.75 ms at 2^22) into *out.  The tail launch (the last 16K
+// entries) also stamps *tail with (call generation << 40 | its max); the body
+// launch skips a block when *tail holds this call's generation and a nonzero
+// max: the tail covered the higher indices, so any body index is below the
+// answer (a full body scan at 2^23 is 110 us; most vectors end in a nonzero
+// value).
+//
+// Round 6: the skip used to read *out itself, which the body launch's own
+// blocks write: a block that started after another block of the same launch
+// had posted its maximum exited without scanning its range, so the length
+// came out short (81152 or 81664 instead of 81920 for HyperPlonk's trimmed
+// full witness at 2^14 rows, whose tail is zero) whenever the launch's blocks
+// did not all start before the first one finished - timing-dependent, seen
+// with the MSM batches' side streams active (micro/handover_dbg.py,
+// profiles/r06_handover_diagnosis.txt).  A short length gives a wrong
+// quotient, so a wrong KZG opening proof; no opening proof enters the
+// transcript, so only a verifier or a proof-by-proof comparison sees it.
 __global__ void __launch_bounds__(256)
-    k_last_nonzero(const Fr* __restrict__ a, size_t lo, size_t hi, int skip,
-                   unsigned long long* out) {
-  if (skip && __hip_atomic_load(out, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT)) return;
+    k_last_nonzero(const Fr* __restrict__ a, size_t lo, size_t hi, unsigned long long* tail,
+                   uint64_t gen, int body, unsigned long long* out) {
+  if (body) {
+    const unsigned long long t = __hip_atomic_load(tail, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+    if ((t >> 40) == gen && (t & ((1ull << 40) - 1)) != 0) return;
+  }
   unsigned long long m = 0;
   for (size_t i = lo + (size_t)blockIdx.x * blockDim.x + threadIdx.x; i < hi;
        i += (size_t)gridDim.x * blockDim.x)
@@ -811,7 +831,10 @@ __global__ void __launch_bounds__(256)
     const unsigned long long o = __shfl_xor(m, k, 64);
     m = o > m ? o : m;
   }
-  if ((threadIdx.x & 63) == 0 && m) atomicMax(out, m);
+  if ((threadIdx.x & 63) == 0) {
+    if (m) atomicMax(out, m);
+    if (!body) atomicMax(tail, (gen << 40) | m);  // this call's stamp, even when m = 0
+  }
 }
 
 // trimmed length of a device vector: the last 16K entries first (8 blocks),
@@ -821,13 +844,18 @@ static void trim_launch(qg_ctx* ctx, const Fr* a, size_t n, unsigned long long* 
   if (n == 0) return;
   constexpr size_t TAIL = 16384;
   const size_t body = n > TAIL ? n - TAIL : 0;
+  // one stamp word per context, reused in stream order; generations only grow,
+  // so a stamp of an earlier call never matches (a wrapped counter only costs
+  // the skip)
+  unsigned long long* tail = ctx->scratch_as<unsigned long long>("trim_tail", 1);
+  const uint64_t gen = (++ctx->trim_gen) & 0xffffffull;
   hipLaunchKernelGGL(k_last_nonzero, dim3((unsigned)std::min<size_t>(8, div_up(n - body, 256))),
-                     dim3(256), 0, ctx->stream, a, body, n, 0, d);
+                     dim3(256), 0, ctx->stream, a, body, n, tail, gen, 0, d);
   QG_LAUNCH_CHECK();
   if (body) {
     const unsigned blocks = (unsigned)std::min<size_t>(2048, div_up(body, 256));
     hipLaunchKernelGGL(k_last_nonzero, dim3(blocks), dim3(256), 0, ctx->stream, a, (size_t)0,
-                       body, 1, d);
+                       body, tail, gen, 1, d);
     QG_LAUNCH_CHECK();
   }
 }
@@ -1599,7 +1627,7 @@ int qg_mle_open_batch_dev(qg_ctx* ctx, const qg_srs* srs, const qg_mle_open_item
   if (!ctx || !srs || (!items && k) || !state || (!outs && k)) return QG_ERR_INVALID;
   for (size_t i = 0; i < k; i++)
     if (!items[i].poly || items[i].n > items[i].poly->n || (!items[i].point && items[i].nvars) ||
-        (items[i].flags & ~(uint32_t)QG_OPEN_UNCHANGED))
+        items[i].nvars > 30 || (items[i].flags & ~(uint32_t)QG_OPEN_UNCHANGED))
       return QG_ERR_INVALID;
   return qg_guard(ctx, [&] {
     QG_CHECK(k <= 256, QG_ERR_UNSUPPORTED, "too many openings in one batch (at most 256)");

@@ -23,6 +23,7 @@
 //    slots on the fly with running sums from the top, then shuffle folds
 //    (suffix scan + tree) and three quad-cooperative folds of 16.
 #include <stdlib.h>
+#include <string.h>
 
 #include "common.h"
 #include "curve29.h"
@@ -114,12 +115,43 @@ static constexpr int SORT_TILE_MAX = 1024;                  // scalars per block
 static constexpr size_t SORT_LDS_A = 72 * 1024;             // LDS budget for staged entries (2 blocks/CU)
 static constexpr int SORT_CHUNK = 8192;                     // entries per block (pass B)
 
+// ---- cross-stream hand-over guard (msm_device_batch) ----------------------
+// A batch on the side streams hands data over by events only: the scalars
+// from the context stream to the side streams, the partial sums back.  Each
+// hand-over is also checked on the device: the producer stream writes this
+// batch's generation into a tag word (k_handover_tag, after its last producer
+// kernel); every block of the consumer kernels reads the tag when it starts
+// and sets an error bit if it does not hold the generation yet, i.e. if the
+// block started before the producer stream reached the tag.  hv[0]: tag of the
+// scalars, hv[1]: error bits (1 = scalars, 2 = partials), hv[2 + p]: tag of
+// side stream p's last accumulation.  The host reads hv[1] with the results
+// and recomputes the batch in stream order if it is not 0 (counted as
+// `msm_handover_violation`).
+__global__ void k_handover_tag(uint32_t* hv, uint32_t w, uint32_t gen, uint32_t clear) {
+  if (threadIdx.x == 0) {
+    if (clear) hv[1] = hv[2] = hv[3] = 0u;
+    hv[w] = gen;
+  }
+}
+
+QG_DEV void msm_handover_check(uint32_t* hv, uint32_t w0, uint32_t nw, uint32_t gen, uint32_t bit) {
+  if (hv == nullptr || threadIdx.x != 0) return;
+  for (uint32_t w = w0; w < w0 + nw; w++)
+    if (__hip_atomic_load(hv + w, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) != gen) {
+      atomicOr(hv + 1, bit);
+      return;
+    }
+}
+
 // Pass A histogram; also writes every scalar's canonical words (`canon`), so
 // the scatter pass reads them without a second Montgomery reduction.
+// hv != null: the scalars came from another stream (hand-over guard above)
 __global__ void __launch_bounds__(SORT_BLOCK)
     k_sortA_hist(const Fr* __restrict__ scalars, size_t n, int c, int W, int LO, int H,
-                 uint32_t nblk, uint32_t tile, uint32_t* __restrict__ hrow, Fr* __restrict__ canon) {
+                 uint32_t nblk, uint32_t tile, uint32_t* __restrict__ hrow, Fr* __restrict__ canon,
+                 uint32_t* hv, uint32_t gen) {
   extern __shared__ uint32_t hist[];
+  msm_handover_check(hv, 0, 1, gen, 1u);
   for (int g = threadIdx.x; g < H; g += blockDim.x) hist[g] = 0;
   __syncthreads();
   const uint32_t tb = xcd_tile(blockIdx.x, nblk);
@@ -869,7 +901,8 @@ QG_DEV uint32_t msm_slot_stride(uint32_t nslot, uint32_t T) {
 __global__ void __launch_bounds__(MSM_BLOCK)
     k_msm_tree_step(X29Raw* __restrict__ partial, const uint32_t* __restrict__ owner,
                     const uint32_t* __restrict__ bstart, uint32_t L, uint32_t T, uint32_t s_lo,
-                    uint32_t s_end, uint32_t s) {
+                    uint32_t s_end, uint32_t s, uint32_t* hv, uint32_t gen) {
+  msm_handover_check(hv, 2, 2, gen, 2u);  // the partials came from the side streams
   const uint32_t i = s_lo + blockIdx.x * blockDim.x + threadIdx.x;
   if (i >= s_end) return;
   const uint32_t b = owner[i];
@@ -1069,8 +1102,10 @@ __device__ __forceinline__ void msm_fold(X29& A, X29 Y, int gl, uint32_t mv, int
 // A_out[w], Y_out[w] with sum_j (j + 1) B_j = sum_w A_w + w Y_w
 __global__ void __launch_bounds__(MSM_BLOCK)
     k_msm_bsum(const MsmRed* __restrict__ runs, MsmRedSet rs, uint32_t nb, int slog, int gl,
-               G1Xyzz* __restrict__ A_out, G1Xyzz* __restrict__ Y_out, size_t ostride) {
+               G1Xyzz* __restrict__ A_out, G1Xyzz* __restrict__ Y_out, size_t ostride,
+               uint32_t* hv, uint32_t gen) {
 #if defined(__HIP_DEVICE_COMPILE__)
+  msm_handover_check(hv, 2, 2, gen, 2u);  // the partials came from the side streams
   const uint32_t t = blockIdx.x * blockDim.x + threadIdx.x;
   const MsmRed rr = runs ? runs[blockIdx.y] : rs.r[blockIdx.y];  // small batches by value
   X29 run = x29_inf(), wsum = x29_inf(), B = x29_inf();
@@ -1335,7 +1370,7 @@ static constexpr int MSM_MAX_BATCH = 1024;
 // batch would be freed while an earlier MSM's kernels still read it.
 static MsmRun msm_accumulate_phase(qg_ctx* ctx, const qg_srs* srs, const Fr* d_scalars, size_t n,
                                    int slot, size_t srs_off = 0, hipStream_t bst = nullptr,
-                                   bool reserve = false) {
+                                   bool reserve = false, uint32_t* hv = nullptr, uint32_t hgen = 0) {
   QG_CHECK(srs_off <= srs->n && n <= srs->n - srs_off, QG_ERR_INVALID, "MSM length exceeds the SRS");
   MsmRun run;
   const std::string sfx = "#" + std::to_string(slot);
@@ -1434,7 +1469,7 @@ static MsmRun msm_accumulate_phase(qg_ctx* ctx, const qg_srs* srs, const Fr* d_s
       QgTimed tm(ctx, side ? "msm_bucketing_side" : "msm_bucketing", bst);
       // pass A: partition digits by the high bucket bits
       hipLaunchKernelGGL(k_sortA_hist, dim3(nblk), dim3(SORT_BLOCK), H * sizeof(uint32_t),
-                         bst, d_scalars, n, c, W, LO, H, nblk, tile, hrow, canon);
+                         bst, d_scalars, n, c, W, LO, H, nblk, tile, hrow, canon, hv, hgen);
       QG_LAUNCH_CHECK();
       hipLaunchKernelGGL(k_transpose32, dim3(div_up(H, 32), div_up(nblk, 32)), dim3(256), 0,
                          bst, hrow, nblk, (uint32_t)H, ghist);
@@ -1552,14 +1587,24 @@ static MsmRun msm_accumulate_phase(qg_ctx* ctx, const qg_srs* srs, const Fr* d_s
 // the two weighted-sum levels and the export for the whole batch — the
 // latency-bound tail of the MSM is paid once per batch.  out: XYZZ (R = 2^256)
 // per MSM, not yet summed over ranks.
+// hv / hgen: the hand-over guard words of a batch whose partials come from
+// the side streams (msm_device_batch); its error word lands in *h_err (pinned)
+// with the results
 static void msm_reduce_phase(qg_ctx* ctx, const qg_srs* srs, const std::vector<MsmRun>& runs,
-                             std::vector<G1Xyzz>& out) {
+                             std::vector<G1Xyzz>& out, uint32_t* hv = nullptr, uint32_t hgen = 0,
+                             uint32_t* h_err = nullptr) {
   const uint32_t k = (uint32_t)runs.size();
   out.assign(k, G1Xyzz::infinity());
   std::vector<uint32_t> live;
   for (uint32_t i = 0; i < k; i++)
     if (!runs[i].empty) live.push_back(i);
-  if (live.empty()) return;
+  if (live.empty()) {
+    if (hv) {  // nothing to reduce: the guard word alone
+      QG_HIP(hipMemcpyAsync(h_err, hv + 1, sizeof(uint32_t), hipMemcpyDeviceToHost, ctx->stream));
+      ctx->sync();
+    }
+    return;
+  }
   QG_CHECK(live.size() <= (size_t)MSM_MAX_BATCH, QG_ERR_UNSUPPORTED, "MSM batch too large");
   const uint32_t kl = (uint32_t)live.size();
   const uint32_t nb = 1u << (srs->c - 1);
@@ -1621,7 +1666,7 @@ static void msm_reduce_phase(qg_ctx* ctx, const qg_srs* srs, const std::vector<M
         QG_CHECK(s_hi < r.nslots, QG_ERR_ASSERT, "MSM partial-slot range");
         hipLaunchKernelGGL(k_msm_tree_step, dim3(div_up(s_hi - s_lo + 1, MSM_BLOCK)), dim3(MSM_BLOCK),
                            0, ctx->stream, r.partial, r.owner, r.bstart, r.L, r.T, s_lo, s_hi + 1,
-                           st);
+                           st, hv, hgen);
         QG_LAUNCH_CHECK();
         st <<= 1;
       }
@@ -1629,14 +1674,16 @@ static void msm_reduce_phase(qg_ctx* ctx, const qg_srs* srs, const std::vector<M
       if (q < MSM_RED_BYVAL) rset.r[q] = h_runs[q];
     }
     const MsmRed* d_runs = nullptr;
-    if (kl > MSM_RED_BYVAL) {
+    if (kl > MSM_RED_BYVAL) {  // through pinned staging: a pageable copy queued behind
+                               // the side streams would block the host until they drain
       MsmRed* d = ctx->scratch_as<MsmRed>("msm_runs", kl);
-      QG_HIP(hipMemcpyAsync(d, h_runs.data(), kl * sizeof(MsmRed), hipMemcpyHostToDevice,
-                            ctx->stream));
+      MsmRed* hs = reinterpret_cast<MsmRed*>(ctx->pinned_get("msm_runs_h", MSM_MAX_BATCH * sizeof(MsmRed)));
+      std::copy(h_runs.begin(), h_runs.end(), hs);
+      QG_HIP(hipMemcpyAsync(d, hs, kl * sizeof(MsmRed), hipMemcpyHostToDevice, ctx->stream));
       d_runs = d;
     }
     hipLaunchKernelGGL(k_msm_bsum, dim3(g1, kl), dim3(MSM_BLOCK), 0, ctx->stream, d_runs, rset, nb,
-                       slog1, gl1, A1, Y1, (size_t)m1);
+                       slog1, gl1, A1, Y1, (size_t)m1, hv, hgen);
     QG_LAUNCH_CHECK();
     // wave folds, 64 elements per wave, until one element per MSM is left
     G1Xyzz *Ai = A1, *Yi = Y1, *Ao = A2, *Yo = Y2;
@@ -1664,6 +1711,7 @@ static void msm_reduce_phase(qg_ctx* ctx, const qg_srs* srs, const std::vector<M
   }
   std::vector<G1Xyzz> h(kl);
   QG_HIP(hipMemcpyAsync(h.data(), d_out, kl * sizeof(G1Xyzz), hipMemcpyDeviceToHost, ctx->stream));
+  if (hv) QG_HIP(hipMemcpyAsync(h_err, hv + 1, sizeof(uint32_t), hipMemcpyDeviceToHost, ctx->stream));
   ctx->sync();
   for (uint32_t q = 0; q < kl; q++) out[live[q]] = h[q];
 }
@@ -1692,36 +1740,55 @@ static G1Affine msm_finish_ranks(qg_ctx* ctx, G1Xyzz acc) {
 // Batches of two or more MSMs run on two side streams by MSM parity, each
 // MSM's bucketing and accumulation on one stream: MSM i + 1's radix passes
 // (memory-bound) run beside MSM i's accumulation (VALU-bound), which slows
-// by ~0.3 ms per 1 ms of bucketing it hosts.  The scalars (written on
-// ctx->stream) and the partial sums (read by the reduction on ctx->stream)
-// cross between streams only through host synchronizations, one at each end
-// of the batch: the first version handed the entry lists from a bucketing
-// stream to the accumulating stream by events and some commitments came out
-// wrong, intermittently, and an event-ordered hand-over of the scalars was
-// still wrong for the last MSMs of a batch (micro/open_batch_dbg.py,
-// profiles/r05_open_batch_ab.txt).  HyperPlonk proof 935.8 / 932.6 ->
-// 896.1 / 894.9 ms, same transcript, every proof oracle-verified and
-// identical across runs (profiles/r05_msm_pipe2_ab.txt).  QG_MSM_PIPE=0
-// keeps a batch on ctx->stream (A/B runs).  A lone MSM split into pieces to
-// get the same overlap is slower (2^24: 18.15 -> 18.7 ms with 2 pieces: each
-// piece pays its own bucket reduction, and the accumulation slows by 0.85 ms
-// under the second piece's bucketing).
-std::vector<G1Affine> msm_device_batch(qg_ctx* ctx, const qg_srs* srs,
-                                       const std::vector<const Fr*>& scalars,
-                                       const std::vector<size_t>& ns) {
-  QG_CHECK(scalars.size() == ns.size(), QG_ERR_INVALID, "MSM batch shape");
-  bool pipe = scalars.size() >= 2;
-  if (const char* ov = getenv("QG_MSM_PIPE")) pipe = pipe && atoi(ov) != 0;
+// by ~0.3 ms per 1 ms of bucketing it hosts.  HyperPlonk proof 935.8 / 932.6
+// -> 896.1 / 894.9 ms (profiles/r05_msm_pipe2_ab.txt).
+//
+// The two cross-stream hand-overs are event-ordered: the scalars (written on
+// ctx->stream) go to both side streams behind one event, the partial sums come
+// back to the reduction (ctx->stream) behind one event per side stream.  Each
+// event is fresh for its hand-over and returns to the pool only after the
+// batch's final synchronization, and each hand-over is checked on the device
+// (the guard words above k_sortA_hist): a consumer block that starts before its
+// producer stream reached the tag sets an error bit; the host then recomputes
+// the batch in stream order and counts it (`msm_handover_violation`, in the
+// bench line).  Round 5 had crossed these hand-overs through host
+// synchronizations after intermittently wrong quotient commitments with
+// event-ordered forms; micro/handover_probe.hip (profiles/r06_handover_probe.txt)
+// then found no ordering or visibility failure of event hand-overs themselves
+// in ~1.3e5 checked hand-overs (RAW and WAW, held and LIFO-recycled events, a
+// D2H copy as the last producer command, under load), DESIGN §5.3 has the
+// analysis.  QG_MSM_PIPE=0 keeps a batch on ctx->stream; QG_MSM_PIPE_SYNC=1
+// crosses through host synchronizations instead of events (A/B runs).
+static std::vector<G1Xyzz> msm_batch_local(qg_ctx* ctx, const qg_srs* srs,
+                                           const std::vector<const Fr*>& scalars,
+                                           const std::vector<size_t>& ns, bool pipe,
+                                           bool* violated) {
+  *violated = false;
   hipStream_t side[2] = {nullptr, nullptr};
+  bool host_sync = false;
+  if (const char* ov = getenv("QG_MSM_PIPE_SYNC")) host_sync = atoi(ov) != 0;
+  std::vector<hipEvent_t> held;  // hand-over events of this batch
+  uint32_t* hv = nullptr;
+  uint32_t hgen = 0;
+  uint32_t* h_err = nullptr;
   if (pipe) {
     if (!ctx->side_stream) QG_HIP(hipStreamCreateWithFlags(&ctx->side_stream, hipStreamNonBlocking));
     if (!ctx->side_stream2) QG_HIP(hipStreamCreateWithFlags(&ctx->side_stream2, hipStreamNonBlocking));
     side[0] = ctx->side_stream;
     side[1] = ctx->side_stream2;
-    // the scalars were written on ctx->stream: the host waits for them rather
-    // than an event (with the event-ordered hand-over some side-stream MSMs
-    // read wrong scalars, profiles/r05_open_batch_ab.txt)
-    QG_HIP(hipStreamSynchronize(ctx->stream));
+    if (host_sync) {
+      QG_HIP(hipStreamSynchronize(ctx->stream));
+    } else {
+      hv = ctx->scratch_as<uint32_t>("msm_handover", 4);
+      h_err = reinterpret_cast<uint32_t*>(ctx->pinned_get("msm_handover_h", 16));
+      hgen = ++ctx->msm_gen;
+      hipLaunchKernelGGL(k_handover_tag, dim3(1), dim3(64), 0, ctx->stream, hv, 0u, hgen, 1u);
+      QG_LAUNCH_CHECK();
+      hipEvent_t ev = ctx->ev_get();
+      held.push_back(ev);
+      QG_HIP(hipEventRecord(ev, ctx->stream));
+      for (hipStream_t st : side) QG_HIP(hipStreamWaitEvent(st, ev, 0));
+    }
   }
   if (scalars.size() >= 2) {  // size the shared scratch for the longest MSM first
     size_t im = 0;
@@ -1732,11 +1799,55 @@ std::vector<G1Affine> msm_device_batch(qg_ctx* ctx, const qg_srs* srs,
   }
   std::vector<MsmRun> runs;
   for (size_t i = 0; i < scalars.size(); i++)
-    runs.push_back(msm_accumulate_phase(ctx, srs, scalars[i], ns[i], (int)i, 0, side[i & 1]));
-  if (pipe)  // the reduction (ctx->stream) after both side streams, likewise
+    runs.push_back(
+        msm_accumulate_phase(ctx, srs, scalars[i], ns[i], (int)i, 0, side[i & 1], false, hv, hgen));
+  if (pipe && host_sync) {
     for (hipStream_t st : side) QG_HIP(hipStreamSynchronize(st));
+  } else if (pipe) {  // the reduction (ctx->stream) after both side streams
+    for (int p = 0; p < 2; p++) {
+      hipLaunchKernelGGL(k_handover_tag, dim3(1), dim3(64), 0, side[p], hv, 2u + (uint32_t)p, hgen, 0u);
+      QG_LAUNCH_CHECK();
+      hipEvent_t ev = ctx->ev_get();
+      held.push_back(ev);
+      QG_HIP(hipEventRecord(ev, side[p]));
+      QG_HIP(hipStreamWaitEvent(ctx->stream, ev, 0));
+    }
+  }
   std::vector<G1Xyzz> local;
-  msm_reduce_phase(ctx, srs, runs, local);  // ends with a stream synchronization
+  // ends with a synchronization of ctx->stream, which waited for both side
+  // streams: the side streams are idle when this returns (the grid-barrier
+  // sumcheck kernels never share the chip with them)
+  msm_reduce_phase(ctx, srs, runs, local, hv, hgen, h_err);
+  for (hipEvent_t e : held) ctx->event_pool.push_back(e);
+  if (hv && *h_err != 0) {
+    ctx->msm_handover_violation++;
+    *violated = true;
+  }
+  return local;
+}
+
+std::vector<G1Affine> msm_device_batch(qg_ctx* ctx, const qg_srs* srs,
+                                       const std::vector<const Fr*>& scalars,
+                                       const std::vector<size_t>& ns) {
+  QG_CHECK(scalars.size() == ns.size(), QG_ERR_INVALID, "MSM batch shape");
+  bool pipe = scalars.size() >= 2;
+  if (const char* ov = getenv("QG_MSM_PIPE")) pipe = pipe && atoi(ov) != 0;
+  bool violated = false;
+  std::vector<G1Xyzz> local = msm_batch_local(ctx, srs, scalars, ns, pipe, &violated);
+  if (violated)  // a hand-over was not ordered: the batch again, in stream order
+    local = msm_batch_local(ctx, srs, scalars, ns, false, &violated);
+  // QG_MSM_VERIFY_BATCH=1 (diagnosis): every side-stream batch again in stream
+  // order; a differing MSM is reported on stderr (micro/handover_dbg.py)
+  if (pipe && getenv("QG_MSM_VERIFY_BATCH")) {
+    bool v2 = false;
+    std::vector<G1Xyzz> chk = msm_batch_local(ctx, srs, scalars, ns, false, &v2);
+    for (size_t i = 0; i < chk.size(); i++) {
+      const G1Affine a = xyzz_to_affine(local[i]), b = xyzz_to_affine(chk[i]);
+      if (memcmp(&a, &b, sizeof(a)) != 0)
+        fprintf(stderr, "QG_MSM_VERIFY_BATCH: MSM %zu of %zu (n = %zu) differs from stream order\n",
+                i, chk.size(), ns[i]);
+    }
+  }
   std::vector<G1Affine> res(local.size());
   for (size_t i = 0; i < local.size(); i++) res[i] = msm_finish_ranks(ctx, local[i]);
   return res;
@@ -1759,12 +1870,15 @@ static G1Affine msm_host(qg_ctx* ctx, const qg_srs* srs, const uint64_t* h, size
     return msm_device(ctx, srs, d, n);
   }
   if (!ctx->copy_stream) QG_HIP(hipStreamCreateWithFlags(&ctx->copy_stream, hipStreamNonBlocking));
+  // the hand-over events return to the pool only after the reduction's
+  // synchronization (none is re-recorded while a queued wait refers to it)
+  std::vector<hipEvent_t> held;
   {  // the uploads start after the work already queued on ctx->stream (stream
      // order in both directions: the scratch slot may still be read there)
     hipEvent_t ev = ctx->ev_get();
+    held.push_back(ev);
     QG_HIP(hipEventRecord(ev, ctx->stream));
     QG_HIP(hipStreamWaitEvent(ctx->copy_stream, ev, 0));
-    ctx->event_pool.push_back(ev);
   }
   std::vector<MsmRun> runs;
   const size_t per = div_up(n, (size_t)P);
@@ -1774,13 +1888,14 @@ static G1Affine msm_host(qg_ctx* ctx, const qg_srs* srs, const uint64_t* h, size
     QG_HIP(hipMemcpyAsync(d + off, h + 4 * off, len * sizeof(Fr), hipMemcpyHostToDevice,
                           ctx->copy_stream));
     hipEvent_t ev = ctx->ev_get();
+    held.push_back(ev);
     QG_HIP(hipEventRecord(ev, ctx->copy_stream));
     QG_HIP(hipStreamWaitEvent(ctx->stream, ev, 0));
-    ctx->event_pool.push_back(ev);
     runs.push_back(msm_accumulate_phase(ctx, srs, d + off, len, k, off));
   }
   std::vector<G1Xyzz> part;
-  msm_reduce_phase(ctx, srs, runs, part);
+  msm_reduce_phase(ctx, srs, runs, part);  // ends with a synchronization
+  for (hipEvent_t e : held) ctx->event_pool.push_back(e);
   G1Xyzz acc = G1Xyzz::infinity();
   for (const G1Xyzz& q : part) acc = xyzz_add(acc, q);
   return msm_finish_ranks(ctx, acc);

@@ -2626,8 +2626,10 @@ static void sumcheck_run(qg_ctx* ctx, uint32_t nvars, uint32_t ntables,
   // is unchanged (arena.h: never an address)
   const std::string memo =
       ctx->arena.derived_key(std::to_string(P->id), 1, ctx->scratch_gen("sc_prog"));
-  if (!ctx->arena.check_or_set("sc_prog", memo))
+  if (!ctx->arena.check("sc_prog", memo)) {
     QG_HIP(hipMemcpyAsync(d_sp, &P->img, sizeof(SopDev), hipMemcpyHostToDevice, ctx->stream));
+    ctx->arena.commit("sc_prog", memo);
+  }
   uint8_t* hio = reinterpret_cast<uint8_t*>(ctx->pinned_get("sc_io", io_bytes));
   memset(hio, 0, o_chal);
   memcpy(hio, &hs, sizeof hs);

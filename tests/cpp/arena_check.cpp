@@ -61,7 +61,10 @@ static bool derived(Arena& a, const std::string& src, int logn) {
   const std::string tag = "pyr:" + src;
   a.get(tag, (size_t)1 << logn);
   const uint64_t st = a.stamp(src);
-  return !a.check_or_set(tag, Arena::derived_key(std::to_string(logn), st, a.gen(tag)), st);
+  const std::string key = Arena::derived_key(std::to_string(logn), st, a.gen(tag));
+  if (a.check(tag, key, st)) return false;
+  a.commit(tag, key);
+  return true;
 }
 
 // a flat table build (ntt_twiddles' rule): rebuilds and stamps when the
@@ -69,8 +72,9 @@ static bool derived(Arena& a, const std::string& src, int logn) {
 static bool build_flat(Arena& a, const std::string& slot, int logn) {
   a.get(slot, (size_t)1 << logn);
   const std::string key = std::to_string(logn) + "|g" + std::to_string(a.gen(slot));
-  if (a.check_or_set(slot, key)) return false;
+  if (a.check(slot, key)) return false;
   a.bump(slot);
+  a.commit(slot, key);
   return true;
 }
 
@@ -138,6 +142,17 @@ int main() {
     rebuilds += !hit;
   }
   CHECK("lru_alternating_two_builds", rebuilds == 2);
+
+  // 6. check + commit: a build whose launches throw never
+  //    commits, so the table stays invalid; a mismatching check clears the
+  //    stale memo, so a later failed rebuild cannot revive the old key
+  Arena e;
+  CHECK("no_memo_invalid", !e.check("t", "k1"));
+  CHECK("uncommitted_build_stays_invalid", !e.check("t", "k1"));
+  e.commit("t", "k1");
+  CHECK("committed_valid", e.check("t", "k1"));
+  CHECK("other_key_invalid", !e.check("t", "k2"));
+  CHECK("stale_memo_cleared", !e.check("t", "k1"));
 
   a.release_all();
   b.release_all();

@@ -12,6 +12,7 @@ import contextlib
 import os
 import random
 
+import numpy as np
 import pytest
 
 import quill_oracle as o
@@ -186,3 +187,91 @@ def test_side_stream_bucketing_matches_stream_order(dev, nv):
     kzg.srs.close()
     assert res[0] == res[1]
     assert res[0][0].evaluation == o.mle_evaluate(poly, point)
+
+
+def test_open_batch_event_handover_matches_stream_order_and_oracle(dev):
+    """The shape that failed in round 5 (profiles/r05_open_batch_ab.txt): one
+    batched opening (qg_mle_open_batch_dev) of 10 vectors of 2^14..2^17
+    entries, i.e. a 10-MSM S-commitment batch and a 40-MSM quotient batch on
+    the two side streams, with event-ordered hand-overs (default), with
+    host-synchronized hand-overs (QG_MSM_PIPE_SYNC=1) and in stream order
+    (QG_MSM_PIPE=0), three times each, against successive single openings.
+    Every proof field and the transcript state are identical, the oracle
+    verifier (mlpcs.rs:126-161, KZG by the trapdoor identity) accepts every
+    proof against [p(tau)] g, and the device hand-over guard never fired."""
+    import oracle_c as oc
+    from quill_amd import KZG, DeviceVec, Transcript
+    tau = 0x48414E444F564552
+    kzg = KZG.trusted_setup((1 << 17) - 1, tau, dev)
+    rnd = random.Random(6060)
+    # (log length, variables, live entries): full, zero-tailed (trims), a
+    # public-column-like vector that trims to one entry, n > 2^nv, n < 2^nv
+    shapes = [(17, 17, None), (16, 16, None), (17, 17, 5 << 14), (14, 14, None), (15, 15, None),
+              (14, 14, 1), (16, 15, None), (15, 16, None), (17, 17, None), (14, 14, None)]
+    vecs, arrs, items = [], [], []
+    for k, (ln, nv, live) in enumerate(shapes):
+        v = DeviceVec(dev, 1 << ln).fill_random(0x6060 + k)
+        if live is not None:  # zero tail: the opening trims it (kzg.rs / ipa.rs)
+            DeviceVec.from_u64(dev, np.zeros((1 << ln) - live, dtype=np.uint64), out=v, offset=live)
+        vecs.append(v)
+        arrs.append(v.to_numpy())
+        items.append((v, 1 << ln, [rnd.randrange(R) for _ in range(nv)], False))
+    items.append((vecs[0], 1 << 17, [rnd.randrange(R) for _ in range(17)], True))  # unchanged reuse
+    ts = Transcript(b"handover")
+    seq = [kzg.open_dev(v, n, pt, ts, unchanged=u) for v, n, pt, u in items]
+    before = dev.counter("msm_handover_violation")
+    for mode in ("events", "host", "stream") * 3:
+        with env("QG_MSM_PIPE", "0" if mode == "stream" else "1"), \
+                env("QG_MSM_PIPE_SYNC", "1" if mode == "host" else "0"):
+            tb = Transcript(b"handover")
+            got = kzg.open_batch_dev(items, tb)
+        assert got == seq, mode
+        assert tb.state == ts.state, mode
+    assert dev.counter("msm_handover_violation") == before
+    okzg = o.KZG((1 << 17) - 1, tau)
+    vt = o.Transcript(b"handover")
+    for (v, n, pt, _), proof in zip(items, seq):
+        arr = arrs[vecs.index(v)]
+        C = oc.g1_mul(o.G1_GEN, oc.fr_horner(arr, tau))
+        pad = (1 << len(pt)) - len(arr)  # n < 2^nv: the zero-extended vector's MLE
+        ext = np.vstack([arr, np.zeros((pad, 4), dtype=np.uint64)]) if pad > 0 else arr
+        assert proof.evaluation == oc.fr_mle_eval(ext, pt)
+        op = o.MLEvalProof(pt, proof.evaluation, proof.s_comm,
+                           *[(getattr(proof, k).x, getattr(proof, k).y, getattr(proof, k).proof)
+                             for k in ("poly_opening", "poly_opening_inv", "s_opening",
+                                       "s_opening_inv")])
+        assert op.verify(C, okzg, vt)
+    assert vt.state == ts.state
+    for v in vecs:
+        v.close()
+    kzg.close()
+
+
+def test_hyperplonk_2p14_rows_event_handover_same_proof(dev):
+    """HyperPlonk at 2^14 rows (the round-5 failing case, micro/open_batch_dbg.py):
+    the proof with the MSM batches' event-ordered hand-overs equals, byte for
+    byte, the proofs with host-synchronized hand-overs and in stream order;
+    the oracle verifier accepts it; the hand-over guard never fired."""
+    import hyperplonk_oracle as ho
+    from quill_amd import KZG, HyperPlonk, serialize
+    from quill_amd import examples as ex
+    from test_gpu_hyperplonk import TAU, _oracle_setup, to_oracle
+    rows = 1 << 14
+    cws = [ex.fibonacci_circuit_and_trace(rows), ex.modified_fibonacci_circuit_and_trace(rows)]
+    pcs = KZG.trusted_setup(max(c.num_cols() * c.num_rows() for c, _ in cws), TAU, dev)
+    hp = HyperPlonk.preprocess([c for c, _ in cws], pcs)
+    ws = [w for _, w in cws]
+    before = dev.counter("msm_handover_violation")
+    out = {}
+    for mode in ("events", "host", "stream", "events"):
+        with env("QG_MSM_PIPE", "0" if mode == "stream" else "1"), \
+                env("QG_MSM_PIPE_SYNC", "1" if mode == "host" else "0"):
+            proof = hp.prove(pcs, ws)
+        enc = serialize(proof)
+        assert out.setdefault(mode, enc) == enc, mode
+        last = proof
+    assert out["events"] == out["host"] == out["stream"]
+    assert dev.counter("msm_handover_violation") == before
+    opcs, ohp, _ = _oracle_setup(rows, ("fib", "mod"))
+    vt = ho.hyperplonk_verify(to_oracle(last), ohp.to_vk(), opcs)
+    assert vt.state == hp.last_transcript.state
