@@ -410,6 +410,9 @@ def main():
         if args.log_mle > 0 and isinstance(out.get("mle_open"), dict):
             out["mle_open"]["cpu_baseline"] = cpu_baseline_mle(args)
     out["msm_plan_refetch"] = dev.counter("msm_plan_refetch")  # over every leg
+    # MSM batches whose event-ordered side-stream hand-over the device guard
+    # found unordered (recomputed in stream order); 0 while the ordering holds
+    out["msm_handover_violation"] = dev.counter("msm_handover_violation")
     if rank == 0:
         write_detail(out, args.detail_out)
         print(json.dumps(compact(out), separators=(",", ":")), flush=True)
@@ -427,7 +430,8 @@ def main():
 # roofline, compute, cpu_baseline and one summary per leg.
 LINE_MAX_BYTES = 6000
 _DROP_KEYS = {"note", "traffic_note", "frac_note", "issue_bound_note", "identity", "pmc",
-              "commitment_check", "final_transcript_state", "cpu_model", "metric_note"}
+              "commitment_check", "final_transcript_state", "cpu_model", "metric_note",
+              "spans_ms_rank0"}
 # sections dropped (in this order) if the line is still over budget
 _SHED_ORDER = ("kernels_ms", "sumcheck_weak_scaling", "msm_strong_scaling", "msm_host_input",
                "logup", "mle_open", "hyperplonk", "hbm_by_kernel")
@@ -678,14 +682,20 @@ def bench_mle(q, dev, args, barrier_sync, max_over_ranks, rank=0, world=1):
     barrier_sync()
     dt = max_over_ranks(time.perf_counter() - t0)
     dev.enable_timing(True)
+    t1 = time.perf_counter()
     step()
-    parts = {nm: dev.kernel_time(nm)[0] for nm in names}
+    ms_timed = (time.perf_counter() - t1) * 1e3
+    # additive device-busy split (overlapped intervals shared evenly: the parts
+    # sum to the busy time); the per-stream spans overlap and stay apart
+    parts = dev.phase_split(names)
+    spans = {nm: dev.kernel_time(nm)[0] for nm in names}
     dev.enable_timing(False)
     poly.close()
     kzg.srs.close()
     return {"metric": f"ML-PCS commit + open (MLEvalProof::prove) ms at 2^{k} evaluations",
             "ms": dt / steps * 1e3, "higher_is_better": False, "msms_per_step": 6,
-            "parts_ms_rank0": parts, "steps": steps,
+            "parts_ms_rank0": parts, "spans_ms_rank0": spans,
+            "ms_with_phase_timing": ms_timed, "steps": steps,
             "sharding": f"2^{k} evaluations over {world} rank(s) (strong scaling); "
                         "S polynomial split by frequency residue (one all-to-all)",
             "note": "6 MSMs (commit, S commitment, 4 KZG quotients) dominate"}
@@ -765,8 +775,10 @@ def bench_logup(q, dev, args, barrier_sync, max_over_ranks, rank=0, world=1, tra
 LOGUP_MULS_PER_ROW = 8.6
 
 # msm_bucketing_side: the bucketing of the MSMs of a batch, which run on two
-# side streams by parity; it and msm_accumulate are per-stream spans that
-# overlap (a bucketing beside the other stream's accumulation): not additive
+# side streams by parity.  parts_ms_rank0 is the additive device-busy split
+# (qg_ctx_phase_split: an interval where several phases run, on any stream, is
+# shared evenly among them, so the parts sum to the busy time <= the proof
+# time); spans_ms_rank0 keeps the per-stream spans, which overlap
 HP_PHASES = ("msm_bucketing", "msm_bucketing_side", "msm_accumulate", "msm_reduce",
              "sumcheck_round", "sumcheck_tail", "logup_column", "eq_table", "inner_product",
              "s_polynomial", "kzg_division")
@@ -823,7 +835,8 @@ def bench_hyperplonk(q, dev, args, barrier_sync, max_over_ranks, rank=0, world=1
     proof = hp.prove(pcs, wits)
     barrier_sync()
     ms_timed = max_over_ranks(time.perf_counter() - t1) * 1e3
-    parts = {nm: dev.kernel_time(nm)[0] for nm in HP_PHASES}
+    parts = dev.phase_split(HP_PHASES)
+    spans = {nm: dev.kernel_time(nm)[0] for nm in HP_PHASES}
     dev.enable_timing(False)
     nopen = sum(len(tp.openings_zero_check) + len(tp.openings_public) + 5
                 for tp in proof.trace_proofs)
@@ -832,6 +845,7 @@ def bench_hyperplonk(q, dev, args, barrier_sync, max_over_ranks, rank=0, world=1
            "ms": dt / steps * 1e3, "higher_is_better": False,
            "proofs_per_s": steps / dt, "steps": steps, "setup_s": setup_s,
            "ml_openings_per_proof": nopen, "parts_ms_rank0": parts,
+           "parts_sum_ms": sum(parts.values()), "spans_ms_rank0": spans,
            "ms_with_phase_timing": ms_timed,
            "final_transcript_state": hp.last_transcript.state.hex(),
            "parallelism": f"sharded x{world}" if world > 1 else "single GPU",

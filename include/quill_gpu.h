@@ -406,6 +406,14 @@ int qg_microbench_fq_mul(qg_ctx* ctx, double* mul_per_s);
 int qg_microbench_fetch(qg_ctx* ctx, size_t rows, size_t gathers, double* gather_ms,
                         double* stream_ms);
 int qg_ctx_kernel_time(const qg_ctx* ctx, const char* name, double* total_ms, uint32_t* launches);
+/* Additive split of the device-busy time among the k phase names given (the
+ * same groups as qg_ctx_kernel_time, timing on): every interval in which m of
+ * the listed phases' regions are open - on any of the context's streams - is
+ * split evenly among those m phases, so the k values sum to the time at least
+ * one of them was running (<= the wall time), where qg_ctx_kernel_time's
+ * per-stream spans overlap (an MSM batch's bucketing beside the other side
+ * stream's accumulation).  busy_ms[i] receives the share of names[i]. */
+int qg_ctx_phase_split(const qg_ctx* ctx, const char* const* names, size_t k, double* busy_ms);
 /* Profiling marker: launches an empty kernel (k_trace_marker) of `tag` work-groups
  * on the context stream, so a rocprofv3 kernel trace can be cut into the
  * caller's phases (profiles/kstats.py --legs groups dispatches by the last

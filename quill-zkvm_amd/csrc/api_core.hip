@@ -3,6 +3,8 @@
 #include <string.h>
 
 #include "blake3.h"
+#include <algorithm>
+
 #include "common.h"
 
 using namespace qg;
@@ -205,6 +207,7 @@ int qg_ctx_destroy(qg_ctx* ctx) {
     (void)hipEventDestroy(kv.second.b);
   }
   for (auto e : ctx->event_pool) (void)hipEventDestroy(e);
+  if (ctx->tref) (void)hipEventDestroy(ctx->tref);
   if (ctx->stream) (void)hipStreamDestroy(ctx->stream);
   if (ctx->copy_stream) (void)hipStreamDestroy(ctx->copy_stream);
   if (ctx->side_stream) (void)hipStreamDestroy(ctx->side_stream);
@@ -217,8 +220,51 @@ const char* qg_last_error(const qg_ctx* ctx) { return ctx ? ctx->last_error.c_st
 
 int qg_ctx_enable_timing(qg_ctx* ctx, int enable) {
   if (!ctx) return QG_ERR_INVALID;
-  ctx->timing = enable != 0;
-  ctx->ktime.clear();
+  return qg_guard(ctx, [&] {
+    QG_HIP(hipSetDevice(ctx->device));
+    ctx->timing = enable != 0;
+    ctx->ktime.clear();
+    ctx->spans.clear();
+    if (ctx->timing) {  // the origin of the spans (qg_ctx_phase_split)
+      if (!ctx->tref) QG_HIP(hipEventCreate(&ctx->tref));
+      QG_HIP(hipEventRecord(ctx->tref, ctx->stream));
+    }
+  });
+}
+
+int qg_ctx_phase_split(const qg_ctx* ctx, const char* const* names, size_t k, double* busy_ms) {
+  if (!ctx || (k && (!names || !busy_ms))) return QG_ERR_INVALID;
+  std::map<std::string, size_t> idx;
+  for (size_t i = 0; i < k; i++) {
+    if (!names[i]) return QG_ERR_INVALID;
+    idx[names[i]] = i;
+    busy_ms[i] = 0.0;
+  }
+  // sweep over the span boundaries of the listed phases: each elementary
+  // interval is shared evenly by the phases open in it
+  std::vector<std::pair<double, long>> ev;  // (time, +(i+1) open / -(i+1) close)
+  for (const auto& sp : ctx->spans) {
+    auto it = idx.find(sp.name);
+    if (it == idx.end() || !(sp.t1 > sp.t0)) continue;
+    ev.push_back({sp.t0, (long)it->second + 1});
+    ev.push_back({sp.t1, -((long)it->second + 1)});
+  }
+  std::sort(ev.begin(), ev.end());
+  std::vector<int> open(k, 0);
+  int nopen = 0;
+  for (size_t e = 0; e < ev.size(); e++) {
+    if (e > 0 && nopen > 0) {
+      const double len = ev[e].first - ev[e - 1].first;
+      int distinct = 0;
+      for (size_t i = 0; i < k; i++) distinct += open[i] > 0;
+      for (size_t i = 0; i < k; i++)
+        if (open[i] > 0) busy_ms[i] += len / distinct;
+    }
+    const long v = ev[e].second;
+    const size_t i = (size_t)(v > 0 ? v : -v) - 1;
+    open[i] += v > 0 ? 1 : -1;
+    nopen += v > 0 ? 1 : -1;
+  }
   return QG_OK;
 }
 

@@ -87,6 +87,15 @@ struct qg_ctx {
   std::map<int, Ev> pending;  // handle -> region (stable across nested syncs)
   int next_handle = 0;
   std::map<std::string, std::pair<double, uint32_t>> ktime;
+  // every resolved region as [t0, t1) ms after the timing origin `tref`
+  // (recorded on the context stream when timing is enabled): the additive
+  // busy-time split of qg_ctx_phase_split
+  hipEvent_t tref = nullptr;
+  struct Span {
+    std::string name;
+    float t0, t1;
+  };
+  std::vector<Span> spans;
   std::vector<hipEvent_t> event_pool;
   // small per-context memo (e.g. which program image the device copy holds)
   std::map<std::string, std::string> memo;
@@ -180,6 +189,11 @@ struct qg_ctx {
       auto& slot = ktime[it->second.name];
       slot.first += ms;
       slot.second += 1;
+      if (tref) {
+        float t0 = 0.f;
+        QG_HIP(hipEventElapsedTime(&t0, tref, it->second.a));
+        spans.push_back({it->second.name, t0, t0 + ms});
+      }
       event_pool.push_back(it->second.a);
       event_pool.push_back(it->second.b);
       it = pending.erase(it);

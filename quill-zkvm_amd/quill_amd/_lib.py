@@ -151,6 +151,7 @@ PROTOTYPES = {
     "qg_microbench_fetch": (C.c_int, [P, C.c_size_t, C.c_size_t, C.POINTER(C.c_double),
                                       C.POINTER(C.c_double)]),
     "qg_ctx_kernel_time": (C.c_int, [P, C.c_char_p, C.POINTER(C.c_double), U32P]),
+    "qg_ctx_phase_split": (C.c_int, [P, C.POINTER(C.c_char_p), SZ, C.POINTER(C.c_double)]),
     "qg_trace_marker": (C.c_int, [P, C.c_uint32]),
     "qg_ctx_counter": (C.c_int, [P, C.c_char_p, C.POINTER(C.c_uint64)]),
 }

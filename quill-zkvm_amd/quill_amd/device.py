@@ -129,6 +129,15 @@ class Device:
         check(lib().qg_ctx_kernel_time(self.h, name.encode(), C.byref(ms), C.byref(n)), self.h)
         return ms.value, n.value
 
+    def phase_split(self, names) -> dict:
+        """additive device-busy ms per phase (qg_ctx_phase_split): overlapped
+        intervals shared evenly, so the values sum to the busy time"""
+        k = len(names)
+        arr = (C.c_char_p * max(k, 1))(*[n.encode() for n in names])
+        out = (C.c_double * max(k, 1))()
+        check(lib().qg_ctx_phase_split(self.h, arr, k, out), self.h)
+        return {n: out[i] for i, n in enumerate(names)}
+
     # ---- device math building blocks (mlpcs.rs / ipa.rs / eq_eval.rs) ----
     def eq_table_dev(self, point, out: "DeviceVec" = None) -> "DeviceVec":
         """fast_eq_eval_hypercube (eq_eval.rs:6-31) into a device vector"""
