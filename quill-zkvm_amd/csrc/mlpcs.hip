@@ -1306,6 +1306,203 @@ static void mle_open_sharded(qg_ctx* ctx, const qg_srs* srs, const Fr* dpoly, si
   kzg_open_sharded(ctx, srs, Sl, L, Slen, r_inv, &out->s_opening_inv);
 }
 
+struct MleOpenItem {
+  const Fr* poly;
+  size_t n;
+  const uint64_t* point;
+  size_t nvars;
+  bool unchanged;
+  uint64_t id;
+  size_t off;
+};
+
+// K openings on a sharded context: mle_open_sharded's data flow, batched the
+// way mle_open_batch_device batches the single-context one.  Per item the eq
+// table, the local dot, the gathered vector's residue-split S slice and the
+// local trimmed lengths are queued; ONE allgather carries every item's dot
+// part and local lengths; the S commitments run as ONE MSM batch (one
+// allgather of the per-rank partials); the transcript steps run on the host
+// in item order; the 4K quotients' local suffix-Horner scans are queued, ONE
+// allgather carries their slice-end values T; the carries (x^(le - i) C) are
+// applied; the 4K quotient commitments run as ONE MSM batch.  Four exchanges
+// per trace instead of ~11 per opening; the proofs and the final transcript
+// state equal K successive mle_open_sharded calls (tests/test_gpu_multirank.py).
+static void mle_open_batch_sharded(qg_ctx* ctx, const qg_srs* srs,
+                                   const std::vector<MleOpenItem>& items, uint8_t state[32],
+                                   qg_mle_proof* outs) {
+  const size_t K = items.size();
+  const size_t W = (size_t)ctx->world, rank = (size_t)ctx->rank;
+  for (const MleOpenItem& it : items) {
+    QG_CHECK(it.nvars <= 30, QG_ERR_INVALID, "too many variables");
+    QG_CHECK(it.n * W == ((size_t)1 << it.nvars), QG_ERR_UNSUPPORTED,
+             "sharded opening needs world * local length == 2^nvars");
+  }
+  // small per-item values of this rank: K dot parts, 2K local trimmed lengths
+  const size_t sm_bytes = K * sizeof(Fr) + 2 * K * sizeof(unsigned long long);
+  uint8_t* d_sm = ctx->scratch_as<uint8_t>("mlebs_small", sm_bytes);
+  Fr* d_part = reinterpret_cast<Fr*>(d_sm);
+  unsigned long long* d_len = reinterpret_cast<unsigned long long*>(d_sm + K * sizeof(Fr));
+  QG_HIP(hipMemsetAsync(d_sm, 0, sm_bytes, ctx->stream));
+  const char* rep = getenv("QG_S_REPLICATED");  // read per call: tests toggle it in-process
+  const bool replicated = rep && atoi(rep) != 0;
+  std::vector<Fr*> Sl(K);
+  for (size_t k = 0; k < K; k++) {
+    const MleOpenItem& it = items[k];
+    const size_t L = it.n, N = (size_t)1 << it.nvars, off = rank * L;
+    Fr* dz = ctx->scratch_as<Fr>("mleb_z#" + std::to_string(k), it.nvars ? it.nvars : 1);
+    Fr* dpr = ctx->scratch_as<Fr>("mle_pr", N);
+    fr_upload(ctx, dz, it.point, it.nvars);
+    eq_table_device(ctx, dz, (uint32_t)it.nvars, dpr);
+    dot_to_device(ctx, it.poly, dpr + off, L, d_part + k);
+    trim_launch(ctx, it.poly, L, d_len + 2 * k);
+    Sl[k] = ctx->scratch_as<Fr>("mleb_Sl#" + std::to_string(k), L);
+    if (N > 1) {
+      Fr* dfull = ctx->scratch_as<Fr>("mle_full", N);
+      comm_allgather_bytes(ctx, it.poly, dfull, L * sizeof(Fr));
+      if (replicated) {
+        Fr* dS = ctx->scratch_as<Fr>("mle_S", N);
+        s_poly_device(ctx, dfull, N, dpr, N, dS, it.point, it.nvars);
+        QG_HIP(hipMemsetAsync(dS + N - 1, 0, sizeof(Fr), ctx->stream));  // h[2M - 1] = 0
+        QG_HIP(hipMemcpyAsync(Sl[k], dS + off, L * sizeof(Fr), hipMemcpyDeviceToDevice,
+                              ctx->stream));
+      } else {
+        s_poly_sharded(ctx, dfull, N, it.point, it.nvars, Sl[k]);
+      }
+    } else {
+      QG_HIP(hipMemsetAsync(Sl[k], 0, L * sizeof(Fr), ctx->stream));
+    }
+    trim_launch(ctx, Sl[k], L, d_len + 2 * k + 1);
+  }
+  // exchange 1: dot parts and local lengths of every rank
+  uint8_t* d_all = ctx->scratch_as<uint8_t>("mlebs_small_all", sm_bytes * W);
+  comm_allgather_bytes(ctx, d_sm, d_all, sm_bytes);
+  std::vector<uint8_t> h_all(sm_bytes * W);
+  QG_HIP(hipMemcpyAsync(h_all.data(), d_all, sm_bytes * W, hipMemcpyDeviceToHost, ctx->stream));
+  ctx->sync();
+  std::vector<Fr> evaluation(K, Fr::zero());
+  std::vector<size_t> Lt(K, 0), Slen(K, 0);
+  for (size_t r = 0; r < W; r++) {
+    const uint8_t* b = h_all.data() + r * sm_bytes;
+    const Fr* parts = reinterpret_cast<const Fr*>(b);
+    const unsigned long long* lens = reinterpret_cast<const unsigned long long*>(b + K * sizeof(Fr));
+    for (size_t k = 0; k < K; k++) {
+      evaluation[k] = evaluation[k] + parts[k];
+      const size_t L = items[k].n;
+      // trimmed_len_global: the largest (rank offset + local length) of a nonzero slice
+      if (lens[2 * k]) Lt[k] = std::max(Lt[k], r * L + (size_t)lens[2 * k]);
+      if (lens[2 * k + 1]) Slen[k] = std::max(Slen[k], r * L + (size_t)lens[2 * k + 1]);
+    }
+  }
+  // the S commitments: one MSM batch over the local parts of the trimmed S
+  std::vector<const Fr*> sp(K);
+  std::vector<size_t> sloc(K);
+  for (size_t k = 0; k < K; k++) {
+    const size_t L = items[k].n, off = rank * L;
+    sp[k] = Sl[k];
+    sloc[k] = Slen[k] > off ? std::min(L, Slen[k] - off) : 0;
+    QG_CHECK(sloc[k] <= srs->n, QG_ERR_INVALID, "Polynomial degree exceeds max degree");
+  }
+  const std::vector<G1Affine> s_comm = msm_device_batch(ctx, srs, sp, sloc);
+  // the transcript steps in item order (mlpcs.rs:100-107)
+  std::vector<Fr> xs(4 * K);
+  for (size_t k = 0; k < K; k++) {
+    const MleOpenItem& it = items[k];
+    std::vector<uint8_t> msg(8 + 32 * it.nvars);
+    u64_to_bytes(it.nvars, msg.data());
+    for (size_t i = 0; i < it.nvars; i++)
+      fr_to_bytes(fr_import(it.point + 4 * i), msg.data() + 8 + 32 * i);
+    transcript_append(state, msg.data(), msg.size());
+    uint8_t b32[32], b64[64];
+    fr_to_bytes(evaluation[k], b32);
+    transcript_append(state, b32, 32);
+    g1_serialize(s_comm[k], b64);
+    transcript_append(state, b64, 64);
+    const Fr r = transcript_draw_fr(state);
+    QG_CHECK(!r.is_zero(), QG_ERR_ASSERT, "challenge r = 0");
+    const Fr r_inv = finv(r);
+    fr_export(evaluation[k], outs[k].evaluation);
+    g1_export(s_comm[k], outs[k].s_comm_xy, &outs[k].s_comm_inf);
+    xs[4 * k] = r;
+    xs[4 * k + 1] = r_inv;
+    xs[4 * k + 2] = r;
+    xs[4 * k + 3] = r_inv;
+  }
+  // the 4K quotients' local scans (kzg_open_sharded, batched): job j = 4k + i
+  // scans this rank's le live coefficients into s_j[0..le); T_j = s_j[0]
+  const size_t J = 4 * K;
+  std::vector<size_t> le(J, 0), glt(J, 0);
+  std::vector<Fr*> sq(J, nullptr);
+  Fr* d_T = ctx->scratch_as<Fr>("mlebs_T", J);
+  QG_HIP(hipMemsetAsync(d_T, 0, J * sizeof(Fr), ctx->stream));
+  for (size_t k = 0; k < K; k++) {
+    const size_t L = items[k].n, off = rank * L;
+    std::vector<ShIn> jobs;
+    for (int i = 0; i < 4; i++) {
+      const size_t j = 4 * k + i;
+      glt[j] = i < 2 ? Lt[k] : Slen[k];
+      le[j] = glt[j] > off ? std::min(L, glt[j] - off) : 0;
+      sq[j] = ctx->scratch_as<Fr>("open_s#" + std::to_string(j), le[j] + 1);
+      if (le[j]) jobs.push_back({i < 2 ? items[k].poly : Sl[k], le[j], xs[j], sq[j]});
+    }
+    {
+      QgTimed tm(ctx, "kzg_division");
+      suffix_horner_batch(ctx, jobs);
+    }
+    for (int i = 0; i < 4; i++) {
+      const size_t j = 4 * k + i;
+      if (le[j])
+        QG_HIP(hipMemcpyAsync(d_T + j, sq[j], sizeof(Fr), hipMemcpyDeviceToDevice, ctx->stream));
+    }
+  }
+  // exchange 2: every rank's T values
+  Fr* d_Tall = ctx->scratch_as<Fr>("mlebs_T_all", J * W);
+  comm_allgather_bytes(ctx, d_T, d_Tall, J * sizeof(Fr));
+  std::vector<Fr> Tall(J * W);
+  QG_HIP(hipMemcpyAsync(Tall.data(), d_Tall, J * W * sizeof(Fr), hipMemcpyDeviceToHost, ctx->stream));
+  ctx->sync();
+  // C_rank = sum_{r' > rank} T_r' x^((r' - rank - 1) L);  y = sum_r T_r x^(r L)
+  std::vector<Fr> ys(J);
+  size_t max_le = 0;
+  for (size_t j = 0; j < J; j++) max_le = std::max(max_le, le[j]);
+  Fr* pw = ctx->scratch_as<Fr>("open_pw", max_le + 1);
+  std::vector<const Fr*> qs(J);
+  std::vector<size_t> qn(J);
+  for (size_t j = 0; j < J; j++) {
+    const size_t L = items[j / 4].n, off = rank * L;
+    const Fr x = xs[j], xL = fpow_small(x, L);
+    Fr C = Fr::zero(), y = Fr::zero();
+    for (size_t r = W; r-- > 0;) {
+      if (r == rank) C = y;
+      y = Tall[r * J + j] + xL * y;
+    }
+    ys[j] = y;
+    if (le[j] > 0) {
+      QgTimed tm(ctx, "kzg_division");
+      const int KP = 64;
+      hipLaunchKernelGGL(k_powers_ml, dim3(div_up(div_up(le[j] + 1, (size_t)KP), ML_BLOCK)),
+                         dim3(ML_BLOCK), 0, ctx->stream, x, le[j] + 1, KP, pw);
+      QG_LAUNCH_CHECK();
+      hipLaunchKernelGGL(k_sh_carry, dim3(div_up(le[j] + 1, ML_BLOCK)), dim3(ML_BLOCK), 0,
+                         ctx->stream, sq[j], le[j], pw, C);
+      QG_LAUNCH_CHECK();
+    }
+    // q_i = s_{i+1} for global i < Lt - 1; this rank's part starts at s + 1
+    qn[j] = (glt[j] > 0 && glt[j] - 1 > off) ? std::min(le[j], glt[j] - 1 - off) : 0;
+    QG_CHECK(qn[j] <= srs->n, QG_ERR_INVALID, "Polynomial degree exceeds max degree");
+    qs[j] = sq[j] + 1;
+  }
+  const std::vector<G1Affine> pis = msm_device_batch(ctx, srs, qs, qn);
+  for (size_t k = 0; k < K; k++) {
+    qg_kzg_opening* o4[4] = {&outs[k].poly_opening, &outs[k].poly_opening_inv,
+                             &outs[k].s_opening, &outs[k].s_opening_inv};
+    for (int i = 0; i < 4; i++) {
+      fr_export(xs[4 * k + i], o4[i]->x);
+      fr_export(ys[4 * k + i], o4[i]->y);
+      g1_export(pis[4 * k + i], o4[i]->proof_xy, &o4[i]->proof_inf);
+    }
+  }
+}
+
 // MLEvalProof::prove (mlpcs.rs:83-124) on a device-resident evaluation vector.
 // Two host round trips per opening, both for values the transcript or the
 // caller needs: the S commitment and the four quotient commitments.  The
@@ -1418,20 +1615,15 @@ static void mle_open_device(qg_ctx* ctx, const qg_srs* srs, const Fr* dpoly, siz
 // Inside a batch the bucketing of MSM i + 1 runs on the side stream beside
 // MSM i's accumulation, and the batch pays one set of reduction launches and
 // one host round trip (msm.hip).  Sharded contexts open item by item.
-struct MleOpenItem {
-  const Fr* poly;
-  size_t n;
-  const uint64_t* point;
-  size_t nvars;
-  bool unchanged;
-  uint64_t id;
-  size_t off;
-};
 
 static void mle_open_batch_device(qg_ctx* ctx, const qg_srs* srs,
                                   const std::vector<MleOpenItem>& items, uint8_t state[32],
                                   qg_mle_proof* outs) {
   const size_t K = items.size();
+  // QG_OPEN_BATCH_SHARDED=0: a sharded context opens item by item (A/B runs)
+  const char* sb = getenv("QG_OPEN_BATCH_SHARDED");
+  if (ctx->sharded && K > 1 && !(sb && atoi(sb) == 0))
+    return mle_open_batch_sharded(ctx, srs, items, state, outs);
   if (ctx->sharded || K <= 1) {
     for (size_t k = 0; k < K; k++)
       mle_open_device(ctx, srs, items[k].poly, items[k].n, items[k].point, items[k].nvars, state,

@@ -1734,6 +1734,37 @@ static G1Affine msm_finish_ranks(qg_ctx* ctx, G1Xyzz acc) {
   return xyzz_to_affine(acc);
 }
 
+// per-rank XYZZ partials of a batch -> the MSMs over all ranks, affine: one
+// allgather of the k partials (a sharded batch of openings exchanges once per
+// MSM batch, not once per MSM)
+static std::vector<G1Affine> msm_finish_ranks_batch(qg_ctx* ctx, const std::vector<G1Xyzz>& loc) {
+  const size_t k = loc.size();
+  std::vector<G1Affine> res(k);
+  if (!ctx->sharded || k == 0) {
+    for (size_t i = 0; i < k; i++) res[i] = xyzz_to_affine(loc[i]);
+    return res;
+  }
+  if (k == 1) {
+    res[0] = msm_finish_ranks(ctx, loc[0]);
+    return res;
+  }
+  const size_t W = (size_t)ctx->world;
+  G1Xyzz* d_send = ctx->scratch_as<G1Xyzz>("msm_comm_send", k);
+  G1Xyzz* d_recv = ctx->scratch_as<G1Xyzz>("msm_comm_recv", k * W);
+  QG_HIP(hipMemcpyAsync(d_send, loc.data(), k * sizeof(G1Xyzz), hipMemcpyHostToDevice, ctx->stream));
+  comm_allgather_bytes(ctx, d_send, d_recv, k * sizeof(G1Xyzz));
+  std::vector<G1Xyzz> all(k * W);
+  QG_HIP(hipMemcpyAsync(all.data(), d_recv, k * W * sizeof(G1Xyzz), hipMemcpyDeviceToHost,
+                        ctx->stream));
+  ctx->sync();
+  for (size_t i = 0; i < k; i++) {
+    G1Xyzz acc = G1Xyzz::infinity();
+    for (size_t r = 0; r < W; r++) acc = xyzz_add(acc, all[r * k + i]);
+    res[i] = xyzz_to_affine(acc);
+  }
+  return res;
+}
+
 // k MSMs over the same SRS (KZG openings of one proof); results per MSM,
 // summed over the RCCL ranks when a communicator is attached
 //
@@ -1848,9 +1879,7 @@ std::vector<G1Affine> msm_device_batch(qg_ctx* ctx, const qg_srs* srs,
                 i, chk.size(), ns[i]);
     }
   }
-  std::vector<G1Affine> res(local.size());
-  for (size_t i = 0; i < local.size(); i++) res[i] = msm_finish_ranks(ctx, local[i]);
-  return res;
+  return msm_finish_ranks_batch(ctx, local);
 }
 
 // MSM of host-resident scalars (qg_kzg_commit / qg_msm_g1): the scalars go up

@@ -260,9 +260,26 @@ class KZG:
         """K openings [(vec, n, eval_point, unchanged), ...] in one call
         (qg_mle_open_batch_dev): the same proofs and transcript as K successive
         open_dev calls, with the S and quotient commitments as two MSM batches.
-        Sharded devices open item by item (each rank's shard SRS)."""
-        if self.dev.world > 1 or len(items) <= 1:
+        Sharded devices batch each run of consecutive items of one local length
+        (they commit against one SRS shard; mle_open_batch_sharded): the runs
+        keep the item order, so the transcript is the same."""
+        if len(items) <= 1:
             return [self.open_dev(v, n, pt, transcript, unch) for v, n, pt, unch in items]
+        if self.dev.world > 1:
+            out, i = [], 0
+            while i < len(items):
+                j = i
+                while j < len(items) and items[j][1] == items[i][1]:
+                    j += 1
+                out += self._open_batch(items[i:j], transcript, self.srs_for(items[i][1]))
+                i = j
+            return out
+        return self._open_batch(items, transcript, self.srs)
+
+    def _open_batch(self, items, transcript: Transcript, srs) -> list:
+        if len(items) == 1:
+            v, n, pt, unch = items[0]
+            return [self.open_dev(v, n, pt, transcript, unch)]
         k = len(items)
         arr = (MleOpenItem * k)()
         pts = []
@@ -272,7 +289,7 @@ class KZG:
             arr[i] = MleOpenItem(vec.h.value, n, a.ctypes.data_as(C.POINTER(C.c_uint64)), len(pt),
                                  1 if unch else 0, 0)
         outs = (MleProof * k)()
-        check(lib().qg_mle_open_batch_dev(self.dev.h, self.srs.h, arr, k, transcript.c_state(),
+        check(lib().qg_mle_open_batch_dev(self.dev.h, srs.h, arr, k, transcript.c_state(),
                                           outs), self.dev.h)
         return [MLEvalProof(list(pt), fr_from_mont_limbs(list(o.evaluation)),
                             g1_from_abi(o.s_comm_xy, o.s_comm_inf),

@@ -347,3 +347,65 @@ def test_sharded_hyperplonk_16_column(world, rows):
         assert state == ot.state
         vt = ho.hyperplonk_verify(to_oracle(proof), ohp.to_vk(), opcs)
         assert vt.state == ot.state
+
+
+@pytest.mark.parametrize("world", [2, 4])
+def test_sharded_mle_open_batch_matches_sequential(world):
+    """qg_mle_open_batch_dev on a sharded context (mle_open_batch_sharded: four
+    exchanges per batch) equals the item-by-item sharded openings
+    (QG_OPEN_BATCH_SHARDED=0) and the single-context batch, proof for proof,
+    with the same transcript state, at 2^14 evaluations: full vectors, a
+    zero tail ending in a lower rank's slice, a vector trimming to one entry,
+    a smaller variable count, and one vector opened twice."""
+    import os
+    import quill_amd as q
+    from quill_amd import KZG, Transcript
+    rnd = random.Random(7700 + world)
+    tau = rnd.randrange(R)
+    shapes = [(14, None), (14, (1 << 14) - 3000), (14, 1), (12, None), (13, None)]
+    polys = []
+    for nv, live in shapes:
+        p = [rnd.randrange(R) for _ in range(1 << nv)]
+        if live is not None:
+            p = p[:live] + [0] * ((1 << nv) - live)
+        polys.append(p)
+    items = [(i, [rnd.randrange(R) for _ in range(shapes[i][0])]) for i in range(len(shapes))]
+    items.append((0, [rnd.randrange(R) for _ in range(14)]))
+    dev0 = q.Device(0)
+    kz = KZG.trusted_setup(1 << 14, tau, dev0)
+    vs = [q.DeviceVec.from_list(dev0, p) for p in polys]
+    t_ref = Transcript(b"shard-batch")
+    ref = kz.open_batch_dev([(vs[i], len(polys[i]), pt, False) for i, pt in items], t_ref)
+    for v in vs:
+        v.close()
+    kz.srs.close()
+    dev0.close()
+
+    def fn(dev, rank, world):
+        kzg = KZG.trusted_setup(1 << 14, tau, dev)  # one SRS shard per local length
+        vecs = []
+        for p in polys:
+            L = len(p) // world
+            vecs.append(q.DeviceVec.from_list(dev, p[rank * L:(rank + 1) * L]))
+        batch = [(vecs[i], len(vecs[i]), pt, False) for i, pt in items]
+        out = []
+        for mode in ("1", "0"):
+            bar.wait()  # every rank is between calls: one sets the mode for all
+            if rank == 0:
+                os.environ["QG_OPEN_BATCH_SHARDED"] = mode
+            bar.wait()
+            t = Transcript(b"shard-batch")
+            out.append((kzg.open_batch_dev(batch, t), t.state))
+        for v in vecs:
+            v.close()
+        kzg.close()
+        return out
+
+    bar = threading.Barrier(world)
+    try:
+        outs = run_ranks(world, fn)
+    finally:
+        os.environ.pop("QG_OPEN_BATCH_SHARDED", None)
+    for (bat, sb), (seq, ss) in outs:
+        assert bat == seq and sb == ss
+        assert bat == ref and sb == t_ref.state
