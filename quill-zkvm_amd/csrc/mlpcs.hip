@@ -530,6 +530,143 @@ __global__ void k_s_combine_br(const Fr* __restrict__ F, const Fr* __restrict__ 
   H[k] = from29(canon29(mul29(v, to29(twMb[k]))));
 }
 
+// ---- the inverse transform at half size (round 6) ------------------------
+// With P_j = F_j G_{-j} + F_{-j} G_j (P_{-j} = P_j) the S polynomial is
+// S_k = p_{k+1} (k < M - 1) for p = IDFT_n(P): H_j = w^{j(M-1)} P_j / n only
+// shifts p by M - 1, and p is even (p_{-d} = p_d).  Split p by parity
+// (N2 = n / 2, w2 = w^2):
+//   p_{2e}     = a_e / n,  a = IDFT_N2(A),  A_j = P_j + P_{j+N2}
+//   p_{2e+1}   = b_e / n,  b = IDFT_N2(B),  B_j = (P_j - P_{j+N2}) w^{-j}
+// A is even (A_{N2-j} = A_j), so a is even; B_{N2-j} = w2^j B_j, so
+// b_{-e} = b_{e-1}.  One half-size inverse of D = A + B gives d = a + b, and
+// d_e - d_{-e} = (a_e + b_e) - (a_e + b_{e-1}) = b_e - b_{e-1}: b is b_0 plus
+// a prefix sum of d_e - d_{N2-e}, with b_0 = sum_j B_j, and a = d - b.  So the
+// size-n inverse NTT becomes a size-n/2 one plus O(n) combine / scan passes.
+// In the bit-reversed domain P_j and P_{j+N2} sit at 2t and 2t + 1
+// (t = bitrev_{N2}(j)), and D_j is needed at position t of the half-size
+// DIT's bit-reversed input: each thread makes one D from two adjacent P.
+// twD[t] = w^{-bitrev(t)} n^-1 2^266, c1 = n^-1 2^266: mul29 of the 2^251-scaled
+// values lands in arkworks form with 1/n folded in (as twM does).
+// bpart[block] = the block's sum of B_j / n (for b_0).
+__global__ void __launch_bounds__(256)
+    k_s_combine_half(const Fr* __restrict__ F, const Fr* __restrict__ G, const Fr* __restrict__ twD,
+                     L9 c1, int logn, Fr* __restrict__ D, Fr* __restrict__ bpart) {
+  __shared__ Fr red[256];
+  const size_t t = (size_t)blockIdx.x * blockDim.x + threadIdx.x;
+  const size_t N2 = (size_t)1 << (logn - 1);
+  Fr bn = Fr::zero();
+  if (t < N2) {
+    R29 P[2];
+#pragma unroll
+    for (int h = 0; h < 2; h++) {
+      const size_t q = 2 * t + h;
+      size_t kn = 0;
+      if (q) {
+        const int hb = 63 - __clzll((unsigned long long)q);
+        kn = q ^ (((size_t)1 << hb) - 1);
+      }
+      const R29 a = to29(F[q]), bb = to29(G[kn]), c = to29(F[kn]), d = to29(G[q]);
+      P[h] = red2p29(add29(mul29(a, bb), mul29(c, d)));  // < 2p, x 2^251
+    }
+    const R29 A = add29(P[0], P[1]);                                      // < 4p, lazy
+    const R29 B = normfull29(subk29(P[0], P[1], F29P<FrP>::K2));          // < 4p, normalized
+    const R29 An = mul29(A, R29::from_l9(c1));
+    const R29 Bn = mul29(B, to29(twD[t]));
+    D[t] = from29(canon29(red2p29(add29(An, Bn))));
+    bn = from29(canon29(Bn));
+  }
+  red[threadIdx.x] = bn;
+  __syncthreads();
+  for (int o = 128; o > 0; o >>= 1) {
+    if ((int)threadIdx.x < o) red[threadIdx.x] = red[threadIdx.x] + red[threadIdx.x + o];
+    __syncthreads();
+  }
+  if (threadIdx.x == 0) bpart[blockIdx.x] = red[0];
+}
+
+// out[0] = sum of in[0 .. n) (one block)
+__global__ void __launch_bounds__(1024) k_fr_sum(const Fr* __restrict__ in, size_t n, Fr* __restrict__ out) {
+  __shared__ Fr red[1024];
+  Fr acc = Fr::zero();
+  for (size_t i = threadIdx.x; i < n; i += 1024) acc = acc + in[i];
+  red[threadIdx.x] = acc;
+  __syncthreads();
+  for (int o = 512; o > 0; o >>= 1) {
+    if ((int)threadIdx.x < o) red[threadIdx.x] = red[threadIdx.x] + red[threadIdx.x + o];
+    __syncthreads();
+  }
+  if (threadIdx.x == 0) out[0] = red[0];
+}
+
+// b_e = b_0 + sum_{t=1..e} (d_t - d_{N2-t}), e = 0 .. E: tiles of SYM_TILE
+// entries, a local inclusive prefix per tile (Q) and the tile totals (tot)
+static constexpr int SYM_PER = 8;
+static constexpr int SYM_TILE = 256 * SYM_PER;
+__global__ void __launch_bounds__(256)
+    k_sym_tiles(const Fr* __restrict__ d, size_t N2, size_t E, Fr* __restrict__ Q, Fr* __restrict__ tot) {
+  __shared__ Fr sh[256];
+  const size_t e0 = (size_t)blockIdx.x * SYM_TILE + (size_t)threadIdx.x * SYM_PER;
+  Fr v[SYM_PER];
+  Fr run = Fr::zero();
+#pragma unroll
+  for (int k = 0; k < SYM_PER; k++) {
+    const size_t e = e0 + k;
+    Fr dl = Fr::zero();
+    if (e >= 1 && e <= E) dl = d[e] - d[N2 - e];
+    run = run + dl;
+    v[k] = run;
+  }
+  sh[threadIdx.x] = run;
+  __syncthreads();
+  for (int o = 1; o < 256; o <<= 1) {  // Hillis-Steele inclusive scan of the thread totals
+    const Fr add = (int)threadIdx.x >= o ? sh[threadIdx.x - o] : Fr::zero();
+    __syncthreads();
+    sh[threadIdx.x] = sh[threadIdx.x] + add;
+    __syncthreads();
+  }
+  const Fr before = threadIdx.x ? sh[threadIdx.x - 1] : Fr::zero();
+#pragma unroll
+  for (int k = 0; k < SYM_PER; k++)
+    if (e0 + k <= E) Q[e0 + k] = before + v[k];
+  if (threadIdx.x == 255) tot[blockIdx.x] = sh[255];
+}
+
+// tot[i] <- b_0 + sum_{i' < i} tot[i'] (one block)
+__global__ void __launch_bounds__(1024) k_sym_top(Fr* __restrict__ tot, int ntiles, const Fr* __restrict__ b0) {
+  __shared__ Fr sh[1024];
+  const int per = (ntiles + 1023) / 1024;
+  const int base = threadIdx.x * per;
+  Fr sum = Fr::zero();
+  for (int k = 0; k < per; k++)
+    if (base + k < ntiles) sum = sum + tot[base + k];
+  sh[threadIdx.x] = sum;
+  __syncthreads();
+  for (int o = 1; o < 1024; o <<= 1) {
+    const Fr add = (int)threadIdx.x >= o ? sh[threadIdx.x - o] : Fr::zero();
+    __syncthreads();
+    sh[threadIdx.x] = sh[threadIdx.x] + add;
+    __syncthreads();
+  }
+  Fr run = b0[0] + (threadIdx.x ? sh[threadIdx.x - 1] : Fr::zero());
+  for (int k = 0; k < per; k++)
+    if (base + k < ntiles) {
+      const Fr t = tot[base + k];
+      tot[base + k] = run;
+      run = run + t;
+    }
+}
+
+// S_{2e-1} = p_{2e} = d_e - b_e (e >= 1), S_{2e} = p_{2e+1} = b_e, for the
+// k = 2e - 1, 2e below M - 1
+__global__ void k_sym_out(const Fr* __restrict__ d, const Fr* __restrict__ Q, const Fr* __restrict__ tot,
+                          size_t M, size_t E, Fr* __restrict__ S) {
+  const size_t e = (size_t)blockIdx.x * blockDim.x + threadIdx.x;
+  if (e > E) return;
+  const Fr b = tot[e / SYM_TILE] + Q[e];
+  if (2 * e + 2 <= M) S[2 * e] = b;                   // k = 2e <= M - 2
+  if (e >= 1 && 2 * e + 1 <= M) S[2 * e - 1] = d[e] - b;  // k = 2e - 1 <= M - 2
+}
+
 __global__ void k_powers_ml(Fr base, size_t n, int K, Fr* out) {
   size_t t = (size_t)blockIdx.x * blockDim.x + threadIdx.x;
   size_t i0 = t * (size_t)K;
@@ -710,14 +847,40 @@ static void s_poly_device(qg_ctx* ctx, const Fr* f, size_t nf, const Fr* g, size
   // (logn, M) only: cached per context in one of four slots by (logn, M), so a
   // prover alternating between a few opening sizes (HyperPlonk: the witness
   // and its public rows) does not rebuild it per opening.
-  const std::string twm_key = std::to_string(logn) + ":" + std::to_string(M);
-  bool twm_hit = false;  // the memo below decides; the LRU only picks the slot
-  const std::string twm_slot = "ntt_twM#" + std::to_string(ctx->twm_lru.slot_for(twm_key, &twm_hit));
-  Fr* twM = ctx->scratch_as<Fr>(twm_slot, n);
+  // QG_S_FULL_INVERSE=1: the size-n inverse (k_s_combine_br + DIT of H) instead
+  // of the half-size one (A/B runs); read per call
+  const char* fi = getenv("QG_S_FULL_INVERSE");
+  const bool half_inverse = !(fi && atoi(fi) != 0);
   Fr *tw, *twi;
   ntt_twiddles(ctx, logn, &tw, &twi);
-  const std::string twm_memo = ctx->arena.derived_key(twm_key, 1, ctx->scratch_gen(twm_slot));
-  if (!ctx->arena.check(twm_slot, twm_memo)) {
+  Fr* twM = nullptr;
+  Fr* twD = nullptr;
+  if (half_inverse) {
+    // w^{-j} n^-1 2^266 for j < n / 2 in bit-reversed order: depends on logn only
+    twD = ctx->scratch_as<Fr>("ntt_twD", n / 2);
+    const std::string memo = ctx->arena.derived_key(std::to_string(logn), 1, ctx->scratch_gen("ntt_twD"));
+    if (!ctx->arena.check("ntt_twD", memo)) {
+      const Fr wi = finv(root_of_unity(logn));
+      const int K = 64;
+      hipLaunchKernelGGL(k_powers_ml, dim3(div_up(div_up(n / 2, K), 256)), dim3(256), 0, ctx->stream,
+                         wi, n / 2, K, H);
+      QG_LAUNCH_CHECK();
+      const Fr ninv_plain = from_mont(finv(from_u64<FrP>(n)));
+      const L9 c9 = l9_of29(ml_plain_mul(ninv_plain, pow2_mod_plain<FrP>(271)));
+      hipLaunchKernelGGL(k_fr_to261_br, dim3(div_up(n / 2, 256)), dim3(256), 0, ctx->stream, H,
+                         logn - 1, c9, twD);
+      QG_LAUNCH_CHECK();
+      ctx->arena.commit("ntt_twD", memo);
+    }
+  }
+  const std::string twm_key = std::to_string(logn) + ":" + std::to_string(M);
+  bool twm_hit = false;  // the memo below decides; the LRU only picks the slot
+  const std::string twm_slot =
+      half_inverse ? std::string() : "ntt_twM#" + std::to_string(ctx->twm_lru.slot_for(twm_key, &twm_hit));
+  if (!half_inverse) twM = ctx->scratch_as<Fr>(twm_slot, n);
+  const std::string twm_memo =
+      half_inverse ? std::string() : ctx->arena.derived_key(twm_key, 1, ctx->scratch_gen(twm_slot));
+  if (!half_inverse && !ctx->arena.check(twm_slot, twm_memo)) {
     const Fr w = root_of_unity(logn);
     const Fr wM = fpow_small(w, (uint64_t)(M - 1));
     const int K = 64;
@@ -789,12 +952,43 @@ static void s_poly_device(qg_ctx* ctx, const Fr* f, size_t nf, const Fr* g, size
   } else {
     ntt_run(ctx, true, g, ng, G, tw, "ntt_tw", logn, 0, 0, nullptr);
   }
-  hipLaunchKernelGGL(k_s_combine_br, dim3(div_up(n, 256)), dim3(256), 0, ctx->stream, F, G, twM,
-                     logn, H);
+  if (!half_inverse) {
+    hipLaunchKernelGGL(k_s_combine_br, dim3(div_up(n, 256)), dim3(256), 0, ctx->stream, F, G, twM,
+                       logn, H);
+    QG_LAUNCH_CHECK();
+    // inverse DIT of H (bit-reversed in, natural out); the last pass writes only
+    // h[M .. 2M-1) = S
+    ntt_run(ctx, false, H, n, H, twi, "ntt_twi", logn, M, 2 * M - 1, S);
+    return;
+  }
+  // the inverse at half size (k_s_combine_half): D into H's first half,
+  // the half-size DIT in place, then b by a prefix scan into S
+  const size_t N2 = n / 2;
+  const unsigned cblocks = div_up(N2, 256);
+  Fr* bpart = ctx->scratch_as<Fr>("s_bpart", (size_t)cblocks + 1);
+  const Fr ninv_plain = from_mont(finv(from_u64<FrP>(n)));
+  const L9 c1 = l9_of29(ml_plain_mul(ninv_plain, pow2_mod_plain<FrP>(266)));
+  hipLaunchKernelGGL(k_s_combine_half, dim3(cblocks), dim3(256), 0, ctx->stream, F, G, twD, c1, logn,
+                     H, bpart);
   QG_LAUNCH_CHECK();
-  // inverse DIT of H (bit-reversed in, natural out); the last pass writes only
-  // h[M .. 2M-1) = S
-  ntt_run(ctx, false, H, n, H, twi, "ntt_twi", logn, M, 2 * M - 1, S);
+  hipLaunchKernelGGL(k_fr_sum, dim3(1), dim3(1024), 0, ctx->stream, bpart, (size_t)cblocks,
+                     bpart + cblocks);
+  QG_LAUNCH_CHECK();
+  Fr *twh, *twhi;
+  ntt_twiddles(ctx, logn - 1, &twh, &twhi, "ntt_twh");
+  ntt_run(ctx, false, H, N2, H, twhi, "ntt_twhi", logn - 1, 0, 0, nullptr);
+  const size_t E = (M - 1) / 2;  // b_e, a_e for e <= E cover S_0 .. S_{M-2}
+  const size_t ntiles = E / SYM_TILE + 1;
+  QG_CHECK(ntiles <= 1024 * 64, QG_ERR_UNSUPPORTED, "S-polynomial scan too large");
+  Fr* tot = ctx->scratch_as<Fr>("s_symtot", ntiles);
+  hipLaunchKernelGGL(k_sym_tiles, dim3((unsigned)ntiles), dim3(256), 0, ctx->stream, H, N2, E, G, tot);
+  QG_LAUNCH_CHECK();
+  hipLaunchKernelGGL(k_sym_top, dim3(1), dim3(1024), 0, ctx->stream, tot, (int)ntiles,
+                     bpart + cblocks);
+  QG_LAUNCH_CHECK();
+  hipLaunchKernelGGL(k_sym_out, dim3(div_up(E + 1, 256)), dim3(256), 0, ctx->stream, H, G, tot, M, E,
+                     S);
+  QG_LAUNCH_CHECK();
 }
 
 // highest nonzero index + 1: per-thread max over a grid-stride range of

@@ -107,3 +107,46 @@ def test_residue_split_s_polynomial(nvars, W):
     for d in range(W):  # all-to-all, then the sum on rank d
         got = [sum(sends[s][d][m] for s in range(W)) % R for m in range(L)]
         assert got == S[d * L:(d + 1) * L], (d, W)
+
+
+def test_half_size_inverse_identity():
+    """The half-size inverse of s_poly_device (k_s_combine_half, k_sym_*,
+    round 6), restated on the CPU: with P_j = F_j G_-j + F_-j G_j (even), D_j =
+    (P_j + P_{j+N2}) + (P_j - P_{j+N2}) w^-j, d = IDFT_N2(D), b_e = b_0 +
+    sum_{t<=e} (d_t - d_{N2-t}) with b_0 = sum_j B_j, a = d - b: S_{2e-1} = a_e
+    / n and S_{2e} = b_e / n equal compute_s_polynomial (ipa.rs:122-157) for
+    even, odd, power-of-two and ragged lengths (n = 2^ceil(log2(2M - 1)))."""
+    import random
+    rnd = random.Random(66)
+    R = o.R_MOD
+
+    def dft(a, w):
+        return [sum(a[i] * pow(w, i * j, R) for i in range(len(a))) % R for j in range(len(a))]
+    for M in (2, 3, 5, 8, 13, 16, 21):
+        f = [rnd.randrange(R) for _ in range(M)]
+        g = [rnd.randrange(R) for _ in range(rnd.randrange(1, M + 1))]
+        S = o.compute_s_polynomial(f, g)
+        S = S + [0] * (M - 1 - len(S))
+        logn = 1
+        while (1 << logn) < 2 * M - 1:
+            logn += 1
+        n, N2 = 1 << logn, 1 << (logn - 1)
+        w = o.two_adic_root(logn)
+        wi = pow(w, R - 2, R)
+        F = dft(f + [0] * (n - M), w)
+        G = dft(g + [0] * (n - len(g)), w)
+        P = [(F[j] * G[-j % n] + F[-j % n] * G[j]) % R for j in range(n)]
+        ninv = pow(n, R - 2, R)
+        B = [(P[j] - P[j + N2]) * pow(wi, j, R) % R for j in range(N2)]
+        D = [(P[j] + P[j + N2] + B[j]) * ninv % R for j in range(N2)]
+        d = dft(D, wi * wi % R)
+        b = [sum(B) * ninv % R]
+        for e in range(1, (M - 1) // 2 + 1):
+            b.append((b[-1] + d[e] - d[N2 - e]) % R)
+        out = [None] * (M - 1)
+        for e, be in enumerate(b):
+            if 2 * e + 2 <= M:
+                out[2 * e] = be
+            if e >= 1 and 2 * e + 1 <= M:
+                out[2 * e - 1] = (d[e] - be) % R
+        assert out == S, M
