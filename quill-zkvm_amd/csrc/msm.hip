@@ -1439,8 +1439,16 @@ static MsmRun msm_accumulate_phase(qg_ctx* ctx, const qg_srs* srs, const Fr* d_s
       // (own-SRS MSMs, profiles/r04_msm_small_elog.txt: 2^20 / 2^18 / 2^16 at
       // c = 17 / 16 / 15 take 1.73 / 1.09 / 0.73 ms with the thread rule alone,
       // 1.69 / 0.87 / 0.69 ms with 64 / 32 / 32 entries per chunk)
+      // In a batch on the side streams (HyperPlonk's openings: 2^20-2^23-scalar
+      // MSMs on the c = 20 tables, many buckets per MSM) at most ~2 chunks per
+      // bucket: fewer partial slots to merge, HyperPlonk reduce 73.5 / 73.9 ->
+      // 63.5 / 63.3 ms per proof, proof 879.7 / 878.3 -> 872.0 / 871.7 ms
+      // (profiles/r06e_msm_cpb_ab.txt); a lone MSM keeps 4 (the 2^24 headline
+      // measured no better with 2).  QG_MSM_CPB overrides (A/B runs).
       int emin = 0;
-      while (emin < 7 && ((size_t)1 << emin) * 4 * nb < max_entries) emin++;
+      size_t cpb = side ? 2 : 4;
+      if (const char* ov = getenv("QG_MSM_CPB")) cpb = (size_t)std::max(1, atoi(ov));
+      while (emin < 7 && ((size_t)1 << emin) * cpb * nb < max_entries) emin++;
       elog = std::max(elog, emin);
       L = 1u << elog;
     }
