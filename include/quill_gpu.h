@@ -226,7 +226,14 @@ int qg_mle_open_dev_ex(qg_ctx* ctx, const qg_srs* srs, const qg_buf* poly, size_
  * on (poly, point) only and no quotient commitment enters the transcript
  * (mlpcs.rs:83-124), so the device runs the K S commitments as one MSM batch,
  * the K transcript steps on the host, then all 4K quotient commitments as one
- * MSM batch.  HyperPlonk's openings of one trace (proof.rs:203-224). */
+ * MSM batch.  HyperPlonk's openings of one trace (proof.rs:203-224).
+ * HBM: the call holds every item's S (M - 1 Fr) and four quotient vectors
+ * plus one partial-sum slot set per MSM until it returns (~1 GB per item of
+ * 2^20 evaluations, mostly the partial slots); per-item scratch beyond the
+ * first 16 items is freed when it returns, the first 16 items' is kept for
+ * the next call.  A sharded
+ * context (qg_ctx_attach_comm) batches too: all items must then share one SRS
+ * shard (the Python mirror batches each run of equal local length). */
 typedef struct qg_mle_open_item {
   const qg_buf* poly;     /* device evaluations (first n entries) */
   size_t n;

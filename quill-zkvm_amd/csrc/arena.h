@@ -75,6 +75,13 @@ struct ScratchArena {
     return false;
   }
   void commit(const std::string& tag, const std::string& key) { memo[tag] = key; }
+  // free one slot now (no-op when absent); its generation is gone with it
+  void release(const std::string& slot) {
+    auto it = slots.find(slot);
+    if (it == slots.end()) return;
+    backend.release(it->second.p);
+    slots.erase(it);
+  }
   void release_all() {
     for (auto& kv : slots) backend.release(kv.second.p);
     slots.clear();

@@ -1510,6 +1510,27 @@ struct MleOpenItem {
   size_t off;
 };
 
+// Per-item scratch of a batch of openings (S vectors, quotient vectors, eq
+// points) and the per-MSM slots of its MSM batches (msm.hip: partials, owners,
+// bucket starts, plan words) stay allocated for the next batch: HyperPlonk
+// reuses them trace after trace.  Beyond a working set of OPEN_KEEP items
+// (4 OPEN_KEEP MSMs) they are freed when the batch ends (a batch of
+// 256 items at 2^20 would otherwise pin ~70-80 GB for the context's lifetime).
+static constexpr size_t OPEN_KEEP = 16;
+static void open_batch_trim_scratch(qg_ctx* ctx, size_t K) {
+  for (size_t k = OPEN_KEEP; k < K; k++) {
+    ctx->arena.release("mleb_S#" + std::to_string(k));
+    ctx->arena.release("mleb_Sl#" + std::to_string(k));
+    ctx->arena.release("mleb_z#" + std::to_string(k));
+    ctx->arena.release("open_y#" + std::to_string(k));
+  }
+  for (size_t j = 4 * OPEN_KEEP; j < 4 * K; j++) {
+    ctx->arena.release("open_s#" + std::to_string(j));
+    for (const char* m : {"msm_partial#", "msm_owner#", "msm_bstart#", "msm_misc#"})
+      ctx->arena.release(m + std::to_string(j));
+  }
+}
+
 // K openings on a sharded context: mle_open_sharded's data flow, batched the
 // way mle_open_batch_device batches the single-context one.  Per item the eq
 // table, the local dot, the gathered vector's residue-split S slice and the
@@ -1695,6 +1716,7 @@ static void mle_open_batch_sharded(qg_ctx* ctx, const qg_srs* srs,
       g1_export(pis[4 * k + i], o4[i]->proof_xy, &o4[i]->proof_inf);
     }
   }
+  open_batch_trim_scratch(ctx, K);
 }
 
 // MLEvalProof::prove (mlpcs.rs:83-124) on a device-resident evaluation vector.
@@ -1936,6 +1958,7 @@ static void mle_open_batch_device(qg_ctx* ctx, const qg_srs* srs,
       g1_export(pis[4 * k + i], o4[i]->proof_xy, &o4[i]->proof_inf);
     }
   }
+  open_batch_trim_scratch(ctx, K);
 }
 
 }  // namespace qg
