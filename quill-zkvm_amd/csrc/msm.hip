@@ -641,10 +641,9 @@ QG_DEV uint4 msm_entries4(const uint32_t* __restrict__ entries, uint32_t e, uint
 template <bool PF>
 __global__ void __launch_bounds__(MSM_BLOCK) __attribute__((amdgpu_waves_per_eu(PF ? 3 : 4)))
     k_msm_accumulate(const MsmPt* __restrict__ table, const uint32_t* __restrict__ entries,
-                     const uint32_t* __restrict__ bstart, uint32_t nb, uint32_t lgL,
+                     const uint32_t* __restrict__ bstart, uint32_t nb, uint32_t L,
                      X29Raw* __restrict__ partial, uint32_t* __restrict__ owner) {
   const uint32_t t = blockIdx.x * blockDim.x + threadIdx.x;
-  const uint32_t L = 1u << lgL;
   const uint32_t total = bstart[nb];
   const uint64_t e0w = (uint64_t)t * L;
   if (e0w >= total) return;
@@ -652,7 +651,7 @@ __global__ void __launch_bounds__(MSM_BLOCK) __attribute__((amdgpu_waves_per_eu(
   const uint32_t e1 = total - e0 < L ? total : e0 + L;
   // the thread index is not kept live through the loop (it cost the
   // non-prefetching form one VGPR spilled and reloaded per addition): a flush
-  // recovers it from the chunk end, t = (e1 - 1) >> lgL; chunks start at
+  // recovers it from the chunk end, t = (e1 - 1) / L; chunks start at
   // multiples of L (>= 4), so the group phase is e & 3
   // bucket of entry e0: the largest b with bstart[b] <= e0 (b < nb)
   uint32_t lo = 0, hi = nb;
@@ -688,7 +687,7 @@ __global__ void __launch_bounds__(MSM_BLOCK) __attribute__((amdgpu_waves_per_eu(
       if (e + 5 < e1) g1 = msm_entries4(entries, e + 5, e1);
     }
     if (e == next) {
-      msm_flush(partial, owner, ((e1 - 1) >> lgL) + b, b, acc, inf);
+      msm_flush(partial, owner, (e1 - 1) / L + b, b, acc, inf);
       inf = true;
       do {
         b++;
@@ -710,7 +709,7 @@ __global__ void __launch_bounds__(MSM_BLOCK) __attribute__((amdgpu_waves_per_eu(
     ay = by;
     pinf = qinf;
   }
-  msm_flush(partial, owner, ((e1 - 1) >> lgL) + b, b, acc, inf);
+  msm_flush(partial, owner, (e1 - 1) / L + b, b, acc, inf);
   return;
   }
   // entries arrive four at a time (one 16-B load per group of four, the next
@@ -724,7 +723,7 @@ __global__ void __launch_bounds__(MSM_BLOCK) __attribute__((amdgpu_waves_per_eu(
     const uint32_t ent = k == 0 ? cur.x : k == 1 ? cur.y : k == 2 ? cur.z : cur.w;
     if (k == 3) cur = nxt;
     if (e == next) {  // bucket boundary (at most a few per thread)
-      msm_flush(partial, owner, ((e1 - 1) >> lgL) + b, b, acc, inf);
+      msm_flush(partial, owner, (e1 - 1) / L + b, b, acc, inf);
       inf = true;
       do {
         b++;
@@ -744,7 +743,7 @@ __global__ void __launch_bounds__(MSM_BLOCK) __attribute__((amdgpu_waves_per_eu(
     }
     if (!x29_acc_madd_tp(acc, ax, ay)) x29_acc_madd_exc(acc, ax, ay, &inf);
   }
-  msm_flush(partial, owner, ((e1 - 1) >> lgL) + b, b, acc, inf);
+  msm_flush(partial, owner, (e1 - 1) / L + b, b, acc, inf);
 }
 
 // Cooperative row gathers (COOP).  One 16-B load per lane of five per row
@@ -806,14 +805,13 @@ __device__ __forceinline__ bool msm_coop_read(const uint4* wbuf, uint32_t lane, 
 #endif
 __global__ void __launch_bounds__(MSM_BLOCK) __attribute__((amdgpu_waves_per_eu(QG_COOP_WPE)))
     k_msm_accumulate_coop(const MsmPt* __restrict__ table, const uint32_t* __restrict__ entries,
-                          const uint32_t* __restrict__ bstart, uint32_t nb, uint32_t lgL,
+                          const uint32_t* __restrict__ bstart, uint32_t nb, uint32_t L,
                           X29Raw* __restrict__ partial, uint32_t* __restrict__ owner) {
 #if defined(__HIP_DEVICE_COMPILE__)
   __shared__ uint4 img[MSM_BLOCK / 64][64 * 8];
   const uint32_t t = blockIdx.x * blockDim.x + threadIdx.x;
   const uint32_t lane = threadIdx.x & 63u;
   uint4* wbuf = img[threadIdx.x >> 6];
-  const uint32_t L = 1u << lgL;
   const uint32_t total = bstart[nb];
   const uint64_t e0w = (uint64_t)t * L;
   // whole waves stay or leave together (the DMA steps are wave-wide); lanes
@@ -853,7 +851,7 @@ __global__ void __launch_bounds__(MSM_BLOCK) __attribute__((amdgpu_waves_per_eu(
     if (i + 1 < L) msm_coop_issue(wbuf, table, lane, e + 1 < e1 ? en : 0u);
     if (e >= e1) continue;
     if (e == next) {
-      msm_flush(partial, owner, ((e1 - 1) >> lgL) + b, b, acc, inf);
+      msm_flush(partial, owner, (e1 - 1) / L + b, b, acc, inf);
       inf = true;
       do {
         b++;
@@ -871,7 +869,7 @@ __global__ void __launch_bounds__(MSM_BLOCK) __attribute__((amdgpu_waves_per_eu(
     }
     if (!x29_acc_madd_tp(acc, ax, ay)) x29_acc_madd_exc(acc, ax, ay, &inf);
   }
-  if (e0 < e1) msm_flush(partial, owner, ((e1 - 1) >> lgL) + b, b, acc, inf);
+  if (e0 < e1) msm_flush(partial, owner, (e1 - 1) / L + b, b, acc, inf);
 #endif
 }
 
@@ -1453,15 +1451,40 @@ static MsmRun msm_accumulate_phase(qg_ctx* ctx, const qg_srs* srs, const Fr* d_s
       L = 1u << elog;
     }
     if (const char* ov = getenv("QG_MSM_ELOG")) L = 1u << atoi(ov);  // tuning experiments
+    // the accumulate form (below) and its resident waves per SIMD
+    bool pf = max_entries >= ((size_t)1 << 27);
+    if (const char* ov = getenv("QG_MSM_PF")) pf = atoi(ov) != 0;
+    bool coop = max_entries >= ((size_t)1 << 25);
+    if (const char* ov = getenv("QG_MSM_COOP")) coop = atoi(ov) != 0;
+    // Equal chunks (any multiple of 4 entries) filling exactly k rounds of the
+    // chip's resident waves: no partly-filled last round, and fewer, longer
+    // chunks leave fewer partial slots per bucket for the reduction.  The MSMs
+    // of a side-stream batch take k = 1: HyperPlonk 866.9 / 870.6 -> 847.1 /
+    // 850.5 ms per proof, its reduce 63.3 -> 52.1 ms (the accumulate itself
+    // slower, the other stream's bucketing beside it faster), 2^24 headline
+    // unchanged (profiles/r06g_msm_eqsplit_ab.txt).  A lone MSM keeps the
+    // power-of-two rule: with k = 1 / 2 / 3 the 2^24 accumulate is 1.4 / 0.7 /
+    // 0.5 ms slower for a reduction 0.20 / 0.10 / 0.18 ms faster (the waves of
+    // one round do not finish together; many rounds even them out).
+    // QG_MSM_EQSPLIT=k overrides (0: the power-of-two rule; A/B runs).
+    int eqk = side ? 1 : 0;
+    if (const char* ov = getenv("QG_MSM_EQSPLIT")) eqk = atoi(ov);
+    {
+      const int k = eqk;
+      if (k > 0) {
+        const size_t wpe = coop ? QG_COOP_WPE : (pf ? 3 : 4);
+        const size_t resident = (size_t)ctx->num_cus() * 4 * wpe * 64;
+        const size_t lq = (div_up(max_entries, resident * (size_t)k) + 3) & ~(size_t)3;
+        L = (uint32_t)std::max<size_t>(4, lq);
+      }
+    }
     // partial slots a bucket's sum adds in a row in the reduction: the typical
     // count + 1 (a bucket of c entries spans ceil(c / L) or one more slots);
     // skewed buckets beyond it are pre-summed by tree steps
     const uint32_t T = std::max<uint32_t>(4, (uint32_t)div_up(div_up(max_entries, nb), L) + 2);
-    // k_msm_accumulate takes log2 L and the group phase of entry e as e & 3
-    QG_CHECK(L >= 4 && L <= 65536 && (L & (L - 1)) == 0, QG_ERR_INVALID,
-             "MSM chunk length out of range");
-    uint32_t lgL = 0;
-    while ((1u << lgL) < L) lgL++;
+    // k_msm_accumulate takes the group phase of entry e as e & 3: chunks start
+    // at multiples of 4
+    QG_CHECK(L >= 4 && L <= 65536 && (L & 3u) == 0, QG_ERR_INVALID, "MSM chunk length out of range");
     const size_t max_threads = div_up(max_entries, L);
     const size_t nslots = max_threads + nb + 1;  // partial slot of (thread t, bucket b): t + b
     X29Raw* partial = ctx->scratch_as<X29Raw>("msm_partial" + sfx, nslots);
@@ -1557,24 +1580,21 @@ static MsmRun msm_accumulate_phase(qg_ctx* ctx, const qg_srs* srs, const Fr* d_s
       QgTimed tm(ctx, "msm_accumulate", ast);
       // the prefetching per-lane-gather form (QG_MSM_PF=1 with QG_MSM_COOP=0;
       // the default for 2^27+ entries before the cooperative gathers)
-      bool pf = max_entries >= ((size_t)1 << 27);
-      if (const char* ov = getenv("QG_MSM_PF")) pf = atoi(ov) != 0;
-      // cooperative row gathers from 2^25 entries (2^22 scalars x 13 windows):
-      // 2^24 accumulate 16.4-16.6 -> 15.3 ms, 2^22 -4 %, 2^20 neutral
-      // (profiles/r05_msm_coop_ab.txt); QG_MSM_COOP=0/1 forces it (A/B runs)
-      bool coop = max_entries >= ((size_t)1 << 25);
-      if (const char* ov = getenv("QG_MSM_COOP")) coop = atoi(ov) != 0;
+      // (pf / coop chosen above) cooperative row gathers from 2^25 entries
+      // (2^22 scalars x 13 windows): 2^24 accumulate 16.4-16.6 -> 15.3 ms, 2^22
+      // -4 %, 2^20 neutral (profiles/r05_msm_coop_ab.txt); QG_MSM_COOP=0/1
+      // forces it (A/B runs)
       if (coop)
         hipLaunchKernelGGL(k_msm_accumulate_coop, dim3(div_up(max_threads, MSM_BLOCK)),
-                           dim3(MSM_BLOCK), 0, ast, srs->d_table, entries, bstart, nb, lgL,
+                           dim3(MSM_BLOCK), 0, ast, srs->d_table, entries, bstart, nb, L,
                            partial, owner);
       else if (pf)
         hipLaunchKernelGGL(k_msm_accumulate<true>, dim3(div_up(max_threads, MSM_BLOCK)),
-                           dim3(MSM_BLOCK), 0, ast, srs->d_table, entries, bstart, nb, lgL,
+                           dim3(MSM_BLOCK), 0, ast, srs->d_table, entries, bstart, nb, L,
                            partial, owner);
       else
         hipLaunchKernelGGL(k_msm_accumulate<false>, dim3(div_up(max_threads, MSM_BLOCK)),
-                           dim3(MSM_BLOCK), 0, ast, srs->d_table, entries, bstart, nb, lgL,
+                           dim3(MSM_BLOCK), 0, ast, srs->d_table, entries, bstart, nb, L,
                            partial, owner);
       QG_LAUNCH_CHECK();
     }
