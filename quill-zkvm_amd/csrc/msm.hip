@@ -619,6 +619,12 @@ QG_DEV void msm_flush(X29Raw* partial, uint32_t* owner, uint32_t slot, uint32_t 
   owner[slot] = b;
 }
 
+// e / L for the chunk length L of a launch (any multiple of 4), by one 64-bit
+// high multiply with Lm = floor((2^64 - 1) / L) + 1: exact for e < 2^32 and
+// L < 2^16 (the error e (Lm - 2^64 / L) / 2^64 < 2^-32 < 1 / L).  A division
+// here made k_msm_accumulate<false> spill 28 B per lane (round 6).
+QG_DEV uint32_t msm_chunk_of(uint32_t e, uint64_t Lm) { return (uint32_t)__umul64hi((uint64_t)e, Lm); }
+
 QG_DEV X29 msm_partial(const X29Raw* partial, uint32_t slot) {
   return x29_acc_finish(x29_unraw(partial[slot]));
 }
@@ -641,7 +647,7 @@ QG_DEV uint4 msm_entries4(const uint32_t* __restrict__ entries, uint32_t e, uint
 template <bool PF>
 __global__ void __launch_bounds__(MSM_BLOCK) __attribute__((amdgpu_waves_per_eu(PF ? 3 : 4)))
     k_msm_accumulate(const MsmPt* __restrict__ table, const uint32_t* __restrict__ entries,
-                     const uint32_t* __restrict__ bstart, uint32_t nb, uint32_t L,
+                     const uint32_t* __restrict__ bstart, uint32_t nb, uint32_t L, uint64_t Lm,
                      X29Raw* __restrict__ partial, uint32_t* __restrict__ owner) {
   const uint32_t t = blockIdx.x * blockDim.x + threadIdx.x;
   const uint32_t total = bstart[nb];
@@ -651,7 +657,7 @@ __global__ void __launch_bounds__(MSM_BLOCK) __attribute__((amdgpu_waves_per_eu(
   const uint32_t e1 = total - e0 < L ? total : e0 + L;
   // the thread index is not kept live through the loop (it cost the
   // non-prefetching form one VGPR spilled and reloaded per addition): a flush
-  // recovers it from the chunk end, t = (e1 - 1) / L; chunks start at
+  // recovers it from the chunk end, t = (e1 - 1) / L (msm_chunk_of); chunks start at
   // multiples of L (>= 4), so the group phase is e & 3
   // bucket of entry e0: the largest b with bstart[b] <= e0 (b < nb)
   uint32_t lo = 0, hi = nb;
@@ -687,7 +693,7 @@ __global__ void __launch_bounds__(MSM_BLOCK) __attribute__((amdgpu_waves_per_eu(
       if (e + 5 < e1) g1 = msm_entries4(entries, e + 5, e1);
     }
     if (e == next) {
-      msm_flush(partial, owner, (e1 - 1) / L + b, b, acc, inf);
+      msm_flush(partial, owner, msm_chunk_of(e1 - 1, Lm) + b, b, acc, inf);
       inf = true;
       do {
         b++;
@@ -709,7 +715,7 @@ __global__ void __launch_bounds__(MSM_BLOCK) __attribute__((amdgpu_waves_per_eu(
     ay = by;
     pinf = qinf;
   }
-  msm_flush(partial, owner, (e1 - 1) / L + b, b, acc, inf);
+  msm_flush(partial, owner, msm_chunk_of(e1 - 1, Lm) + b, b, acc, inf);
   return;
   }
   // entries arrive four at a time (one 16-B load per group of four, the next
@@ -723,7 +729,7 @@ __global__ void __launch_bounds__(MSM_BLOCK) __attribute__((amdgpu_waves_per_eu(
     const uint32_t ent = k == 0 ? cur.x : k == 1 ? cur.y : k == 2 ? cur.z : cur.w;
     if (k == 3) cur = nxt;
     if (e == next) {  // bucket boundary (at most a few per thread)
-      msm_flush(partial, owner, (e1 - 1) / L + b, b, acc, inf);
+      msm_flush(partial, owner, msm_chunk_of(e1 - 1, Lm) + b, b, acc, inf);
       inf = true;
       do {
         b++;
@@ -743,7 +749,7 @@ __global__ void __launch_bounds__(MSM_BLOCK) __attribute__((amdgpu_waves_per_eu(
     }
     if (!x29_acc_madd_tp(acc, ax, ay)) x29_acc_madd_exc(acc, ax, ay, &inf);
   }
-  msm_flush(partial, owner, (e1 - 1) / L + b, b, acc, inf);
+  msm_flush(partial, owner, msm_chunk_of(e1 - 1, Lm) + b, b, acc, inf);
 }
 
 // Cooperative row gathers (COOP).  One 16-B load per lane of five per row
@@ -805,7 +811,7 @@ __device__ __forceinline__ bool msm_coop_read(const uint4* wbuf, uint32_t lane, 
 #endif
 __global__ void __launch_bounds__(MSM_BLOCK) __attribute__((amdgpu_waves_per_eu(QG_COOP_WPE)))
     k_msm_accumulate_coop(const MsmPt* __restrict__ table, const uint32_t* __restrict__ entries,
-                          const uint32_t* __restrict__ bstart, uint32_t nb, uint32_t L,
+                          const uint32_t* __restrict__ bstart, uint32_t nb, uint32_t L, uint64_t Lm,
                           X29Raw* __restrict__ partial, uint32_t* __restrict__ owner) {
 #if defined(__HIP_DEVICE_COMPILE__)
   __shared__ uint4 img[MSM_BLOCK / 64][64 * 8];
@@ -851,7 +857,7 @@ __global__ void __launch_bounds__(MSM_BLOCK) __attribute__((amdgpu_waves_per_eu(
     if (i + 1 < L) msm_coop_issue(wbuf, table, lane, e + 1 < e1 ? en : 0u);
     if (e >= e1) continue;
     if (e == next) {
-      msm_flush(partial, owner, (e1 - 1) / L + b, b, acc, inf);
+      msm_flush(partial, owner, msm_chunk_of(e1 - 1, Lm) + b, b, acc, inf);
       inf = true;
       do {
         b++;
@@ -869,7 +875,7 @@ __global__ void __launch_bounds__(MSM_BLOCK) __attribute__((amdgpu_waves_per_eu(
     }
     if (!x29_acc_madd_tp(acc, ax, ay)) x29_acc_madd_exc(acc, ax, ay, &inf);
   }
-  if (e0 < e1) msm_flush(partial, owner, (e1 - 1) / L + b, b, acc, inf);
+  if (e0 < e1) msm_flush(partial, owner, msm_chunk_of(e1 - 1, Lm) + b, b, acc, inf);
 #endif
 }
 
@@ -1485,6 +1491,7 @@ static MsmRun msm_accumulate_phase(qg_ctx* ctx, const qg_srs* srs, const Fr* d_s
     // k_msm_accumulate takes the group phase of entry e as e & 3: chunks start
     // at multiples of 4
     QG_CHECK(L >= 4 && L <= 65536 && (L & 3u) == 0, QG_ERR_INVALID, "MSM chunk length out of range");
+    const uint64_t Lm = ~0ull / L + 1;  // msm_chunk_of's multiplier
     const size_t max_threads = div_up(max_entries, L);
     const size_t nslots = max_threads + nb + 1;  // partial slot of (thread t, bucket b): t + b
     X29Raw* partial = ctx->scratch_as<X29Raw>("msm_partial" + sfx, nslots);
@@ -1586,15 +1593,15 @@ static MsmRun msm_accumulate_phase(qg_ctx* ctx, const qg_srs* srs, const Fr* d_s
       // forces it (A/B runs)
       if (coop)
         hipLaunchKernelGGL(k_msm_accumulate_coop, dim3(div_up(max_threads, MSM_BLOCK)),
-                           dim3(MSM_BLOCK), 0, ast, srs->d_table, entries, bstart, nb, L,
+                           dim3(MSM_BLOCK), 0, ast, srs->d_table, entries, bstart, nb, L, Lm,
                            partial, owner);
       else if (pf)
         hipLaunchKernelGGL(k_msm_accumulate<true>, dim3(div_up(max_threads, MSM_BLOCK)),
-                           dim3(MSM_BLOCK), 0, ast, srs->d_table, entries, bstart, nb, L,
+                           dim3(MSM_BLOCK), 0, ast, srs->d_table, entries, bstart, nb, L, Lm,
                            partial, owner);
       else
         hipLaunchKernelGGL(k_msm_accumulate<false>, dim3(div_up(max_threads, MSM_BLOCK)),
-                           dim3(MSM_BLOCK), 0, ast, srs->d_table, entries, bstart, nb, L,
+                           dim3(MSM_BLOCK), 0, ast, srs->d_table, entries, bstart, nb, L, Lm,
                            partial, owner);
       QG_LAUNCH_CHECK();
     }
