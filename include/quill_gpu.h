@@ -171,6 +171,14 @@ int qg_msm_g1(qg_ctx* ctx, const qg_srs* srs, const uint64_t* scalars, size_t n,
               uint64_t out_xy[8], uint8_t* out_inf);
 int qg_msm_g1_dev(qg_ctx* ctx, const qg_srs* srs, const qg_buf* scalars, size_t n,
                   uint64_t out_xy[8], uint8_t* out_inf);
+/* k MSMs over one SRS in one call (at most 1024): out_xy[8 i ..], out_inf[i]
+ * for scalars[i] (first ns[i] entries), each equal to qg_msm_g1_dev of it.
+ * They run as one MSM batch (bucketing beside the previous MSM's accumulation
+ * on two side streams, one set of reduction launches): the commitments a
+ * caller needs together, e.g. HyperPlonk's two Logup denominator columns
+ * (multiset_check.rs:43-95) or its trace witnesses (proof.rs:252-262). */
+int qg_msm_g1_dev_batch(qg_ctx* ctx, const qg_srs* srs, const qg_buf* const* scalars,
+                        const size_t* ns, size_t k, uint64_t* out_xy, uint8_t* out_inf);
 /* KZG::commit (kzg.rs:61-73): QG_ERR_INVALID when n > max_degree + 1
  * (reference: assert! at kzg.rs:62-65). */
 int qg_kzg_commit(qg_ctx* ctx, const qg_srs* srs, const uint64_t* poly, size_t n,

@@ -2213,6 +2213,25 @@ int qg_msm_g1_dev(qg_ctx* ctx, const qg_srs* srs, const qg_buf* scalars, size_t 
   });
 }
 
+int qg_msm_g1_dev_batch(qg_ctx* ctx, const qg_srs* srs, const qg_buf* const* scalars,
+                        const size_t* ns, size_t k, uint64_t* out_xy, uint8_t* out_inf) {
+  if (!ctx || !srs || (k && (!scalars || !ns || !out_xy || !out_inf))) return QG_ERR_INVALID;
+  for (size_t i = 0; i < k; i++)
+    if (!scalars[i] || ns[i] > scalars[i]->n) return QG_ERR_INVALID;
+  return qg_guard(ctx, [&] {
+    QG_CHECK(k <= (size_t)MSM_MAX_BATCH, QG_ERR_UNSUPPORTED, "MSM batch too large");
+    QG_HIP(hipSetDevice(ctx->device));
+    std::vector<const Fr*> sc(k);
+    std::vector<size_t> n(k);
+    for (size_t i = 0; i < k; i++) {
+      sc[i] = scalars[i]->d;
+      n[i] = ns[i];
+    }
+    const std::vector<G1Affine> r = msm_device_batch(ctx, srs, sc, n);
+    for (size_t i = 0; i < k; i++) g1_export(r[i], out_xy + 8 * i, out_inf + i);
+  });
+}
+
 int qg_msm_g1(qg_ctx* ctx, const qg_srs* srs, const uint64_t* scalars, size_t n,
               uint64_t out_xy[8], uint8_t* out_inf) {
   if (!ctx || !srs || (!scalars && n) || !out_xy) return QG_ERR_INVALID;

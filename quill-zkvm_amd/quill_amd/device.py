@@ -347,6 +347,17 @@ class Srs:
         check(lib().qg_msm_g1_dev(self.dev.h, self.h, vec.h, n, xy, C.byref(inf)), self.dev.h)
         return g1_from_abi(xy, inf.value)
 
+    def msm_dev_batch(self, vecs, ns=None) -> list:
+        """qg_msm_g1_dev_batch: the MSMs of several device vectors as one batch"""
+        k = len(vecs)
+        ns = [v.n for v in vecs] if ns is None else list(ns)
+        hs = (C.c_void_p * max(k, 1))(*[v.h.value for v in vecs])
+        nn = (C.c_size_t * max(k, 1))(*ns)
+        xy = (C.c_uint64 * (8 * max(k, 1)))()
+        inf = (C.c_uint8 * max(k, 1))()
+        check(lib().qg_msm_g1_dev_batch(self.dev.h, self.h, hs, nn, k, xy, inf), self.dev.h)
+        return [g1_from_abi(xy[8 * i:8 * i + 8], inf[i]) for i in range(k)]
+
     def close(self):
         if self.h:
             lib().qg_srs_destroy(self.h)

@@ -104,7 +104,7 @@ class MultisetEqualityProof:
             assert multiplicities is None, \
                 "Multiplicities polynomial must not be provided in equality mode"
             right, _ = logup_column(store, h_right, beta, None, dev)
-        cl, cr = pcs.commit(left), pcs.commit(right)
+        cl, cr = pcs.commit_batch([left, right])
         transcript.append_g1(cl)
         transcript.append_g1(cr)
         lam = transcript.draw_field_element()
@@ -189,7 +189,7 @@ class SetInclusionProof:
         gamma = transcript.draw_field_element()  # logup_eval_point
         left, sum_left = logup_column(store_left, h_left, gamma, None, dev)
         right, sum_right = logup_column(store_right, h_right, gamma, multiplicities, dev)
-        cl, cr = pcs.commit(left), pcs.commit(right)
+        cl, cr = pcs.commit_batch([left, right])
         transcript.append_g1(cl)
         transcript.append_g1(cr)
         z1 = [transcript.draw_field_element() for _ in range(nl)]

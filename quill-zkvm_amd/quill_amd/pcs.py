@@ -5,6 +5,7 @@ are affine (x, y) tuples or None (infinity)."""
 from __future__ import annotations
 
 import ctypes as C
+import os
 from dataclasses import dataclass
 
 import numpy as np
@@ -231,6 +232,18 @@ class KZG:
         check(lib().qg_kzg_commit(self.dev.h, self.srs.h, u64p(arr), len(poly), xy,
                                   C.byref(inf)), self.dev.h)
         return g1_from_abi(xy, inf.value)
+
+    def commit_batch(self, polys) -> list:
+        """[commit(p) for p in polys], device vectors of one SRS shard as one MSM
+        batch (qg_msm_g1_dev_batch); the same points"""
+        if (len(polys) < 2 or not all(isinstance(p, DeviceVec) for p in polys)
+                or (self.dev.world > 1 and len({len(p) for p in polys}) != 1)
+                or os.environ.get("QUILL_COMMIT_BATCH", "1") == "0"):  # A/B runs
+            return [self.commit(p) for p in polys]
+        for p in polys:
+            if len(p) > self._max_degree + 1:
+                raise QuillGpuError(-1, "Polynomial degree exceeds max degree")
+        return self.srs_for(len(polys[0])).msm_dev_batch(polys)
 
     # KZG::open (kzg.rs:75-96)
     def open_univariate(self, poly, x: int) -> KZGOpeningProof:

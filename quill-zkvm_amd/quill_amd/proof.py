@@ -324,10 +324,12 @@ class HyperPlonk:
             owned += own
             if check_constraints:
                 circuit.check_constraints(cols)
-            Cm = pcs.commit(full)
-            t.append_g1(Cm)
-            comms.append(Cm)
             layouts.append((cols, full))
+        # the witness commitments (proof.rs:252-262) as one MSM batch, absorbed in
+        # trace order: the same transcript as committing one by one
+        comms = pcs.commit_batch([full for _, full in layouts])
+        for Cm in comms:
+            t.append_g1(Cm)
         proofs = []
         for (cols, full), vk, pk in zip(layouts, self.trace_vks, self.trace_pks):
             proofs.append(self.prove_trace(pcs, cols, full, t, pk, vk.circuit))

@@ -275,3 +275,25 @@ def test_hyperplonk_2p14_rows_event_handover_same_proof(dev):
     opcs, ohp, _ = _oracle_setup(rows, ("fib", "mod"))
     vt = ho.hyperplonk_verify(to_oracle(last), ohp.to_vk(), opcs)
     assert vt.state == hp.last_transcript.state
+
+
+def test_msm_dev_batch_equals_single_commits(dev):
+    """qg_msm_g1_dev_batch (one MSM batch on the side streams) gives the same
+    points as one qg_msm_g1_dev per vector: lengths 2^16, 1000, 0, 2^15 + 3 on
+    one SRS, and the trapdoor identity [p(tau)] g for each."""
+    import oracle_c as oc
+    import quill_amd as q
+    from quill_amd import KZG
+    tau = 0x4241544348
+    kzg = KZG.trusted_setup((1 << 16) - 1, tau, dev)
+    vecs = [q.DeviceVec(dev, n).fill_random(77 + i) for i, n in enumerate((1 << 16, 1000, 1, (1 << 15) + 3))]
+    ns = [1 << 16, 1000, 0, (1 << 15) + 3]
+    got = kzg.srs.msm_dev_batch(vecs, ns)
+    assert got == [kzg.srs.msm_dev(v, n) for v, n in zip(vecs, ns)]
+    for v, n, P in zip(vecs, ns, got):
+        want = oc.g1_mul(o.G1_GEN, oc.fr_horner(v.to_numpy(n), tau)) if n else None
+        assert P == want
+    assert kzg.commit_batch(vecs[:2]) == got[:2]
+    for v in vecs:
+        v.close()
+    kzg.close()
