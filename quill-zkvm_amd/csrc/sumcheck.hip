@@ -1376,7 +1376,10 @@ __global__ void __launch_bounds__(TAIL_BLOCK)
 // log2(G) rounds alone (the table again in LDS).  The deferred absorb of the
 // previous challenge runs on the last wave beside the other waves' evaluation.
 // ---------------------------------------------------------------------------
-static constexpr int SL_BLOCK = 256;
+#ifndef QG_SL_BLOCK
+#define QG_SL_BLOCK 256
+#endif
+static constexpr int SL_BLOCK = QG_SL_BLOCK;
 // entries per slot of a block's slice in the first tail round (LDS: K slots x
 // 1.5 x SL_SMAX entries of 36 B: the slice and its half-size fold)
 QG_HD constexpr uint32_t sl_smax(int K) { return K <= 4 ? 256u : 128u; }
