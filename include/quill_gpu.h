@@ -116,6 +116,15 @@ int qg_g1_serialize(const uint64_t xy[8], uint8_t infinity, uint8_t out[64]);
  * precomputed window-shifted copies. */
 int qg_srs_upload(qg_ctx* ctx, const uint64_t* affine_xy, const uint8_t* infinity, size_t n,
                   qg_srs** out);
+/* Bases for one-shot MSMs (VariableBaseMSM::msm_unchecked over bases used
+ * once, the call at pcs/src/kzg.rs:72 with a base slice that is not a fixed
+ * SRS): same layout and MSM results as qg_srs_upload, but only ONE table is
+ * built (no window-shifted copies: 1/W of the HBM and none of the W - 1 shift
+ * passes, 0.63 s at 2^24).  Every MSM over these bases then bins its W windows
+ * in W passes and combines the window sums by Horner steps; use qg_srs_upload
+ * for bases that serve many MSMs.  Any qg_* call taking a qg_srs accepts it. */
+int qg_bases_upload(qg_ctx* ctx, const uint64_t* affine_xy, const uint8_t* infinity, size_t n,
+                    qg_srs** out);
 /* KZG::trusted_setup with an explicit tau (kzg.rs:35-59): bases [tau^i] g for
  * i < n, generated on the device.  `g_xy` NULL = the BN254 generator (1, 2). */
 int qg_srs_generate(qg_ctx* ctx, const uint64_t tau[4], const uint64_t* g_xy, size_t n,
@@ -127,7 +136,8 @@ int qg_srs_generate_range(qg_ctx* ctx, const uint64_t tau[4], const uint64_t* g_
 int qg_srs_destroy(qg_srs* srs);
 size_t qg_srs_len(const qg_srs* srs);
 /* MSM window geometry of this SRS: signed-digit window bits c and window
- * count W (the tables hold W shifted copies of the bases). */
+ * count W (the tables hold W shifted copies of the bases; one table for
+ * qg_bases_upload). */
 int qg_srs_window_info(const qg_srs* srs, int* c, int* windows);
 /* Copy bases [offset, offset+n) back to the host (affine, Montgomery). */
 int qg_srs_download(const qg_srs* srs, size_t offset, size_t n, uint64_t* affine_xy,

@@ -221,7 +221,10 @@ struct qg_srs {
   size_t n = 0;  // number of bases
   int c = 0;     // MSM window bits (signed digits)
   int W = 0;     // number of windows = ceil(255 / c)
-  // W * n rows; table[w * n + i] = 2^(c*w) * base_i   (curve.h MsmPt layout)
+  // tables * n rows; table[w * n + i] = 2^(c*w) * base_i   (curve.h MsmPt layout)
+  // tables == W: window-shifted tables (a fixed SRS); tables == 1: bases for
+  // one-shot MSMs (qg_bases_upload), whose windows are summed by Horner steps
+  int tables = 0;
   qg::MsmPt* d_table = nullptr;
 };
 

@@ -146,10 +146,11 @@ QG_DEV void msm_handover_check(uint32_t* hv, uint32_t w0, uint32_t nw, uint32_t 
 // Pass A histogram; also writes every scalar's canonical words (`canon`), so
 // the scatter pass reads them without a second Montgomery reduction.
 // hv != null: the scalars came from another stream (hand-over guard above)
+// wsel >= 0: only window wsel's digits (one-shot bases, msm_oneshot_local)
 __global__ void __launch_bounds__(SORT_BLOCK)
     k_sortA_hist(const Fr* __restrict__ scalars, size_t n, int c, int W, int LO, int H,
                  uint32_t nblk, uint32_t tile, uint32_t* __restrict__ hrow, Fr* __restrict__ canon,
-                 uint32_t* hv, uint32_t gen) {
+                 uint32_t* hv, uint32_t gen, int wsel) {
   extern __shared__ uint32_t hist[];
   msm_handover_check(hv, 0, 1, gen, 1u);
   for (int g = threadIdx.x; g < H; g += blockDim.x) hist[g] = 0;
@@ -161,7 +162,9 @@ __global__ void __launch_bounds__(SORT_BLOCK)
   for (size_t i = base + threadIdx.x; i < end; i += blockDim.x) {
     const Fr s = fr_canon29(scalars[i]);
     canon[i] = s;
-    for_each_digit(s, c, W, [&](int, uint32_t b, bool) { atomicAdd(&hist[b >> LO], 1u); });
+    for_each_digit(s, c, W, [&](int w, uint32_t b, bool) {
+      if (wsel < 0 || w == wsel) atomicAdd(&hist[b >> LO], 1u);
+    });
   }
   __syncthreads();
   // row-major (tile, group): one contiguous row per block; transposed for the scan
@@ -224,16 +227,18 @@ __device__ __forceinline__ int lds_upper(const uint32_t* off, int n, uint32_t p)
 // (coalesced stores) through a per-block base table, no per-element search.
 // The block's counts and global offsets are contiguous rows (hrow / orow).
 // Output per digit: the table entry (u32) and the bucket's low LO bits (u16).
+// wsel >= 0: only window wsel's digits, entry = the base's row in the one
+// table of one-shot bases (no window offset)
 __global__ void __launch_bounds__(SORT_BLOCK)
     k_sortA_scatter(const Fr* __restrict__ canon, size_t n, size_t N, size_t off, int c, int W, int LO,
                     int H,
                     uint32_t nblk, uint32_t tile, const uint32_t* __restrict__ hrow,
                     const uint32_t* __restrict__ orow, uint32_t* __restrict__ tmp_e,
-                    uint16_t* __restrict__ tmp_l) {
+                    uint16_t* __restrict__ tmp_l, int wsel) {
   extern __shared__ __attribute__((aligned(16))) unsigned char smem[];
   uint32_t* ent = reinterpret_cast<uint32_t*>(smem);
-  uint32_t* bkt = ent + (size_t)tile * W;
-  uint32_t* loff = bkt + (size_t)tile * W;
+  uint32_t* bkt = ent + (size_t)tile * (wsel < 0 ? W : 1);
+  uint32_t* loff = bkt + (size_t)tile * (wsel < 0 ? W : 1);
   uint32_t* cur = loff + H;
   uint32_t* gb = cur + H;
   uint32_t* scr = gb + H;
@@ -262,9 +267,11 @@ __global__ void __launch_bounds__(SORT_BLOCK)
     const size_t i = base + threadIdx.x + (size_t)j * SORT_BLOCK;
     if (i >= end) break;
     for_each_digit(sv[j], c, W, [&](int w, uint32_t b, bool neg) {
+      if (wsel >= 0 && w != wsel) return;
       const uint32_t g = b >> LO;
       const uint32_t slot = loff[g] + atomicAdd(&cur[g], 1u);
-      ent[slot] = (uint32_t)((size_t)w * N + off + i) | (neg ? 0x80000000u : 0u);
+      const size_t row = (wsel < 0 ? (size_t)w * N : 0) + off + i;
+      ent[slot] = (uint32_t)row | (neg ? 0x80000000u : 0u);
       bkt[slot] = b;
     });
   }
@@ -1312,14 +1319,14 @@ static void srs_build_tables(qg_ctx* ctx, qg_srs* srs, const G1Affine* base) {
   hipLaunchKernelGGL(k_srs_pack, dim3(div_up(srs->n, 256)), dim3(256), 0, ctx->stream, base,
                      srs->n, srs->d_table);
   QG_LAUNCH_CHECK();
-  for (int w = 1; w < srs->W; w++) {
+  for (int w = 1; w < srs->tables; w++) {
     hipLaunchKernelGGL(k_srs_shift, dim3(div_up(srs->n, 256)), dim3(256), 0, ctx->stream,
                        srs->d_table, srs->n, w, srs->c);
     QG_LAUNCH_CHECK();
   }
 }
 
-static qg_srs* srs_alloc(qg_ctx* ctx, size_t n) {
+static qg_srs* srs_alloc(qg_ctx* ctx, size_t n, bool oneshot = false) {
   qg_srs* srs = new qg_srs();
   srs->ctx = ctx;
   srs->n = n;
@@ -1330,7 +1337,8 @@ static qg_srs* srs_alloc(qg_ctx* ctx, size_t n) {
   QG_CHECK(ct >= 4 && ct <= 26, QG_ERR_INVALID, "MSM window bits out of range");
   srs->W = (255 + ct - 1) / ct;
   srs->c = (255 + srs->W - 1) / srs->W;
-  hipError_t e = hipMalloc(&srs->d_table, (size_t)srs->W * n * sizeof(MsmPt));
+  srs->tables = oneshot ? 1 : srs->W;
+  hipError_t e = hipMalloc(&srs->d_table, (size_t)srs->tables * n * sizeof(MsmPt));
   if (e != hipSuccess) {
     delete srs;
     throw Error(QG_ERR_OOM, "qg_srs: hipMalloc of the window tables failed");
@@ -1372,9 +1380,12 @@ static constexpr int MSM_MAX_BATCH = 1024;
 // stream `slot` selects) for an MSM of length n, launching nothing.  A batch
 // reserves for its longest MSM first: a slot that grew in the middle of a
 // batch would be freed while an earlier MSM's kernels still read it.
+// wsel >= 0: the digits of window wsel only, over the one table of one-shot
+// bases (msm_oneshot_local); -1: every window over the window-shifted tables
 static MsmRun msm_accumulate_phase(qg_ctx* ctx, const qg_srs* srs, const Fr* d_scalars, size_t n,
                                    int slot, size_t srs_off = 0, hipStream_t bst = nullptr,
-                                   bool reserve = false, uint32_t* hv = nullptr, uint32_t hgen = 0) {
+                                   bool reserve = false, uint32_t* hv = nullptr, uint32_t hgen = 0,
+                                   int wsel = -1) {
   QG_CHECK(srs_off <= srs->n && n <= srs->n - srs_off, QG_ERR_INVALID, "MSM length exceeds the SRS");
   MsmRun run;
   const std::string sfx = "#" + std::to_string(slot);
@@ -1386,8 +1397,11 @@ static MsmRun msm_accumulate_phase(qg_ctx* ctx, const qg_srs* srs, const Fr* d_s
   const std::string tg = side ? "@" + std::to_string(slot & 1) : std::string();
   if (n > 0) {
     const int c = srs->c, W = srs->W;
+    QG_CHECK((wsel < 0) == (srs->tables == W) && wsel < W, QG_ERR_INVALID,
+             "MSM window selection does not match the SRS tables");
+    const int WE = wsel < 0 ? W : 1;  // digits per scalar this run bins
     const uint32_t nb = 1u << (c - 1);
-    const size_t max_entries = n * (size_t)W;
+    const size_t max_entries = n * (size_t)WE;
     QG_CHECK((size_t)W * srs->n < 0x80000000ull, QG_ERR_UNSUPPORTED, "SRS table index overflow");
     QG_CHECK(max_entries < 0xffffffffull, QG_ERR_UNSUPPORTED, "too many MSM entries");
     // bucket id b = (g << LO) | l
@@ -1395,7 +1409,7 @@ static MsmRun msm_accumulate_phase(qg_ctx* ctx, const qg_srs* srs, const Fr* d_s
     const int H = 1 << HI, NL = 1 << LO;
     // pass-A tile: as many scalars as fit their W digits (8 B each) in LDS
     uint32_t tile = SORT_TILE_MAX;
-    while (tile > 64 && (size_t)tile * W * 8 > SORT_LDS_A) tile >>= 1;
+    while (tile > 64 && (size_t)tile * WE * 8 > SORT_LDS_A) tile >>= 1;
     if (const char* ov = getenv("QG_SORT_TILE")) tile = (uint32_t)atoi(ov);  // tuning experiments
     QG_CHECK(tile >= 64 && tile <= SORT_TILE_MAX && (tile & (tile - 1)) == 0, QG_ERR_INVALID,
              "QG_SORT_TILE must be a power of two in [64, 1024]");
@@ -1507,7 +1521,7 @@ static MsmRun msm_accumulate_phase(qg_ctx* ctx, const qg_srs* srs, const Fr* d_s
       QgTimed tm(ctx, side ? "msm_bucketing_side" : "msm_bucketing", bst);
       // pass A: partition digits by the high bucket bits
       hipLaunchKernelGGL(k_sortA_hist, dim3(nblk), dim3(SORT_BLOCK), H * sizeof(uint32_t),
-                         bst, d_scalars, n, c, W, LO, H, nblk, tile, hrow, canon, hv, hgen);
+                         bst, d_scalars, n, c, W, LO, H, nblk, tile, hrow, canon, hv, hgen, wsel);
       QG_LAUNCH_CHECK();
       hipLaunchKernelGGL(k_transpose32, dim3(div_up(H, 32), div_up(nblk, 32)), dim3(256), 0,
                          bst, hrow, nblk, (uint32_t)H, ghist);
@@ -1528,7 +1542,7 @@ static MsmRun msm_accumulate_phase(qg_ctx* ctx, const qg_srs* srs, const Fr* d_s
       QG_LAUNCH_CHECK();
       hipLaunchKernelGGL(k_sortA_rows, dim3(nblk), dim3(SORT_BLOCK), 0, bst, hrow, orow, H);
       QG_LAUNCH_CHECK();
-      const size_t smemA = (size_t)tile * W * 8 + (3 * (size_t)H + SORT_BLOCK) * 4;
+      const size_t smemA = (size_t)tile * WE * 8 + (3 * (size_t)H + SORT_BLOCK) * 4;
       QG_CHECK(smemA <= 160 * 1024, QG_ERR_UNSUPPORTED, "pass-A tile exceeds LDS");
       // the >64 KiB dynamic-LDS attribute, once per context (= per device and
       // per calling thread: a context is used by one thread at a time)
@@ -1540,7 +1554,8 @@ static MsmRun msm_accumulate_phase(qg_ctx* ctx, const qg_srs* srs, const Fr* d_s
         ctx->memo["msm_lds_attr"] = "1";
       }
       hipLaunchKernelGGL(k_sortA_scatter, dim3(nblk), dim3(SORT_BLOCK), smemA, bst,
-                         canon, n, srs->n, srs_off, c, W, LO, H, nblk, tile, hrow, orow, tmp_e, tmp_l);
+                         canon, n, srs->n, srs_off, c, W, LO, H, nblk, tile, hrow, orow, tmp_e, tmp_l,
+                         wsel);
       QG_LAUNCH_CHECK();
       // pass B: sort every group by the low bits, in chunks
       hipLaunchKernelGGL(k_sort_chunks, dim3(1), dim3(1024), 0, bst, goff, nblk, H,
@@ -1825,11 +1840,42 @@ static std::vector<G1Affine> msm_finish_ranks_batch(qg_ctx* ctx, const std::vect
 // D2H copy as the last producer command, under load), DESIGN §5.3 has the
 // analysis.  QG_MSM_PIPE=0 keeps a batch on ctx->stream; QG_MSM_PIPE_SYNC=1
 // crosses through host synchronizations instead of events (A/B runs).
+// One-shot bases (qg_bases_upload: ONE table, no window-shifted copies): the
+// W windows of an MSM are W runs over that table, run w binning only the w-th
+// signed digit of every scalar into its 2^(c-1) buckets (k_sortA_* wsel); the
+// runs share one batched reduction, and the window sums R_w combine as
+// sum_w 2^(c w) R_w by Horner steps on the host (c doublings + one addition per
+// window, ~260 XYZZ operations).  It pays W bucketing passes over the scalars
+// and W bucket sets in the reduction instead of the W - 1 table shifts a fixed
+// SRS pays once (k_srs_shift, 0.63 s at 2^24), so a caller of msm_unchecked
+// with bases it uses once (ark-ec's VariableBaseMSM::msm_unchecked, kzg.rs:72)
+// need not build 13 tables for one MSM.
+static G1Xyzz msm_oneshot_local(qg_ctx* ctx, const qg_srs* srs, const Fr* d, size_t n) {
+  if (n == 0) return G1Xyzz::infinity();
+  std::vector<MsmRun> runs;
+  for (int w = 0; w < srs->W; w++)
+    runs.push_back(msm_accumulate_phase(ctx, srs, d, n, w, 0, nullptr, false, nullptr, 0, w));
+  std::vector<G1Xyzz> part;
+  msm_reduce_phase(ctx, srs, runs, part);  // ends with a synchronization
+  G1Xyzz acc = part[srs->W - 1];
+  for (int w = srs->W - 2; w >= 0; w--) {
+    for (int k = 0; k < srs->c; k++) acc = xyzz_dbl(acc);
+    acc = xyzz_add(acc, part[w]);
+  }
+  return acc;
+}
+
 static std::vector<G1Xyzz> msm_batch_local(qg_ctx* ctx, const qg_srs* srs,
                                            const std::vector<const Fr*>& scalars,
                                            const std::vector<size_t>& ns, bool pipe,
                                            bool* violated) {
   *violated = false;
+  if (srs->tables != srs->W) {  // one-shot bases: each MSM window by window, stream order
+    std::vector<G1Xyzz> local;
+    for (size_t i = 0; i < scalars.size(); i++)
+      local.push_back(msm_oneshot_local(ctx, srs, scalars[i], ns[i]));
+    return local;
+  }
   hipStream_t side[2] = {nullptr, nullptr};
   bool host_sync = false;
   if (const char* ov = getenv("QG_MSM_PIPE_SYNC")) host_sync = atoi(ov) != 0;
@@ -1896,7 +1942,7 @@ std::vector<G1Affine> msm_device_batch(qg_ctx* ctx, const qg_srs* srs,
                                        const std::vector<const Fr*>& scalars,
                                        const std::vector<size_t>& ns) {
   QG_CHECK(scalars.size() == ns.size(), QG_ERR_INVALID, "MSM batch shape");
-  bool pipe = scalars.size() >= 2;
+  bool pipe = scalars.size() >= 2 && srs->tables == srs->W;
   if (const char* ov = getenv("QG_MSM_PIPE")) pipe = pipe && atoi(ov) != 0;
   bool violated = false;
   std::vector<G1Xyzz> local = msm_batch_local(ctx, srs, scalars, ns, pipe, &violated);
@@ -1929,7 +1975,7 @@ static G1Affine msm_host(qg_ctx* ctx, const qg_srs* srs, const uint64_t* h, size
   int P = (int)std::min<size_t>(8, std::max<size_t>(1, n >> 21));
   if (const char* ov = getenv("QG_MSM_PIECES")) P = atoi(ov);  // tuning experiments
   QG_CHECK(P >= 1 && P <= 64, QG_ERR_INVALID, "QG_MSM_PIECES out of range");
-  if (P == 1 || n < (size_t)P) {
+  if (P == 1 || n < (size_t)P || srs->tables != srs->W) {  // one-shot bases: whole upload first
     fr_upload(ctx, d, h, n);
     return msm_device(ctx, srs, d, n);
   }
@@ -2081,15 +2127,15 @@ int qg_microbench_fq_mul(qg_ctx* ctx, double* mul_per_s) {
   });
 }
 
-int qg_srs_upload(qg_ctx* ctx, const uint64_t* affine_xy, const uint8_t* infinity, size_t n,
-                  qg_srs** out) {
+static int srs_upload_impl(qg_ctx* ctx, const uint64_t* affine_xy, const uint8_t* infinity, size_t n,
+                           bool oneshot, qg_srs** out) {
   if (!ctx || !out || (!affine_xy && n)) return QG_ERR_INVALID;
   *out = nullptr;
   qg_srs* srs = nullptr;
   int rc = qg_guard(ctx, [&] {
     QG_CHECK(n > 0, QG_ERR_INVALID, "empty SRS");
     QG_HIP(hipSetDevice(ctx->device));
-    srs = srs_alloc(ctx, n);
+    srs = srs_alloc(ctx, n, oneshot);
     uint64_t* d_xy = ctx->scratch_as<uint64_t>("srs_up_xy", n * 8);
     uint8_t* d_inf = nullptr;
     QG_HIP(hipMemcpyAsync(d_xy, affine_xy, n * 64, hipMemcpyHostToDevice, ctx->stream));
@@ -2113,6 +2159,16 @@ int qg_srs_upload(qg_ctx* ctx, const uint64_t* affine_xy, const uint8_t* infinit
   }
   *out = srs;
   return QG_OK;
+}
+
+int qg_srs_upload(qg_ctx* ctx, const uint64_t* affine_xy, const uint8_t* infinity, size_t n,
+                  qg_srs** out) {
+  return srs_upload_impl(ctx, affine_xy, infinity, n, false, out);
+}
+
+int qg_bases_upload(qg_ctx* ctx, const uint64_t* affine_xy, const uint8_t* infinity, size_t n,
+                    qg_srs** out) {
+  return srs_upload_impl(ctx, affine_xy, infinity, n, true, out);
 }
 
 int qg_srs_generate(qg_ctx* ctx, const uint64_t tau[4], const uint64_t* g_xy, size_t n,

@@ -83,6 +83,7 @@ PROTOTYPES = {
     "qg_fr_serialize": (C.c_int, [U64P, U8P]),
     "qg_g1_serialize": (C.c_int, [U64P, C.c_uint8, U8P]),
     "qg_srs_upload": (C.c_int, [P, U64P, U8P, SZ, C.POINTER(P)]),
+    "qg_bases_upload": (C.c_int, [P, U64P, U8P, SZ, C.POINTER(P)]),
     "qg_srs_generate": (C.c_int, [P, U64P, U64P, SZ, C.POINTER(P)]),
     "qg_srs_generate_range": (C.c_int, [P, U64P, U64P, C.c_uint64, SZ, C.POINTER(P)]),
     "qg_srs_destroy": (C.c_int, [P]),

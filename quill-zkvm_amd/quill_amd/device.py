@@ -286,7 +286,10 @@ class Srs:
         return cls(dev, h)
 
     @classmethod
-    def upload(cls, dev: Device, points):
+    def upload(cls, dev: Device, points, oneshot: bool = False):
+        """bases from oracle points (None = infinity).  oneshot: qg_bases_upload
+        (one table, for bases that serve a single MSM) instead of the
+        window-shifted tables of qg_srs_upload"""
         n = len(points)
         xy = np.zeros((n, 8), dtype=np.uint64)
         inf = np.zeros(n, dtype=np.uint8)
@@ -294,9 +297,17 @@ class Srs:
             a, f = g1_to_abi(P)
             xy[i, :] = list(a)
             inf[i] = f
+        return cls.upload_raw(dev, xy, inf, oneshot)
+
+    @classmethod
+    def upload_raw(cls, dev: Device, xy: np.ndarray, inf: np.ndarray, oneshot: bool = False):
+        """bases as ABI limbs: (n, 8) uint64 x||y Montgomery + (n,) uint8 flags"""
+        xy = np.ascontiguousarray(xy, dtype=np.uint64)
+        inf = np.ascontiguousarray(inf, dtype=np.uint8)
         h = C.c_void_p()
-        check(lib().qg_srs_upload(dev.h, u64p(xy), inf.ctypes.data_as(C.POINTER(C.c_uint8)), n,
-                                  C.byref(h)), dev.h)
+        fn = lib().qg_bases_upload if oneshot else lib().qg_srs_upload
+        check(fn(dev.h, u64p(xy), inf.ctypes.data_as(C.POINTER(C.c_uint8)), xy.shape[0],
+                 C.byref(h)), dev.h)
         return cls(dev, h)
 
     def __len__(self):
