@@ -65,6 +65,9 @@ def parse():
                     help="rows (log2) of the C5 CPU-baseline sample (HyperPlonk prove in C)")
     ap.add_argument("--cpu-sample-log", type=int, default=20,
                     help="log2 size of the CPU-baseline MSM sample (a prefix of the workload)")
+    ap.add_argument("--no-oneshot", dest="oneshot", action="store_false",
+                    help="skip the one-shot-bases leg: the headline MSM over the same bases "
+                         "uploaded with qg_bases_upload (one table, no window-shifted copies)")
     ap.add_argument("--no-host-input", dest="host_input", action="store_false",
                     help="skip the drop-in leg: the same commitment from host memory "
                          "(qg_kzg_commit, H2D inside the timed region)")
@@ -86,7 +89,8 @@ SC_KERNELS = ("k_sc_big", "k_sc_round", "k_sc_persist", "k_sc_finish", "k_sc_sli
 # to its leg (kernels of one grid shape recur across legs)
 LEG_TAGS = {"msm_2p24": 1, "sumcheck": 2, "msm_host": 3, "scaling": 4, "mle_open": 5, "logup": 6,
             "hyperplonk": 7, "msm_2p20": 8, "cpu_baseline": 9, "probe_msm": 10,
-            "probe_sumcheck": 11, "probe_logup": 12, "probe_mle": 13, "probe_cal": 14}
+            "probe_sumcheck": 11, "probe_logup": 12, "probe_mle": 13, "probe_cal": 14,
+            "msm_oneshot": 15}
 
 
 def traffic_probe(args):
@@ -378,6 +382,11 @@ def main():
         dev.trace_marker(LEG_TAGS["msm_host"])
         out["msm_host_input"] = bench_msm_host(q, dev, args, barrier_sync, max_over_ranks, srs,
                                                scalars, ms_per_step, res)
+    if args.oneshot:
+        _progress(rank, "MSM over one-shot bases")
+        dev.trace_marker(LEG_TAGS["msm_oneshot"])
+        out["msm_oneshot"] = bench_msm_oneshot(q, dev, args, barrier_sync, max_over_ranks, srs,
+                                               scalars, res)
     if not args.no_scaling_modes:
         _progress(rank, "scaling modes")
         dev.trace_marker(LEG_TAGS["scaling"])
@@ -433,7 +442,8 @@ _DROP_KEYS = {"note", "traffic_note", "frac_note", "issue_bound_note", "identity
               "commitment_check", "final_transcript_state", "cpu_model", "metric_note",
               "spans_ms_rank0"}
 # sections dropped (in this order) if the line is still over budget
-_SHED_ORDER = ("kernels_ms", "sumcheck_weak_scaling", "msm_strong_scaling", "msm_host_input",
+_SHED_ORDER = ("kernels_ms", "sumcheck_weak_scaling", "msm_strong_scaling", "msm_oneshot",
+               "msm_host_input",
                "logup", "mle_open", "hyperplonk", "hbm_by_kernel")
 
 
@@ -529,6 +539,37 @@ def bench_msm_host(q, dev, args, barrier_sync, max_over_ranks, srs, scalars, res
             if ms > resident_ms else None,
             "matches_resident_commitment": got == res,
             "note": "pageable host scalars -> qg_kzg_commit; value is never the headline"}
+
+
+def bench_msm_oneshot(q, dev, args, barrier_sync, max_over_ranks, srs, scalars, res):
+    """msm_unchecked (kzg.rs:72) over bases used once: the headline's bases
+    uploaded with qg_bases_upload (one table, no window-shifted copies; the MSM
+    bins its windows in W passes and adds them by Horner steps) and the
+    headline's scalars; the commitment must equal the headline's.  upload_s is
+    the whole preprocessing such bases get (the window-shifted tables of
+    qg_srs_upload take ~0.65 s at 2^24, profiles/r06m_oneshot_prof.json)."""
+    n = 1 << args.log_msm
+    xy, inf = srs.download_raw()
+    barrier_sync()
+    t0 = time.perf_counter()
+    one = q.Srs.upload_raw(dev, xy, inf, oneshot=True)
+    upload_s = time.perf_counter() - t0
+    del xy, inf
+    steps = max(1, min(args.steps, 10))
+    got = one.msm_dev(scalars)
+    barrier_sync()
+    t0 = time.perf_counter()
+    for _ in range(steps):
+        got = one.msm_dev(scalars)
+    barrier_sync()
+    dt = max_over_ranks(time.perf_counter() - t0)
+    c_bits, n_win = one.window_info()
+    one.close()
+    ms = dt / steps * 1e3
+    return {"ms_per_step": ms, "value": dev.world * n / (ms * 1e-3), "unit": "scalars/s",
+            "steps": steps, "upload_s": upload_s, "window_bits": c_bits, "windows": n_win,
+            "matches_headline_commitment": got == res,
+            "note": "qg_bases_upload: one table; value is never the headline"}
 
 
 def bench_msm_small(q, dev, args, barrier_sync, max_over_ranks, rank, world):

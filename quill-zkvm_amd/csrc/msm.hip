@@ -146,11 +146,13 @@ QG_DEV void msm_handover_check(uint32_t* hv, uint32_t w0, uint32_t nw, uint32_t 
 // Pass A histogram; also writes every scalar's canonical words (`canon`), so
 // the scatter pass reads them without a second Montgomery reduction.
 // hv != null: the scalars came from another stream (hand-over guard above)
-// wsel >= 0: only window wsel's digits (one-shot bases, msm_oneshot_local)
+// wsel >= 0: only window wsel's digits (one-shot bases, msm_oneshot_local);
+// canon_ready: `canon` already holds these scalars' canonical words (the
+// one-shot windows after the first), read instead of recomputed and rewritten
 __global__ void __launch_bounds__(SORT_BLOCK)
     k_sortA_hist(const Fr* __restrict__ scalars, size_t n, int c, int W, int LO, int H,
                  uint32_t nblk, uint32_t tile, uint32_t* __restrict__ hrow, Fr* __restrict__ canon,
-                 uint32_t* hv, uint32_t gen, int wsel) {
+                 uint32_t* hv, uint32_t gen, int wsel, int canon_ready) {
   extern __shared__ uint32_t hist[];
   msm_handover_check(hv, 0, 1, gen, 1u);
   for (int g = threadIdx.x; g < H; g += blockDim.x) hist[g] = 0;
@@ -160,8 +162,13 @@ __global__ void __launch_bounds__(SORT_BLOCK)
   const size_t end = base + tile < n ? base + tile : n;
   static_assert(SORT_TILE_MAX % SORT_BLOCK == 0, "pass-A tile must split evenly over the block");
   for (size_t i = base + threadIdx.x; i < end; i += blockDim.x) {
-    const Fr s = fr_canon29(scalars[i]);
-    canon[i] = s;
+    Fr s;
+    if (canon_ready) {
+      s = canon[i];
+    } else {
+      s = fr_canon29(scalars[i]);
+      canon[i] = s;
+    }
     for_each_digit(s, c, W, [&](int w, uint32_t b, bool) {
       if (wsel < 0 || w == wsel) atomicAdd(&hist[b >> LO], 1u);
     });
@@ -1333,6 +1340,11 @@ static qg_srs* srs_alloc(qg_ctx* ctx, size_t n, bool oneshot = false) {
   // balanced signed windows: W = ceil(255 / c_target), c = ceil(255 / W), so the
   // top window is not a sliver that funnels every scalar into a few buckets
   int ct = msm_window_bits(n);
+  // one-shot bases: every window is a bucket set of its own in the reduction
+  // (W x 2^(c-1) buckets), so the best c is smaller: 2^24 one-shot MSM 29.3 /
+  // 29.6 / 30.2 / 27.9 / 28.2 / 31.0 ms at c = 20 / 20 / 19 / 18 / 17 / 16
+  // (profiles/r06n_oneshot_c_sweep.txt)
+  if (oneshot) ct = std::min(ct, 18);
   if (const char* ov = getenv("QG_MSM_WINDOW_BITS")) ct = atoi(ov);  // tuning experiments
   QG_CHECK(ct >= 4 && ct <= 26, QG_ERR_INVALID, "MSM window bits out of range");
   srs->W = (255 + ct - 1) / ct;
@@ -1385,7 +1397,7 @@ static constexpr int MSM_MAX_BATCH = 1024;
 static MsmRun msm_accumulate_phase(qg_ctx* ctx, const qg_srs* srs, const Fr* d_scalars, size_t n,
                                    int slot, size_t srs_off = 0, hipStream_t bst = nullptr,
                                    bool reserve = false, uint32_t* hv = nullptr, uint32_t hgen = 0,
-                                   int wsel = -1) {
+                                   int wsel = -1, bool canon_ready = false) {
   QG_CHECK(srs_off <= srs->n && n <= srs->n - srs_off, QG_ERR_INVALID, "MSM length exceeds the SRS");
   MsmRun run;
   const std::string sfx = "#" + std::to_string(slot);
@@ -1521,7 +1533,8 @@ static MsmRun msm_accumulate_phase(qg_ctx* ctx, const qg_srs* srs, const Fr* d_s
       QgTimed tm(ctx, side ? "msm_bucketing_side" : "msm_bucketing", bst);
       // pass A: partition digits by the high bucket bits
       hipLaunchKernelGGL(k_sortA_hist, dim3(nblk), dim3(SORT_BLOCK), H * sizeof(uint32_t),
-                         bst, d_scalars, n, c, W, LO, H, nblk, tile, hrow, canon, hv, hgen, wsel);
+                         bst, d_scalars, n, c, W, LO, H, nblk, tile, hrow, canon, hv, hgen, wsel,
+                         canon_ready ? 1 : 0);
       QG_LAUNCH_CHECK();
       hipLaunchKernelGGL(k_transpose32, dim3(div_up(H, 32), div_up(nblk, 32)), dim3(256), 0,
                          bst, hrow, nblk, (uint32_t)H, ghist);
@@ -1853,8 +1866,10 @@ static std::vector<G1Affine> msm_finish_ranks_batch(qg_ctx* ctx, const std::vect
 static G1Xyzz msm_oneshot_local(qg_ctx* ctx, const qg_srs* srs, const Fr* d, size_t n) {
   if (n == 0) return G1Xyzz::infinity();
   std::vector<MsmRun> runs;
+  // all on ctx->stream: window w > 0 reads the canonical scalars window 0's
+  // pass A left in the (per-stream) canon scratch
   for (int w = 0; w < srs->W; w++)
-    runs.push_back(msm_accumulate_phase(ctx, srs, d, n, w, 0, nullptr, false, nullptr, 0, w));
+    runs.push_back(msm_accumulate_phase(ctx, srs, d, n, w, 0, nullptr, false, nullptr, 0, w, w > 0));
   std::vector<G1Xyzz> part;
   msm_reduce_phase(ctx, srs, runs, part);  // ends with a synchronization
   G1Xyzz acc = part[srs->W - 1];
