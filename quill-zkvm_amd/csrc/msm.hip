@@ -113,7 +113,10 @@ QG_DEV uint32_t xcd_tile(uint32_t b, uint32_t G) {
 static constexpr int SORT_BLOCK = 256;
 static constexpr int SORT_TILE_MAX = 1024;                  // scalars per block (pass A)
 static constexpr size_t SORT_LDS_A = 72 * 1024;             // LDS budget for staged entries (2 blocks/CU)
-static constexpr int SORT_CHUNK = 8192;                     // entries per block (pass B)
+#ifndef QG_SORT_CHUNK
+#define QG_SORT_CHUNK 8192
+#endif
+static constexpr int SORT_CHUNK = QG_SORT_CHUNK;            // entries per block (pass B)
 
 // ---- cross-stream hand-over guard (msm_device_batch) ----------------------
 // A batch on the side streams hands data over by events only: the scalars
