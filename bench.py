@@ -382,7 +382,7 @@ def main():
         dev.trace_marker(LEG_TAGS["msm_host"])
         out["msm_host_input"] = bench_msm_host(q, dev, args, barrier_sync, max_over_ranks, srs,
                                                scalars, ms_per_step, res)
-    if args.oneshot:
+    if args.oneshot and world == 1:  # a capability leg: one GPU only
         _progress(rank, "MSM over one-shot bases")
         dev.trace_marker(LEG_TAGS["msm_oneshot"])
         out["msm_oneshot"] = bench_msm_oneshot(q, dev, args, barrier_sync, max_over_ranks, srs,
