@@ -55,6 +55,28 @@ def test_sharded_msm(world):
     assert all(r == exp for r in run_ranks(world, fn))
 
 
+@pytest.mark.parametrize("world", [2, 4])
+def test_sharded_msm_oneshot_bases(world):
+    """each rank's shard of the bases uploaded one-shot (qg_bases_upload): the
+    window-by-window MSM's per-rank partials summed over the ranks"""
+    import quill_amd as q
+    rnd = random.Random(40 + world)
+    L = 3000
+    tau = rnd.randrange(R)
+    scal = [rnd.randrange(R) for _ in range(world * L)]
+    exp = o.g1_mul(o.G1_GEN, o.poly_eval(scal, tau))
+
+    def fn(dev, rank, world):
+        full = q.Srs.generate(dev, tau, L, offset=rank * L)
+        xy, inf = full.download_raw()
+        full.close()
+        one = q.Srs.upload_raw(dev, xy, inf, oneshot=True)
+        r = one.msm(scal[rank * L:(rank + 1) * L])
+        one.close()
+        return r
+    assert all(r == exp for r in run_ranks(world, fn))
+
+
 @pytest.mark.parametrize("world,nv_local", [(2, 9), (4, 6), (2, 1), (8, 5), (8, 1), (1, 9)])
 def test_sharded_sumcheck(world, nv_local):
     import quill_amd as q
