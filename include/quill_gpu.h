@@ -360,6 +360,27 @@ int qg_sumcheck_prove_dev(qg_ctx* ctx, uint32_t nvars, uint32_t ntables,
                           const uint64_t* consts, size_t nconsts, const uint64_t claimed_sum[4],
                           uint8_t state[32], uint64_t* round_coeffs, uint32_t* round_lens,
                           uint64_t* point, uint64_t evaluation[4]);
+/* The caller's transcript stays authoritative (the callback
+ * form of SumcheckProof::prove, sumcheck.rs:28-114, whose `transcript:
+ * &mut Transcript` is any implementation).  Per round j the library computes
+ * the trimmed coefficient-form message and calls
+ *   challenge(user, coeffs, len, out_r)
+ * with `len` coefficients (len x 4 uint64, arkworks' in-memory Montgomery
+ * limbs; len = 0 for an all-zero message); the callback appends the message
+ * to its transcript (append_serializable of the DensePolynomial,
+ * sumcheck.rs:80), draws r_j (draw_field_element, :82) and writes it to out_r
+ * (Montgomery limbs); a nonzero return aborts the prove (QG_ERR_INVALID).
+ * The caller appends num_vars and claimed_sum itself before the call
+ * (sumcheck.rs:35-36); `claimed_sum` is not absorbed here.  Device tables,
+ * any expression (the interpreted path; one host round trip per round), and
+ * on a sharded context every rank calls its own callback (the ranks' replicas
+ * must return the same r_j).  Outputs as qg_sumcheck_prove. */
+typedef int (*qg_challenge_fn)(void* user, const uint64_t* coeffs, uint32_t len, uint64_t out_r[4]);
+int qg_sumcheck_prove_cb(qg_ctx* ctx, uint32_t nvars, uint32_t ntables,
+                         const qg_buf* const* tables, const qg_expr_op* prog, size_t prog_len,
+                         const uint64_t* consts, size_t nconsts, qg_challenge_fn challenge,
+                         void* user, uint64_t* round_coeffs, uint32_t* round_lens,
+                         uint64_t* point, uint64_t evaluation[4]);
 
 /* ZeroCheckProof::prove (hyperplonk/src/piops/zerocheck.rs:14-49): draws
  * z (nvars challenges), builds eq(., z) on the device (eq_eval.rs:6-31),

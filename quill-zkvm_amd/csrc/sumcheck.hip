@@ -2395,12 +2395,20 @@ void expr_table_device(qg_ctx* ctx, size_t n, uint32_t ntables, const std::vecto
 // step; then every rank folds its block by r_{m-1} to one value per slot,
 // allgathers those W x K values (the rank is the high index bits) and runs the
 // last lw rounds redundantly on the gathered W-entry tables.
+// cb != nullptr (qg_sumcheck_prove_cb): the caller's transcript absorbs each
+// message and draws each challenge through the callback; `state` and
+// `claimed_sum` are unused (the caller absorbed num_vars and the claim)
+struct ScChallengeCb {
+  qg_challenge_fn fn;
+  void* user;
+};
+
 static void sumcheck_run_generic(qg_ctx* ctx, uint32_t nvars, uint32_t ntables,
                                  const std::vector<const Fr*>& d_tables, const qg_expr_op* prog,
                                  size_t prog_len, const uint64_t* consts, size_t nconsts,
                                  const uint64_t claimed_sum[4], uint8_t state[32],
                                  uint64_t* round_coeffs, uint32_t* round_lens, uint64_t* point,
-                                 uint64_t evaluation[4]) {
+                                 uint64_t evaluation[4], const ScChallengeCb* cb = nullptr) {
   const uint32_t world = (uint32_t)ctx->world;
   uint32_t lw = 0;
   while ((1u << lw) < world) lw++;
@@ -2443,7 +2451,7 @@ static void sumcheck_run_generic(qg_ctx* ctx, uint32_t nvars, uint32_t ntables,
   Fr* d_out = ctx->scratch_as<Fr>("gen_out", GEN_NPMAX);
   Fr* d_all = ctx->scratch_as<Fr>("gen_all", (size_t)world * std::max<size_t>(GEN_NPMAX, Ks));
   // transcript: append num_vars (usize) and claimed_sum (sumcheck.rs:35-36)
-  {
+  if (!cb) {
     uint8_t b8[8], b32[32];
     u64_to_bytes(nvars, b8);
     transcript_append(state, b8, 8);
@@ -2555,11 +2563,23 @@ static void sumcheck_run_generic(qg_ctx* ctx, uint32_t nvars, uint32_t ntables,
       co[t] = a;
       if (!a.is_zero()) len = t + 1;
     }
-    std::vector<uint8_t> msg(8 + 32 * (size_t)len);
-    u64_to_bytes(len, msg.data());
-    for (uint32_t t = 0; t < len; t++) fr_to_bytes(co[t], msg.data() + 8 + 32 * t);
-    transcript_append(state, msg.data(), msg.size());
-    r = transcript_draw_fr(state);
+    if (cb) {  // the caller's transcript: absorb the message, draw r_j
+      std::vector<uint64_t> cm(4 * (size_t)std::max<uint32_t>(len, 1), 0);
+      for (uint32_t t = 0; t < len; t++) fr_export(co[t], cm.data() + 4 * t);
+      uint64_t rr[4] = {0, 0, 0, 0};
+      QG_CHECK(cb->fn(cb->user, cm.data(), len, rr) == 0, QG_ERR_INVALID,
+               "sumcheck challenge callback failed");
+      r = fr_import(rr);
+      Fr rc = r;
+      reduce_once<FrP>(rc.v);
+      QG_CHECK(rc == r, QG_ERR_INVALID, "challenge callback returned a non-reduced Fr");
+    } else {
+      std::vector<uint8_t> msg(8 + 32 * (size_t)len);
+      u64_to_bytes(len, msg.data());
+      for (uint32_t t = 0; t < len; t++) fr_to_bytes(co[t], msg.data() + 8 + 32 * t);
+      transcript_append(state, msg.data(), msg.size());
+      r = transcript_draw_fr(state);
+    }
     for (uint32_t t = 0; t < width; t++)
       fr_export(t < len ? co[t] : Fr::zero(), round_coeffs + 4 * ((size_t)j * width + t));
     round_lens[j] = len;
@@ -2845,6 +2865,31 @@ int qg_sumcheck_prove_dev(qg_ctx* ctx, uint32_t nvars, uint32_t ntables,
     }
     sumcheck_run(ctx, nvars, ntables, d, prog, prog_len, consts, nconsts, claimed_sum, state,
                  round_coeffs, round_lens, point, evaluation);
+  });
+}
+
+int qg_sumcheck_prove_cb(qg_ctx* ctx, uint32_t nvars, uint32_t ntables,
+                         const qg_buf* const* tables, const qg_expr_op* prog, size_t prog_len,
+                         const uint64_t* consts, size_t nconsts, qg_challenge_fn challenge,
+                         void* user, uint64_t* round_coeffs, uint32_t* round_lens,
+                         uint64_t* point, uint64_t evaluation[4]) {
+  if (!ctx || (!tables && ntables) || !prog || !challenge || !round_coeffs || !round_lens ||
+      !point || !evaluation || (!consts && nconsts))
+    return QG_ERR_INVALID;
+  return qg_guard(ctx, [&] {
+    QG_CHECK(nvars >= 1 && nvars <= 34, QG_ERR_INVALID, "nvars out of range");
+    QG_HIP(hipSetDevice(ctx->device));
+    std::vector<const Fr*> d;
+    for (uint32_t i = 0; i < ntables; i++) {
+      QG_CHECK(tables[i] && tables[i]->n >= local_table_size(ctx, nvars), QG_ERR_INVALID,
+               "device table shorter than its (local) hypercube size");
+      d.push_back(tables[i]->d);
+    }
+    const ScChallengeCb cb{challenge, user};
+    const uint64_t zero[4] = {0, 0, 0, 0};
+    uint8_t unused[32] = {0};
+    sumcheck_run_generic(ctx, nvars, ntables, d, prog, prog_len, consts, nconsts, zero, unused,
+                         round_coeffs, round_lens, point, evaluation, &cb);
   });
 }
 

@@ -59,6 +59,9 @@ U64P = C.POINTER(C.c_uint64)
 U8P = C.POINTER(C.c_uint8)
 U32P = C.POINTER(C.c_uint32)
 SZ = C.c_size_t
+# qg_challenge_fn(user, coeffs, len, out_r): the caller's transcript (qg_sumcheck_prove_cb)
+CHALLENGE_FN = C.CFUNCTYPE(C.c_int, C.c_void_p, C.POINTER(C.c_uint64), C.c_uint32,
+                           C.POINTER(C.c_uint64))
 
 # name -> (restype, argtypes)
 PROTOTYPES = {
@@ -132,6 +135,9 @@ PROTOTYPES = {
     "qg_sumcheck_prove_dev": (C.c_int, [P, C.c_uint32, C.c_uint32, C.POINTER(P),
                                         C.POINTER(ExprOp), SZ, U64P, SZ, U64P, U8P, U64P, U32P,
                                         U64P, U64P]),
+    "qg_sumcheck_prove_cb": (C.c_int, [P, C.c_uint32, C.c_uint32, C.POINTER(P),
+                                       C.POINTER(ExprOp), SZ, U64P, SZ, CHALLENGE_FN, P, U64P,
+                                       U32P, U64P, U64P]),
     "qg_zerocheck_prove": (C.c_int, [P, C.c_uint32, C.c_uint32, C.POINTER(U64P),
                                      C.POINTER(ExprOp), SZ, U64P, SZ, U8P, U64P, U32P, U64P,
                                      U64P, U64P]),

@@ -348,6 +348,43 @@ def sumcheck_prove_device(dev: Device, num_vars: int, tables, expr: VirtualPolyE
     return coeffs, lens, point, ev
 
 
+def sumcheck_prove_callback(dev: Device, num_vars: int, tables, expr: VirtualPolyExpr,
+                            challenge):
+    """qg_sumcheck_prove_cb: the caller's transcript stays authoritative.
+    `challenge(coeffs) -> r` gets each round's trimmed message (list of Fr
+    ints) and returns r_j; the caller has absorbed num_vars and the claimed
+    sum beforehand (sumcheck.rs:35-36).  Tables are DeviceVec.  Returns
+    (r_polys, point, evaluation)."""
+    from ._lib import CHALLENGE_FN
+    from .field import fr_from_mont_limbs, fr_to_mont_limbs
+    prog, plen, carr, nc = _program_c(expr)
+    width = expr_degree(expr) + 1
+    ptrs = (C.c_void_p * len(tables))(*[t.h for t in tables])
+    coeffs = np.zeros((num_vars * width, 4), dtype=np.uint64)
+    lens = np.zeros(num_vars, dtype=np.uint32)
+    point = np.zeros((num_vars, 4), dtype=np.uint64)
+    ev = (C.c_uint64 * 4)()
+    errors = []
+
+    def _cb(_user, cptr, n, out):
+        try:
+            msg = [fr_from_mont_limbs([cptr[4 * i + k] for k in range(4)]) for i in range(n)]
+            limbs = fr_to_mont_limbs(int(challenge(msg)))
+            for k in range(4):
+                out[k] = limbs[k]
+            return 0
+        except Exception as e:  # reported after the call
+            errors.append(e)
+            return 1
+    fn = CHALLENGE_FN(_cb)
+    rc = lib().qg_sumcheck_prove_cb(dev.h, num_vars, len(tables), ptrs, prog, plen, u64p(carr),
+                                    nc, fn, None, u64p(coeffs), u32p(lens), u64p(point), ev)
+    if errors:
+        raise errors[0]
+    check(rc, dev.h)
+    return _unpack(num_vars, width, coeffs, lens, point, ev)
+
+
 _DEV = None
 
 
