@@ -181,6 +181,14 @@ int qg_msm_g1(qg_ctx* ctx, const qg_srs* srs, const uint64_t* scalars, size_t n,
               uint64_t out_xy[8], uint8_t* out_inf);
 int qg_msm_g1_dev(qg_ctx* ctx, const qg_srs* srs, const qg_buf* scalars, size_t n,
                   uint64_t out_xy[8], uint8_t* out_inf);
+/* msm_unchecked over the base slice srs[offset..] (SURVEY 8(b)'s `offset`):
+ * sum of scalars[i] * srs[offset + i] over i < min(n, qg_srs_len - offset),
+ * truncated like msm_unchecked; QG_ERR_INVALID when offset > qg_srs_len.
+ * Host (`_at`) and device-resident (`_dev_at`) scalars. */
+int qg_msm_g1_at(qg_ctx* ctx, const qg_srs* srs, size_t offset, const uint64_t* scalars,
+                 size_t n, uint64_t out_xy[8], uint8_t* out_inf);
+int qg_msm_g1_dev_at(qg_ctx* ctx, const qg_srs* srs, size_t offset, const qg_buf* scalars,
+                     size_t n, uint64_t out_xy[8], uint8_t* out_inf);
 /* k MSMs over one SRS in one call (at most 1024): out_xy[8 i ..], out_inf[i]
  * for scalars[i] (first ns[i] entries), each equal to qg_msm_g1_dev of it.
  * They run as one MSM batch (bucketing beside the previous MSM's accumulation

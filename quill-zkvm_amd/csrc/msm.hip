@@ -1866,13 +1866,15 @@ static std::vector<G1Affine> msm_finish_ranks_batch(qg_ctx* ctx, const std::vect
 // SRS pays once (k_srs_shift, 0.63 s at 2^24), so a caller of msm_unchecked
 // with bases it uses once (ark-ec's VariableBaseMSM::msm_unchecked, kzg.rs:72)
 // need not build 13 tables for one MSM.
-static G1Xyzz msm_oneshot_local(qg_ctx* ctx, const qg_srs* srs, const Fr* d, size_t n) {
+static G1Xyzz msm_oneshot_local(qg_ctx* ctx, const qg_srs* srs, const Fr* d, size_t n,
+                                size_t srs_off = 0) {
   if (n == 0) return G1Xyzz::infinity();
   std::vector<MsmRun> runs;
   // all on ctx->stream: window w > 0 reads the canonical scalars window 0's
   // pass A left in the (per-stream) canon scratch
   for (int w = 0; w < srs->W; w++)
-    runs.push_back(msm_accumulate_phase(ctx, srs, d, n, w, 0, nullptr, false, nullptr, 0, w, w > 0));
+    runs.push_back(
+        msm_accumulate_phase(ctx, srs, d, n, w, srs_off, nullptr, false, nullptr, 0, w, w > 0));
   std::vector<G1Xyzz> part;
   msm_reduce_phase(ctx, srs, runs, part);  // ends with a synchronization
   G1Xyzz acc = part[srs->W - 1];
@@ -2031,6 +2033,22 @@ static G1Affine msm_host(qg_ctx* ctx, const qg_srs* srs, const uint64_t* h, size
 
 G1Affine msm_device(qg_ctx* ctx, const qg_srs* srs, const Fr* d_scalars, size_t n) {
   return msm_device_batch(ctx, srs, {d_scalars}, {n})[0];
+}
+
+// msm_unchecked over the base slice srs[off..] (qg_msm_g1_at / _dev_at): the
+// entries point at rows off + i of each table (msm_accumulate_phase srs_off)
+static G1Affine msm_device_at(qg_ctx* ctx, const qg_srs* srs, const Fr* d, size_t n, size_t off) {
+  if (off == 0) return msm_device(ctx, srs, d, n);
+  G1Xyzz acc = G1Xyzz::infinity();
+  if (srs->tables != srs->W) {
+    acc = msm_oneshot_local(ctx, srs, d, n, off);
+  } else if (n > 0) {
+    std::vector<MsmRun> runs{msm_accumulate_phase(ctx, srs, d, n, 0, off)};
+    std::vector<G1Xyzz> part;
+    msm_reduce_phase(ctx, srs, runs, part);  // ends with a synchronization
+    acc = part[0];
+  }
+  return msm_finish_ranks(ctx, acc);
 }
 
 // dependent Fq multiply chains: 8 independent chains per thread, ITER steps
@@ -2284,6 +2302,29 @@ int qg_msm_g1_dev(qg_ctx* ctx, const qg_srs* srs, const qg_buf* scalars, size_t 
     QG_HIP(hipSetDevice(ctx->device));
     G1Affine r = msm_device(ctx, srs, scalars->d, n);
     g1_export(r, out_xy, out_inf);
+  });
+}
+
+int qg_msm_g1_dev_at(qg_ctx* ctx, const qg_srs* srs, size_t offset, const qg_buf* scalars,
+                     size_t n, uint64_t out_xy[8], uint8_t* out_inf) {
+  if (!ctx || !srs || !scalars || !out_xy || n > scalars->n || offset > srs->n)
+    return QG_ERR_INVALID;
+  return qg_guard(ctx, [&] {
+    QG_HIP(hipSetDevice(ctx->device));
+    const size_t m = std::min(n, srs->n - offset);  // msm_unchecked truncation
+    g1_export(msm_device_at(ctx, srs, scalars->d, m, offset), out_xy, out_inf);
+  });
+}
+
+int qg_msm_g1_at(qg_ctx* ctx, const qg_srs* srs, size_t offset, const uint64_t* scalars,
+                 size_t n, uint64_t out_xy[8], uint8_t* out_inf) {
+  if (!ctx || !srs || (!scalars && n) || !out_xy || offset > srs->n) return QG_ERR_INVALID;
+  return qg_guard(ctx, [&] {
+    QG_HIP(hipSetDevice(ctx->device));
+    const size_t m = std::min(n, srs->n - offset);
+    Fr* d = ctx->scratch_as<Fr>("msm_scalars", m ? m : 1);
+    fr_upload(ctx, d, scalars, m);
+    g1_export(msm_device_at(ctx, srs, d, m, offset), out_xy, out_inf);
   });
 }
 

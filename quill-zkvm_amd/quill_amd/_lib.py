@@ -107,6 +107,8 @@ PROTOTYPES = {
     "qg_buf_first_mismatch": (C.c_int, [P, SZ, P, SZ, SZ, C.POINTER(C.c_int64)]),
     "qg_msm_g1": (C.c_int, [P, P, U64P, SZ, U64P, U8P]),
     "qg_msm_g1_dev": (C.c_int, [P, P, P, SZ, U64P, U8P]),
+    "qg_msm_g1_at": (C.c_int, [P, P, SZ, U64P, SZ, U64P, U8P]),
+    "qg_msm_g1_dev_at": (C.c_int, [P, P, SZ, P, SZ, U64P, U8P]),
     "qg_msm_g1_dev_batch": (C.c_int, [P, P, C.POINTER(P), C.POINTER(SZ), SZ,
                                       C.POINTER(C.c_uint64), C.POINTER(C.c_uint8)]),
     "qg_kzg_commit": (C.c_int, [P, P, U64P, SZ, U64P, U8P]),

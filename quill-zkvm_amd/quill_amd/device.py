@@ -351,11 +351,25 @@ class Srs:
         check(lib().qg_kzg_commit(self.dev.h, self.h, u64p(arr), n, xy, C.byref(inf)), self.dev.h)
         return g1_from_abi(xy, inf.value)
 
-    def msm_dev(self, vec: DeviceVec, n=None):
+    def msm_dev(self, vec: DeviceVec, n=None, offset: int = 0):
+        """msm_unchecked(bases[offset..], vec[..n]) (qg_msm_g1_dev[_at])"""
         n = vec.n if n is None else n
         xy = (C.c_uint64 * 8)()
         inf = C.c_uint8()
-        check(lib().qg_msm_g1_dev(self.dev.h, self.h, vec.h, n, xy, C.byref(inf)), self.dev.h)
+        if offset:
+            rc = lib().qg_msm_g1_dev_at(self.dev.h, self.h, offset, vec.h, n, xy, C.byref(inf))
+        else:
+            rc = lib().qg_msm_g1_dev(self.dev.h, self.h, vec.h, n, xy, C.byref(inf))
+        check(rc, self.dev.h)
+        return g1_from_abi(xy, inf.value)
+
+    def msm_at(self, offset: int, scalars):
+        """msm_unchecked(bases[offset..], scalars) from host scalars (qg_msm_g1_at)"""
+        arr = fr_array(scalars) if len(scalars) else np.zeros((1, 4), dtype=np.uint64)
+        xy = (C.c_uint64 * 8)()
+        inf = C.c_uint8()
+        check(lib().qg_msm_g1_at(self.dev.h, self.h, offset, u64p(arr), len(scalars), xy,
+                                 C.byref(inf)), self.dev.h)
         return g1_from_abi(xy, inf.value)
 
     def msm_dev_batch(self, vecs, ns=None) -> list:

@@ -77,3 +77,37 @@ def test_oneshot_equals_srs_tables_and_trapdoor(dev, logn):
     v.close()
     one.close()
     full.close()
+
+
+@pytest.mark.parametrize("oneshot", [False, True])
+def test_msm_at_offset_matches_trapdoor(dev, oneshot):
+    """msm_unchecked(bases[offset..], scalars) (qg_msm_g1_at / _dev_at):
+    [sum s_i tau^(offset+i)] g, truncated at the end of the bases; offset 0 is
+    the plain MSM, offset = len gives infinity, offset > len is rejected"""
+    import oracle_c as oc
+    import quill_amd as q
+    from quill_amd import Srs
+    from quill_amd._lib import QuillGpuError
+    n = 5000
+    tau = 0x0FF5E7 + int(oneshot)
+    full = Srs.generate(dev, tau, n)
+    srs = full
+    if oneshot:
+        xy, inf = full.download_raw()
+        srs = Srs.upload_raw(dev, xy, inf, oneshot=True)
+    rnd = random.Random(7 + int(oneshot))
+    v = q.DeviceVec(dev, 4096).fill_random(55 + int(oneshot))
+    sc = v.to_list()
+    for off, m in ((0, 4096), (1, 4096), (903, 3000), (4000, 4096), (4999, 17), (n, 10)):
+        k = min(m, n - off)
+        want = oc.g1_mul(o.G1_GEN, oc.fr_horner(v.to_numpy(k), tau) * pow(tau, off, R) % R) if k else None
+        assert srs.msm_dev(v, m, offset=off) == want, (off, m)
+        assert srs.msm_at(off, sc[:m]) == want, (off, m)
+    small = [rnd.randrange(R) for _ in range(3)]
+    assert srs.msm_at(2, small) == o.g1_mul(o.G1_GEN, sum(s * pow(tau, 2 + i, R) for i, s in enumerate(small)) % R)
+    with pytest.raises(QuillGpuError):
+        srs.msm_at(n + 1, small)
+    v.close()
+    if oneshot:
+        srs.close()
+    full.close()
