@@ -90,7 +90,7 @@ SC_KERNELS = ("k_sc_big", "k_sc_round", "k_sc_persist", "k_sc_finish", "k_sc_sli
 LEG_TAGS = {"msm_2p24": 1, "sumcheck": 2, "msm_host": 3, "scaling": 4, "mle_open": 5, "logup": 6,
             "hyperplonk": 7, "msm_2p20": 8, "cpu_baseline": 9, "probe_msm": 10,
             "probe_sumcheck": 11, "probe_logup": 12, "probe_mle": 13, "probe_cal": 14,
-            "msm_oneshot": 15}
+            "msm_oneshot": 15, "zerocheck": 16}
 
 
 def traffic_probe(args):
@@ -373,6 +373,9 @@ def main():
             tot = sum((traffic[k]["read_bytes_per_launch"] + traffic[k]["write_bytes_per_launch"])
                       * traffic[k]["launches"] for k in SC_KERNELS if k in traffic)
             out["sumcheck"]["roofline"]["traffic"] = tot
+        _progress(rank, "zero-check")
+        dev.trace_marker(LEG_TAGS["zerocheck"])
+        out["zerocheck"] = bench_zerocheck(q, dev, args, barrier_sync, max_over_ranks, rank)
     if args.log_msm_small > 0:
         _progress(rank, f"MSM 2^{args.log_msm_small} (config 2)")
         dev.trace_marker(LEG_TAGS["msm_2p20"])
@@ -443,6 +446,7 @@ _DROP_KEYS = {"note", "traffic_note", "frac_note", "issue_bound_note", "identity
               "spans_ms_rank0"}
 # sections dropped (in this order) if the line is still over budget
 _SHED_ORDER = ("kernels_ms", "sumcheck_weak_scaling", "msm_strong_scaling", "msm_oneshot",
+               "zerocheck",
                "msm_host_input",
                "logup", "mle_open", "hyperplonk", "hbm_by_kernel")
 
@@ -696,6 +700,36 @@ def bench_sumcheck(q, dev, args, barrier_sync, max_over_ranks, rank, weak=False)
             "round_kernels_ms_per_call": rk_ms / max(args.steps, 1),
             "tail_kernel_ms_per_call": tl_ms / max(args.steps, 1),
             "ms_with_kernel_timing": ms_timed}
+
+
+def bench_zerocheck(q, dev, args, barrier_sync, max_over_ranks, rank):
+    """SURVEY 8(d) C3's variant: ZeroCheckProof::prove (zerocheck.rs:14-49) at
+    2^log-sumcheck variables, h = g1*g2 - g3 (k = 4 tables with eq, degree 3 after
+    x eq): z drawn, eq(., z) built on the device, the sumcheck of h*eq.  Sharded
+    like the sumcheck leg (strong: one 2^n prove over the ranks)."""
+    from quill_amd import VirtualPolyExpr as E
+    from quill_amd.hyperplonk import zerocheck_prove_device
+    world = dev.world
+    nv = args.log_sumcheck
+    N = (1 << nv) // world
+    tabs = [q.DeviceVec(dev, N).fill_random(0x5155494C4C + 13 + 7 * i + 100 * rank)
+            for i in range(3)]
+    expr = E.Input(0) * E.Input(1) - E.Input(2)
+    for _ in range(args.warmup):
+        zerocheck_prove_device(dev, nv, tabs, expr, q.Transcript(b"zerocheck_bench"))
+    barrier_sync()
+    t0 = time.perf_counter()
+    for _ in range(args.steps):
+        zerocheck_prove_device(dev, nv, tabs, expr, q.Transcript(b"zerocheck_bench"))
+    barrier_sync()
+    ms = max_over_ranks(time.perf_counter() - t0) / args.steps * 1e3
+    for t in tabs:
+        t.close()
+    return {"metric": f"zero-check prover ms at 2^{nv} vars (h = g1*g2 - g3, x eq)", "ms": ms,
+            "higher_is_better": False,
+            "parallelism": f"sharded x{world} (strong scaling)" if world > 1 else "single GPU",
+            "note": "random tables (the prover's work does not depend on h vanishing); "
+                    "includes the eq table and the z draws"}
 
 
 def bench_mle(q, dev, args, barrier_sync, max_over_ranks, rank=0, world=1):

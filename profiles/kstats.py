@@ -18,7 +18,8 @@ import sys
 # script runs without importing the bench)
 LEGS = {1: "msm_2p24", 2: "sumcheck", 3: "msm_host", 4: "scaling", 5: "mle_open", 6: "logup",
         7: "hyperplonk", 8: "msm_2p20", 9: "cpu_baseline", 10: "probe_msm", 11: "probe_sumcheck",
-        12: "probe_logup", 13: "probe_mle", 14: "probe_cal", 15: "msm_oneshot"}
+        12: "probe_logup", 13: "probe_mle", 14: "probe_cal", 15: "msm_oneshot",
+        16: "zerocheck"}
 MARKER = "k_trace_marker"
 
 

@@ -348,6 +348,24 @@ def sumcheck_prove_device(dev: Device, num_vars: int, tables, expr: VirtualPolyE
     return coeffs, lens, point, ev
 
 
+def zerocheck_prove_device(dev: Device, num_vars: int, tables, expr: VirtualPolyExpr,
+                           transcript: Transcript):
+    """qg_zerocheck_prove_dev on DeviceVec tables (the bench's zero-check
+    variant): returns the raw (coeffs, lens, point, ev) like
+    sumcheck_prove_device, round messages of degree(expr) + 1."""
+    prog, plen, carr, nc = _program_c(expr)
+    width = expr_degree(expr) + 2
+    ptrs = (C.c_void_p * len(tables))(*[t.h for t in tables])
+    coeffs = np.zeros((num_vars * width, 4), dtype=np.uint64)
+    lens = np.zeros(num_vars, dtype=np.uint32)
+    point = np.zeros((num_vars, 4), dtype=np.uint64)
+    ev = (C.c_uint64 * 4)()
+    check(lib().qg_zerocheck_prove_dev(
+        dev.h, num_vars, len(tables), ptrs, prog, plen, u64p(carr), nc, transcript.c_state(),
+        u64p(coeffs), u32p(lens), u64p(point), ev), dev.h)
+    return coeffs, lens, point, ev
+
+
 def sumcheck_prove_callback(dev: Device, num_vars: int, tables, expr: VirtualPolyExpr,
                             challenge):
     """qg_sumcheck_prove_cb: the caller's transcript stays authoritative.
