@@ -112,6 +112,18 @@ def test_invalid_arguments_return_status(L):
     out = (C.c_uint8 * 65)()
     assert L.qg_transcript_draw(st, out, 65) == -1  # > 64 bytes
     assert L.qg_ctx_create(0, None) == -1
+    # round-6 entry points: null handles / callbacks are rejected before any
+    # device work (QG_ERR_INVALID)
+    h = C.c_void_p()
+    xy = (C.c_uint64 * 8)()
+    inf = C.c_uint8()
+    assert L.qg_bases_upload(None, xy, None, 1, C.byref(h)) == -1
+    assert L.qg_msm_g1_at(None, None, 0, None, 0, xy, C.byref(inf)) == -1
+    assert L.qg_msm_g1_dev_at(None, None, 0, None, 0, xy, C.byref(inf)) == -1
+    assert L.qg_msm_g1_dev_batch(None, None, None, None, 0, None, None) == -1
+    assert L.qg_sumcheck_prove_cb(None, 1, 0, None, prog, 1, None, 0, C.cast(None, L.qg_sumcheck_prove_cb.argtypes[8]),
+                                  None, None, None, None, None) == -1
+    assert L.qg_ctx_phase_split(None, None, 0, None) == -1
 
 
 def test_no_device_is_an_error_not_a_fallback():
