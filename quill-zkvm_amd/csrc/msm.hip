@@ -196,24 +196,29 @@ __global__ void __launch_bounds__(256)
 }
 
 // Block-local exclusive scan of n <= 4 * SORT_BLOCK counts in LDS (in place).
-__device__ void lds_exscan(uint32_t* a, int n, uint32_t* tmp /* SORT_BLOCK words */) {
+// Each thread owns `per` consecutive counts; the thread totals are scanned
+// within the wave by shuffles, the 4 wave totals through LDS: two barriers
+// (a Hillis-Steele scan over the block took 2 x 8).
+__device__ void lds_exscan(uint32_t* a, int n, uint32_t* tmp /* >= SORT_BLOCK / 64 words */) {
   const int per = (n + SORT_BLOCK - 1) / SORT_BLOCK;
   const int b = threadIdx.x * per;
+  const int lane = threadIdx.x & 63, wid = threadIdx.x >> 6;
   uint32_t tot = 0;
   for (int k = 0; k < per; k++)
     if (b + k < n) tot += a[b + k];
-  tmp[threadIdx.x] = tot;
-  __syncthreads();
-  for (int off = 1; off < SORT_BLOCK; off <<= 1) {
-    uint32_t add = threadIdx.x >= (unsigned)off ? tmp[threadIdx.x - off] : 0u;
-    __syncthreads();
-    tmp[threadIdx.x] += add;
-    __syncthreads();
+  uint32_t inc = tot;
+#pragma unroll
+  for (int d = 1; d < 64; d <<= 1) {
+    const uint32_t y = __shfl_up(inc, d, 64);
+    if (lane >= d) inc += y;
   }
-  uint32_t run = tmp[threadIdx.x] - tot;
+  if (lane == 63) tmp[wid] = inc;
+  __syncthreads();
+  uint32_t run = inc - tot;
+  for (int w = 0; w < wid; w++) run += tmp[w];
   for (int k = 0; k < per; k++) {
     if (b + k < n) {
-      uint32_t v = a[b + k];
+      const uint32_t v = a[b + k];
       a[b + k] = run;
       run += v;
     }
