@@ -142,3 +142,69 @@ def test_rccl_logup_matches_single(rdev, dev):
         for tb in tabs + [out]:
             tb.close()
     assert res[0] == res[1]
+
+
+def test_rccl_msm_dev_batch_matches_single(rdev, dev):
+    """msm_finish_ranks_batch at world 1: one ncclAllGather of a batch's k
+    partials (round 6); equal to the single-context batch"""
+    import quill_amd as q
+    tau = 0x5CA1AB1E
+    ns = [1 << 14, 1000, 0, (1 << 13) + 5]
+    out = []
+    for d in (dev, rdev):
+        srs = q.Srs.generate(d, tau, 1 << 14)
+        vs = [q.DeviceVec(d, 1 << 14).fill_random(31 + i) for i in range(len(ns))]
+        out.append(srs.msm_dev_batch(vs, ns))
+        for v in vs:
+            v.close()
+        srs.close()
+    assert out[0] == out[1]
+
+
+def test_rccl_mle_open_batch_matches_single(rdev, dev):
+    """mle_open_batch_sharded at world 1 (round 6: four exchanges per batch over
+    ncclAllGather / grouped send-recv): the proofs and transcript state of the
+    single-context batch, items of one local length incl. a zero tail"""
+    import quill_amd as q
+    from quill_amd import KZG, Transcript
+    rnd = random.Random(66)
+    nv = 12
+    N = 1 << nv
+    tau = rnd.randrange(R)
+    polys = [[rnd.randrange(R) for _ in range(N)] for _ in range(3)]
+    polys[1] = polys[1][:N - 700] + [0] * 700
+    items = [(0, [rnd.randrange(R) for _ in range(nv)]), (1, [rnd.randrange(R) for _ in range(nv)]),
+             (2, [rnd.randrange(R) for _ in range(nv)]), (0, [rnd.randrange(R) for _ in range(nv)])]
+    res = []
+    for d in (dev, rdev):
+        kzg = KZG.trusted_setup(N, tau, d)
+        vs = [q.DeviceVec.from_list(d, p) for p in polys]
+        t = Transcript(b"rccl-open-batch")
+        res.append((kzg.open_batch_dev([(vs[i], N, pt, False) for i, pt in items], t), t.state))
+        for v in vs:
+            v.close()
+        kzg.close()
+    assert res[0] == res[1]
+
+
+def test_rccl_hyperplonk_matches_oracle(rdev):
+    """HyperPlonk::prove (proof.rs:239-301) on the forced one-rank RCCL context:
+    the sharded prover end to end (full-witness exchange, sharded commitments
+    and commitment batches, zero-checks, Logup, batched sharded openings) over
+    the real RCCL transport; the proof equals the oracle prover's field by
+    field with the same transcript state"""
+    import quill_amd as q
+    from quill_amd import examples as ex
+    from test_gpu_hyperplonk import TAU, _oracle_setup, assert_same_proof
+    rows, which = 64, ("fib", "mod")
+    opcs, ohp, ows = _oracle_setup(rows, which)
+    oproof, ot = ohp.prove(opcs, ows)
+    b = {"fib": ex.fibonacci_circuit_and_trace, "mod": ex.modified_fibonacci_circuit_and_trace}
+    cws = [b[w](rows) for w in which]
+    maxdeg = max(c.num_cols() * c.num_rows() for c, _ in cws)
+    pcs = q.KZG.trusted_setup(maxdeg, TAU, rdev)
+    hp = q.HyperPlonk.preprocess([c for c, _ in cws], pcs)
+    proof = hp.prove(pcs, [w for _, w in cws])
+    pcs.close()
+    assert_same_proof(proof, oproof)
+    assert hp.last_transcript.state == ot.state
